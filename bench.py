@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric on MI355X:
+"fp32->int32 quantize+pack GB/s (device-resident), 256 MiB bucket, 1/2/4/8 GPU".
+
+One step = one pass of the hot path (CpuExponentQuantizerPPP's
+PreprocessSingle over a whole job slice: per-packet exponent, fp32->int32
+scale+round, big-endian pack — ppp.cc:69-156) over one 256 MiB fp32 bucket
+that is already resident in HBM, as one launch of the fused HIP kernel
+sml_quantize_pack (K1).  Exponents are the loopback's (the dummy backend
+returns them unchanged, so the local exponent is the global one: W = 1).
+
+Multi-GPU (launched by torch.distributed.run): "sharding mode" — every rank
+owns its own 256 MiB slice of a G x 256 MiB job (FifoScheduler slicing,
+fifo_scheduler.cc:93-109, slice g -> GPU g); the path has no exchange step
+at W = 1, so there is no collective in the timed region (weak scaling).
+value = all ranks' algorithmic bytes / max-over-ranks time.
+
+Units: value / roofline.achieved = ALGORITHMIC bytes per second: 4N read
+(fp32 in) + 4N written (int32 payload) + B written (int8 exponents),
+B = N/256 — see DESIGN.md §4.  input_GBps = 4N / t is reported alongside.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--numel", type=int, default=64 * 1024 * 1024, help="fp32 elements per GPU (256 MiB)")
+    ap.add_argument("--packet-numel", type=int, default=256)
+    ap.add_argument("--grid-limit", type=int, default=0, help="workgroups per launch (0 = one per 4 tiles)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--extra", action="store_true", help="also time dequantize / fused round trip / copy")
+    return ap.parse_args()
+
+
+def load_traffic(numel, P):
+    """HBM bytes per launch from the PMC passes (profiles/pmc_traffic.json,
+    written by profiles/collect_pmc.py from separate rocprofv3 --pmc runs)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d.get("quantize_pack", {})
+        if k.get("numel") == numel and k.get("packet_numel") == P:
+            return k.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(numel, P, budget_s):
+    """The oracle's restatement of the reference CPU path (per-packet
+    PreprocessSingle calls in DummyWorkerThread order, b = mop/T ring) on this
+    host's cores, over the same 256 MiB bucket, repeated for ~budget_s."""
+    import numpy as np
+    from oracle import oracle as O
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    cores = max(1, min(cores, 16))
+    x = O.splitmix_normal(42, numel)
+    out = np.empty_like(x)
+    alg = 8 * numel + O.num_blocks(numel, P)
+
+    def run(T, deadline_s, min_reps):
+        rates, t_end, reps = [], time.perf_counter() + deadline_s, 0
+        while reps < min_reps or time.perf_counter() < t_end:
+            t0 = time.perf_counter()
+            O.dummy_allreduce(x, P=P, max_outstanding_packets=256, num_worker_threads=T,
+                              num_workers=1, threaded=T > 1, mode=O.MODE_PREPROCESS, out=out)
+            rates.append(alg / (time.perf_counter() - t0) / 1e9)
+            reps += 1
+        return float(np.median(rates)), reps
+
+    single, reps1 = run(1, budget_s * 0.35, 2)
+    multi, repsT = run(cores, budget_s * 0.65, 3)
+    return {
+        "value": round(multi, 3),
+        "unit": "GB/s (8N+B algorithmic bytes, same as value)",
+        "cores": cores,
+        "kind": "port",
+        "sample": (f"oracle/sml_oracle.c restatement of CpuExponentQuantizerPPP (VCL=0) driven in "
+                   f"DummyWorkerThread order, PreprocessSingle only (exponent + quantize + BE pack into "
+                   f"the b-packet ring), the full {numel * 4 >> 20} MiB bucket, packet_numel {P}, "
+                   f"max_outstanding_packets 256; {cores} worker threads x {repsT} reps (median); "
+                   f"1 thread: {single:.3f} GB/s over {reps1} reps"),
+        "single_thread_value": round(single, 3),
+        "input_GBps": round(multi * 4 * numel / alg, 3),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import switchml_amd as sw
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    sw.lib()
+    if args.grid_limit:
+        sw.set_grid_limit(args.grid_limit)
+
+    N, P = args.numel, args.packet_numel
+    B = sw.num_blocks(N, P)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(42 + rank)
+    x = torch.randn(N, dtype=torch.float32, device=dev, generator=gen)
+    payload = torch.empty(B * P, dtype=torch.int32, device=dev)
+    exps = torch.empty(B, dtype=torch.int8, device=dev)
+    stream = torch.cuda.current_stream()
+    alg_bytes = 8 * N + B
+
+    def step():
+        sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # kernel-duration events on the launch stream (torch.cuda.Event records on `stream`)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms_max = float(t[0]), float(t[1])
+
+    # sanity: the timed output is the HIP kernel's and it is deterministic
+    ok = bool(torch.equal(exps[:4].cpu(), sw.exponents(x[:4 * P], P).cpu()))
+
+    extra = {}
+    if args.extra and rank == 0:
+        extra = extra_measurements(sw, torch, x, payload, exps, N, P, stream)
+
+    if rank == 0:
+        ms_per_step = elapsed * 1e3 / args.steps
+        value = world * alg_bytes / (elapsed / args.steps) / 1e9
+        achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
+        line = {
+            "metric": "fp32→int32 quantize+pack GB/s (device-resident), 256 MiB bucket, 1/2/4/8 GPU",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32->i32",
+            "data": "synthetic N(0,1) fp32 (torch.randn on device, seed 42+rank)",
+            "config": {
+                "workload": "configs[2]-sized bucket: 256 MiB fp32 per GPU, fused exponent+quantize+BE pack "
+                            "(sml_quantize_pack, K1), loopback exponents (W=1)",
+                "numel_per_gpu": N,
+                "packet_numel": P,
+                "num_blocks_per_gpu": B,
+                "parallelism": f"shard{world} (FIFO slices, no data-path collective)",
+                "bytes_per_step_per_gpu": alg_bytes,
+            },
+            "input_GBps": round(world * 4 * N / (elapsed / args.steps) / 1e9, 2),
+            "kernel_ms": round(kern_ms_max, 5),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": load_traffic(N, P),
+                "kernel": f"sml::k_quantize_pack<{P},aligned,fused,BE,half-away>",
+            },
+            "self_check": ok,
+        }
+        if extra:
+            line["extra"] = extra
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(N, P, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
+    """Side measurements (not the headline): dequantize, fused loopback round
+    trip, and a plain device copy as the practical HBM ceiling."""
+    out = torch.empty_like(x)
+    res = {}
+
+    def timeit(fn):
+        for _ in range(3):
+            fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            fn()
+        b.record(stream)
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps * 1e-3
+
+    B = exps.numel()
+    t = timeit(lambda: sw.dequantize(payload, exps, N, P, 1, out=out, stream=stream))
+    res["dequantize_GBps"] = round((8 * N + B) / t / 1e9, 1)
+    t = timeit(lambda: sw.roundtrip_loopback(x, P, 1, out=out, stream=stream))
+    res["roundtrip_fused_GBps"] = round(8 * N / t / 1e9, 1)
+    t = timeit(lambda: out.copy_(x))
+    res["copy_GBps"] = round(8 * N / t / 1e9, 1)
+    return res
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+/*
+ * switchml_hip.h — C-ABI of the MI355X-native SwitchML end-host
+ * pre/post-processor (exponent quantizer) and its loopback/switch helpers.
+ *
+ * This is the drop-in boundary for the hot path of SwitchML's client_lib:
+ * what `CpuExponentQuantizerPPP` (client_lib/src/prepostprocessors/
+ * cpu_exponent_quantizer_ppp.{h,cc}) does one 1 KiB LTU at a time on the
+ * CPU, these entry points do for a whole job slice at once on the GPU — the
+ * "bulk" hooks the reference reserved in prepostprocessor.h:112-116.
+ *
+ * Conventions
+ *  - plain C types only; every pointer argument named d_* is DEVICE memory
+ *    (hipMalloc / torch CUDA tensor); `stream` is a hipStream_t passed as
+ *    void* (NULL = the legacy default stream).  Calls are asynchronous on
+ *    that stream, like every HIP launch.
+ *  - no exceptions cross this ABI; every entry point returns sml_status_t.
+ *    The reference aborts with LOG(FATAL) on a bad data type / PPP name
+ *    (ppp.cc:190,297; prepostprocessor.cc:39); here that is an error code.
+ *  - "job slice" = one contiguous run of `numel` elements, exactly what a
+ *    worker thread receives from FifoScheduler::GetJobSlice
+ *    (schedulers/fifo_scheduler.cc:93-109).  Blocks (LTUs) restart at the
+ *    slice start.  Block k covers elements [k*P, min((k+1)*P, numel)).
+ *  - planes: the per-packet exponent plane `exps[B]` (int8, byte 0 of the
+ *    reference's 2-byte extra-info slot) and the payload plane `payload[B*P]`
+ *    (int32, big-endian by default = the packet's wire bytes).  Packet p of
+ *    the reference's stream carries exps[p] (p < B) and payload block p-b
+ *    (p >= b); see DESIGN.md §2 and SURVEY.md §8 A6.  Payload words of the
+ *    last, partial block past `numel` are written as 0 (the reference
+ *    leaves stale ring bytes there).
+ *  - B = sml_num_blocks(numel, P) = ceil(numel / P)   (ppp.cc:56-57)
+ *
+ * All file:line citations are relative to /root/reference/dev_root/.
+ */
+#ifndef SWITCHML_HIP_H_
+#define SWITCHML_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SML_ABI_VERSION 1
+
+typedef enum {
+    SML_OK = 0,
+    SML_ERR_INVALID_ARG = 1,   /* null pointer with numel > 0, bad W, ... */
+    SML_ERR_UNSUPPORTED = 2,   /* packet_numel not in {64,128,256,512,1024}, bad dtype */
+    SML_ERR_ALIGNMENT = 3,     /* payload plane not 16-byte aligned */
+    SML_ERR_HIP = 4            /* a HIP runtime call or launch failed */
+} sml_status_t;
+
+/* client_lib/src/common.h:51-55 */
+typedef enum { SML_FLOAT32 = 0, SML_INT32 = 1 } sml_data_type_t;
+
+/* flags for the quantize / dequantize entry points */
+#define SML_FLAG_PAYLOAD_LE   0x1u  /* payload plane in host (little-endian) order: the
+                                       form RCCL can sum (switch-sim mode); default is
+                                       big-endian wire order as htonl() at ppp.cc:103 */
+#define SML_FLAG_ROUND_RNE    0x2u  /* VCL=1 semantics (ppp.cc:88-99): round-to-nearest-even
+                                       on the 16-aligned body of each block, scalar
+                                       half-away tail; out-of-range -> INT32_MIN.
+                                       PARITY UNPINNED (VCL is un-vendored). Default is the
+                                       VCL=0 scalar path: roundf half-away-from-zero. */
+
+int sml_abi_version(void);
+const char* sml_status_string(sml_status_t s);
+/* Last HIP error string seen by this library on the calling thread ("" if none). */
+const char* sml_last_error(void);
+
+/* ceil(numel*4 / (packet_numel*4)) — CpuExponentQuantizerPPP::SetupJobSlice, ppp.cc:54-62 */
+uint64_t sml_num_blocks(uint64_t numel, uint32_t packet_numel);
+
+/* Host: scale factors for all 256 int8 exponents, lut[(uint8_t)e] =
+ *   (float)(double(INT32_MAX) / (num_workers * powf(2, e)))
+ * — the scale PostprocessSingle stores from the received global exponent,
+ * ppp.cc:254-260.  num_workers >= 1. */
+sml_status_t sml_scale_lut(uint16_t num_workers, float lut[256]);
+
+/* Device: the same 256 scales as computed INSIDE the kernels (test hook that
+ * proves the device formula equals sml_scale_lut bit for bit). d_lut: float[256]. */
+sml_status_t sml_scale_lut_device(uint16_t num_workers, float* d_lut, void* stream);
+
+/* K2 — exponent plane only: d_exps[k] = int8 exponent of block k (max |x|,
+ * NaN skipped, ((bits & 0x7f800000) >> 23) - 126) — the exponent half of
+ * PreprocessSingle, ppp.cc:115-156.  Used before the exponent exchange in
+ * switch-sim mode (the switch's signed int8 max, p4/exponents.p4:48-54). */
+sml_status_t sml_exponents(const float* d_in, uint64_t numel, uint32_t packet_numel,
+                           int8_t* d_exps, void* stream);
+
+/* K1 / K3 — quantize + pack, the quantize half of PreprocessSingle
+ * (ppp.cc:72-113):  payload[k*P+i] = htonl((int32)roundf(x[k*P+i] * scale(W, e_k)))
+ *  - d_global_exps == NULL  (K1, fused): e_k is the block's own exponent, as
+ *    the dummy/loopback backend returns it unchanged (dummy_backend.cc:72-84);
+ *    d_exps_out (nullable) receives the exponent plane.
+ *  - d_global_exps != NULL  (K3): e_k = d_global_exps[k], the switch's
+ *    aggregated exponent; d_exps_out must be NULL or equal to it (not written).
+ *  d_payload: int32[B*P], 16-byte aligned.  d_in may have any 4-byte alignment
+ *  (slices start at arbitrary element offsets). */
+sml_status_t sml_quantize_pack(const float* d_in, uint64_t numel, uint32_t packet_numel,
+                               uint16_t num_workers, const int8_t* d_global_exps,
+                               int32_t* d_payload, int8_t* d_exps_out,
+                               uint32_t flags, void* stream);
+
+/* K4 — dequantize the aggregated payload, the dequantize half of
+ * PostprocessSingle (ppp.cc:197-251):
+ *   out[k*P+i] = (float)(int32)ntohl(payload[k*P+i]) / scale(W, exps[k])
+ * (int->float RNE, IEEE division).  Only `numel` outputs are written.
+ * d_out may have any 4-byte alignment; d_payload 16-byte aligned. */
+sml_status_t sml_dequantize(const int32_t* d_payload, const int8_t* d_exps, uint64_t numel,
+                            uint32_t packet_numel, uint16_t num_workers, float* d_out,
+                            uint32_t flags, void* stream);
+
+/* INT32 jobs — byte-order conversion only (ppp.cc:158-190 pre, 262-298 post).
+ * d_out[i] = bswap32(d_in[i]) for i < numel; in == out allowed. */
+sml_status_t sml_bswap_i32(const int32_t* d_in, int32_t* d_out, uint64_t numel, void* stream);
+
+/* K5 — the dummy backend's "switch": every BE payload word is multiplied by
+ * num_workers with int32 wrap-around, exponents pass through unchanged
+ * (DummyBackend::ProcessPacket, client_lib/src/backends/dummy/dummy_backend.cc:72-84).
+ * count = B*P words (stale/zero tails included, as the reference does). */
+sml_status_t sml_loopback_aggregate(int32_t* d_payload, uint64_t count, uint16_t num_workers,
+                                    uint32_t flags, void* stream);
+
+/* Fused loopback round trip for FLOAT32 (dummy backend, one pass over HBM):
+ * exponent -> quantize -> x num_workers -> dequantize, writing d_out[numel]
+ * and, when d_payload != NULL, the on-wire payload plane as sent (before the
+ * loopback multiply) and d_exps_out.  Bit-identical to K1 -> K5 -> K4. */
+sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t numel,
+                                    uint32_t packet_numel, uint16_t num_workers,
+                                    int32_t* d_payload, int8_t* d_exps_out,
+                                    uint32_t flags, void* stream);
+
+/* Launch-geometry knob for experiments: workgroups per launch for the
+ * streaming kernels (0 = one 256-thread workgroup per 4 tiles of 1024
+ * elements, i.e. no grid-stride).  Process-wide; returns the previous value. */
+uint32_t sml_set_grid_limit(uint32_t max_workgroups);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SWITCHML_HIP_H_ */

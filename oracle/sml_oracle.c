@@ -1,0 +1,385 @@
+/*
+ * sml_oracle.c — CPU restatement of SwitchML's end-host pre/post-processor
+ * (CpuExponentQuantizerPPP, VCL=0 build) and of the dummy-backend packet loop
+ * that drives it.
+ *
+ * TEST INFRASTRUCTURE ONLY — see sml_oracle.h for who may call this and for
+ * its parity status ("parity unpinned" at the bit level: the reference is not
+ * buildable in this image; pinned by the reference's 1 % known-answer checks
+ * and hand-derived vectors).
+ *
+ * Citations are relative to /root/reference/dev_root/client_lib/src/.
+ */
+#include "sml_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+static inline uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+
+static inline uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+uint64_t orc_num_blocks(uint64_t numel, uint64_t P) {
+    /* ppp.cc:56-57: tensor_size = numel * DataTypeSize; (size + ltu - 1) / ltu */
+    uint64_t bytes = numel * 4, ltu = P * 4;
+    return (bytes + ltu - 1) / ltu;
+}
+
+int8_t orc_block_exponent(const float* x, uint64_t n) {
+    /* ppp.cc:129-146 (scalar loop): current_max starts at 0; v = abs(x);
+     * if (v > current_max) current_max = v.  NaN compares false: never taken. */
+    float current_max = 0.0f;
+    for (uint64_t i = 0; i < n; i++) {
+        float v = fabsf(x[i]);
+        if (v > current_max) current_max = v;
+    }
+    /* ppp.cc:154: ((bits & 0x7f800000) >> 23) - 126, stored through int8_t* */
+    int32_t bits = (int32_t)f2u(current_max);
+    int32_t e = ((bits & 0x7f800000) >> 23) - 126;
+    return (int8_t)(uint8_t)(e & 0xff);
+}
+
+float orc_scale(uint16_t num_workers, int8_t exponent) {
+    /* ppp.cc:257-258: scaling_factors_[ltu] =
+     *   double(INT32_MAX) / (num_workers * powf(2, exponent));
+     * num_workers (uint16) * float -> float multiply; the quotient is a double
+     * and is rounded to float on store. */
+    float denom = (float)num_workers * powf(2.0f, (float)exponent);
+    double q = (double)2147483647 / (double)denom;
+    return (float)q;
+}
+
+void orc_scale_lut(uint16_t num_workers, float lut[256]) {
+    for (int i = 0; i < 256; i++) lut[i] = orc_scale(num_workers, (int8_t)(uint8_t)i);
+}
+
+/* gcc x86-64 lowers the (UB for negatives) float -> uint32_t conversion of
+ * ppp.cc:103 as cvttss2si %xmm, %rax (64-bit signed truncation) and keeps the
+ * low 32 bits.  Out-of-int64-range or NaN gives the "integer indefinite"
+ * 0x8000000000000000, whose low half is 0. */
+static inline uint32_t x86_f2u32(float r) {
+    if (!(fabsf(r) < 0x1p63f)) return 0u;
+    return (uint32_t)(uint64_t)(int64_t)r;
+}
+
+uint32_t orc_quantize_value(float x, float scale) {
+    /* ppp.cc:103: out_ptr[i] = htonl(std::round(in_ptr[i] * scaling_factors_[ltu_id])); */
+    float prod = x * scale;           /* float * float, correctly rounded */
+    float r = roundf(prod);           /* std::round(float): half away from zero */
+    return bswap32(x86_f2u32(r));     /* htonl on little-endian */
+}
+
+uint32_t orc_quantize_value_rne(float x, float scale) {
+    /* VCL=1 body (ppp.cc:96-98): roundi() = cvtps2dq under the default MXCSR
+     * (round-to-nearest-even); out of int32 range or NaN -> 0x80000000. */
+    float prod = x * scale;
+    uint32_t q;
+    if (!(fabsf(prod) < 0x1p31f)) {
+        q = 0x80000000u;
+    } else {
+        float r = nearbyintf(prod); /* default rounding mode is RNE */
+        q = (uint32_t)(int32_t)r;
+    }
+    return bswap32(q);
+}
+
+float orc_dequantize_value(uint32_t be_word, float scale) {
+    /* ppp.cc:240-241: int32_t in_be = (int32_t) ntohl(in_ptr[j]);
+     *                 out_ptr[j] = in_be / scaling_factors_[ltu_id];
+     * int -> float conversion (RNE) then IEEE float division. */
+    int32_t v = (int32_t)bswap32(be_word);
+    return (float)v / scale;
+}
+
+void orc_exponents(const float* in, uint64_t numel, uint64_t P, int8_t* exps) {
+    uint64_t B = orc_num_blocks(numel, P);
+    for (uint64_t k = 0; k < B; k++) {
+        uint64_t off = k * P, n = numel - off < P ? numel - off : P;
+        exps[k] = orc_block_exponent(in + off, n);
+    }
+}
+
+void orc_quantize(const float* in, uint64_t numel, uint64_t P, uint16_t num_workers,
+                  const int8_t* global_exps, int rounding, uint32_t* payload_be) {
+    uint64_t B = orc_num_blocks(numel, P);
+    float lut[256];
+    orc_scale_lut(num_workers, lut);
+    for (uint64_t k = 0; k < B; k++) {
+        uint64_t off = k * P, n = numel - off < P ? numel - off : P;
+        int8_t e = global_exps ? global_exps[k] : orc_block_exponent(in + off, n);
+        float s = lut[(uint8_t)e];
+        uint64_t i = 0;
+        if (rounding == 1) {
+            /* VCL body covers n - n % 16 elements (ppp.cc:92-99), scalar tail after. */
+            uint64_t vec = n - n % 16;
+            for (; i < vec; i++) payload_be[off + i] = orc_quantize_value_rne(in[off + i], s);
+        }
+        for (; i < n; i++) payload_be[off + i] = orc_quantize_value(in[off + i], s);
+        for (; i < P; i++) payload_be[off + i] = 0u; /* reference: stale ring bytes */
+    }
+}
+
+void orc_dequantize(const uint32_t* payload_be, const int8_t* global_exps, uint64_t numel,
+                    uint64_t P, uint16_t num_workers, float* out) {
+    uint64_t B = orc_num_blocks(numel, P);
+    float lut[256];
+    orc_scale_lut(num_workers, lut);
+    for (uint64_t k = 0; k < B; k++) {
+        uint64_t off = k * P, n = numel - off < P ? numel - off : P;
+        float s = lut[(uint8_t)global_exps[k]];
+        for (uint64_t i = 0; i < n; i++) out[off + i] = orc_dequantize_value(payload_be[off + i], s);
+    }
+}
+
+void orc_bswap32(const uint32_t* in, uint32_t* out, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++) out[i] = bswap32(in[i]);
+}
+
+void orc_loopback_aggregate(uint32_t* payload_be, uint64_t n, uint16_t num_workers) {
+    /* dummy_backend.cc:78-82: SWAP_INT32, *= num_workers (int32 wrap), SWAP_INT32 */
+    for (uint64_t j = 0; j < n; j++) {
+        uint32_t v = bswap32(payload_be[j]);
+        v = v * (uint32_t)num_workers;
+        payload_be[j] = bswap32(v);
+    }
+}
+
+void orc_switch_exps(const int8_t* const* exps, int W, uint64_t B, int8_t* out) {
+    /* exponents.p4:48-54: signed max over workers of int<8> */
+    for (uint64_t k = 0; k < B; k++) {
+        int8_t m = exps[0][k];
+        for (int w = 1; w < W; w++) if (exps[w][k] > m) m = exps[w][k];
+        out[k] = m;
+    }
+}
+
+void orc_switch_payload(const uint32_t* const* payload_be, int W, uint64_t n, uint32_t* out) {
+    /* processor.p4:48-54: value = value + worker value as bit<32> (wrapping);
+     * the switch parses the payload big-endian and emits big-endian. */
+    for (uint64_t j = 0; j < n; j++) {
+        uint32_t acc = 0;
+        for (int w = 0; w < W; w++) acc += bswap32(payload_be[w][j]);
+        out[j] = bswap32(acc);
+    }
+}
+
+void orc_slice(uint64_t numel, int T, int t, uint64_t* offset, uint64_t* slice_numel) {
+    /* fifo_scheduler.cc:93-109 */
+    uint64_t n = numel / (uint64_t)T;
+    uint64_t rem = numel % (uint64_t)T;
+    if (rem > (uint64_t)t) {
+        n++;
+        *offset = (uint64_t)t * n;
+    } else {
+        *offset = (uint64_t)t * n + rem;
+    }
+    *slice_numel = n;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Packet-loop restatement: one PPP instance per worker thread.              */
+
+typedef struct {
+    const float* in;
+    float* out;
+    uint64_t numel;   /* slice numel */
+    uint64_t P;       /* ltu numel */
+    uint64_t B;       /* total_main_num_ltus_ (ppp.cc:57) */
+    uint64_t b;       /* batch_num_ltus_ (ppp.cc:58) */
+    uint16_t W;
+    float* scales;    /* scaling_factors_ (ppp.cc:60) */
+    const float* lut;
+} orc_ppp;
+
+/* PreprocessSingle, FLOAT32 branch — ppp.cc:69-156 */
+static void ppp_preprocess(orc_ppp* s, uint64_t ltu_id, uint32_t* entries, uint8_t* extra) {
+    if (ltu_id >= s->b) {
+        uint64_t k = ltu_id - s->b;
+        uint64_t off = k * s->P;
+        uint64_t n = s->numel - off < s->P ? s->numel - off : s->P;
+        float sc = s->scales[k];
+        for (uint64_t i = 0; i < n; i++) entries[i] = orc_quantize_value(s->in[off + i], sc);
+        ltu_id = k + s->b;
+    }
+    if (ltu_id < s->B) {
+        uint64_t off = ltu_id * s->P;
+        uint64_t n = s->numel - off < s->P ? s->numel - off : s->P;
+        extra[0] = (uint8_t)orc_block_exponent(s->in + off, n);
+    }
+}
+
+/* PostprocessSingle, FLOAT32 branch — ppp.cc:194-260 */
+static void ppp_postprocess(orc_ppp* s, uint64_t ltu_id, const uint32_t* entries, const uint8_t* extra) {
+    if (ltu_id >= s->b) {
+        uint64_t k = ltu_id - s->b;
+        uint64_t off = k * s->P;
+        uint64_t n = s->numel - off < s->P ? s->numel - off : s->P;
+        float sc = s->scales[k];
+        for (uint64_t i = 0; i < n; i++) s->out[off + i] = orc_dequantize_value(entries[i], sc);
+        ltu_id = k + s->b;
+    }
+    if (ltu_id < s->B) s->scales[ltu_id] = s->lut[extra[0]];
+}
+
+typedef struct {
+    orc_ppp ppp;
+    int mode;
+    int8_t* pkt_exps;       /* optional stream capture */
+    uint32_t* pkt_payload;  /* optional stream capture */
+    int rc;
+} orc_worker;
+
+/* Record packet p as sent: the exponent byte if p < B, the payload words of
+ * block p-b if p >= b; everything the reference leaves stale is recorded as 0. */
+static void capture(orc_worker* w, uint64_t p, const uint32_t* ent, const uint8_t* ex) {
+    const orc_ppp* s = &w->ppp;
+    w->pkt_exps[p] = p < s->B ? (int8_t)ex[0] : 0;
+    uint32_t* dst = w->pkt_payload + p * s->P;
+    memset(dst, 0, s->P * 4);
+    if (p >= s->b) {
+        uint64_t off = (p - s->b) * s->P;
+        uint64_t n = s->numel - off < s->P ? s->numel - off : s->P;
+        memcpy(dst, ent, n * 4);
+    }
+}
+
+/* DummyWorkerThread::operator() main loop for one slice, in-order delivery
+ * (dummy_worker_thread.cc:86-177; ReceiveBurst's random order does not change
+ * results: packet p only needs scale[p-b], stored when packet p-b returned). */
+static void* worker_run(void* arg) {
+    orc_worker* w = (orc_worker*)arg;
+    orc_ppp* s = &w->ppp;
+    w->rc = 0;
+    if (s->numel == 0) return NULL; /* dummy_worker_thread.cc:87 */
+    uint64_t total = s->B + s->b;   /* NeedsExtraBatch() for FLOAT32 (:95-99) */
+    uint32_t* ring = (uint32_t*)calloc(s->b * s->P, 4);
+    uint8_t* extra = (uint8_t*)calloc(s->b * 2, 1);
+    s->scales = (float*)malloc(s->B * sizeof(float));
+    if (!ring || !extra || !s->scales) { w->rc = -1; goto done; }
+
+    for (uint64_t p = 0; p < s->b; p++) { /* first batch (:106-116) */
+        ppp_preprocess(s, p, ring + (p % s->b) * s->P, extra + (p % s->b) * 2);
+        if (w->pkt_exps) capture(w, p, ring + (p % s->b) * s->P, extra + (p % s->b) * 2);
+    }
+    for (uint64_t p = 0; p < total; p++) { /* receive loop (:126-177), in order */
+        uint32_t* ent = ring + (p % s->b) * s->P;
+        uint8_t* ex = extra + (p % s->b) * 2;
+        if (w->mode == ORC_MODE_ROUNDTRIP) {
+            orc_loopback_aggregate(ent, s->P, s->W); /* ProcessPacket (dummy_backend.cc:72-84) */
+            ppp_postprocess(s, p, ent, ex);
+        } else if (p < s->B) {
+            s->scales[p] = s->lut[ex[0]]; /* the scale-store half of PostprocessSingle */
+        }
+        uint64_t np = p + s->b;
+        if (np >= total) continue;
+        ppp_preprocess(s, np, ent, ex);
+        if (w->pkt_exps) capture(w, np, ent, ex);
+    }
+done:
+    free(ring);
+    free(extra);
+    free(s->scales);
+    s->scales = NULL;
+    return NULL;
+}
+
+int orc_dummy_allreduce(const float* in, float* out, uint64_t numel, uint64_t P,
+                        uint32_t max_outstanding_packets, int T, uint16_t W,
+                        int threaded, int mode) {
+    if (T <= 0 || P == 0) return -1;
+    float lut[256];
+    orc_scale_lut(W, lut);
+    orc_worker* ws = (orc_worker*)calloc((size_t)T, sizeof(orc_worker));
+    pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
+    if (!ws || !th) { free(ws); free(th); return -1; }
+    uint64_t batch_max = max_outstanding_packets / (uint64_t)T; /* dummy_worker_thread.cc:59 */
+    for (int t = 0; t < T; t++) {
+        uint64_t off, n;
+        orc_slice(numel, T, t, &off, &n);
+        orc_ppp* s = &ws[t].ppp;
+        s->in = in + off;
+        s->out = out + off;
+        s->numel = n;
+        s->P = P;
+        s->B = orc_num_blocks(n, P);
+        s->b = s->B < batch_max ? s->B : batch_max;
+        s->W = W;
+        s->lut = lut;
+        ws[t].mode = mode;
+        if (s->b == 0 && s->B > 0) { free(ws); free(th); return -1; }
+    }
+    int rc = 0;
+    if (threaded && T > 1) {
+        for (int t = 0; t < T; t++) pthread_create(&th[t], NULL, worker_run, &ws[t]);
+        for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+    } else {
+        for (int t = 0; t < T; t++) worker_run(&ws[t]);
+    }
+    for (int t = 0; t < T; t++) rc |= ws[t].rc;
+    free(ws);
+    free(th);
+    return rc;
+}
+
+int orc_dummy_packet_stream(const float* in, uint64_t numel, uint64_t P, uint32_t batch_max,
+                            uint16_t W, int8_t* pkt_exps, uint32_t* pkt_payload, float* out) {
+    float lut[256];
+    orc_scale_lut(W, lut);
+    orc_worker w;
+    memset(&w, 0, sizeof(w));
+    w.ppp.in = in;
+    w.ppp.out = out;
+    w.ppp.numel = numel;
+    w.ppp.P = P;
+    w.ppp.B = orc_num_blocks(numel, P);
+    w.ppp.b = w.ppp.B < batch_max ? w.ppp.B : batch_max;
+    w.ppp.W = W;
+    w.ppp.lut = lut;
+    w.mode = ORC_MODE_ROUNDTRIP;
+    w.pkt_exps = pkt_exps;
+    w.pkt_payload = pkt_payload;
+    if (w.ppp.b == 0) return -1;
+    memset(pkt_exps, 0, w.ppp.B + w.ppp.b);
+    memset(pkt_payload, 0, (w.ppp.B + w.ppp.b) * P * 4);
+    worker_run(&w);
+    return w.rc;
+}
+
+/* glibc srandom_r/random_r, TYPE_3 (degree 31, separation 3) — the generator
+ * behind rand() that the reference's benchmarks seed with srand(seed). */
+void orc_glibc_rand(uint32_t seed, uint64_t n, int32_t* out) {
+    int32_t r[34];
+    int64_t word;
+    if (seed == 0) seed = 1;
+    r[0] = (int32_t)seed;
+    for (int i = 1; i < 31; i++) {
+        int64_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+        word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        r[i] = (int32_t)word;
+    }
+    /* ring of the last 34 values; discard the first 310 outputs */
+    uint32_t ring[34];
+    for (int i = 0; i < 31; i++) ring[i] = (uint32_t)r[i];
+    for (int i = 31; i < 34; i++) ring[i] = ring[i - 31];
+    uint64_t k = 34;
+    for (uint64_t i = 0; i < 310 + n; i++, k++) {
+        uint32_t v = ring[(k - 31) % 34] + ring[(k - 3) % 34];
+        ring[k % 34] = v;
+        if (i >= 310) out[i - 310] = (int32_t)(v >> 1);
+    }
+}
+
+void orc_ref_random_floats(uint32_t seed, uint64_t n, float* out) {
+    int32_t* r = (int32_t*)malloc(n * sizeof(int32_t));
+    if (!r) return;
+    orc_glibc_rand(seed, n, r);
+    for (uint64_t i = 0; i < n; i++) {
+        int32_t v = r[i];
+        uint32_t bits = ((uint32_t)(v % 2) << 31) | ((uint32_t)(v % 254) << 23) | (uint32_t)(v % (1 << 23));
+        memcpy(&out[i], &bits, 4);
+    }
+    free(r);
+}

@@ -1,0 +1,700 @@
+// sml_quantizer.hip — CDNA4 (gfx950) kernels for SwitchML's end-host
+// pre/post-processor and the C-ABI entry points of include/switchml_hip.h.
+//
+// What the reference does per 1 KiB LTU on one CPU thread
+// (client_lib/src/prepostprocessors/cpu_exponent_quantizer_ppp.cc, "ppp.cc"),
+// these kernels do for a whole job slice per launch.  The work is a pure
+// HBM stream (8 B/element for quantize+pack), so the design rules are the
+// streaming ones: 16-B-per-lane coalesced loads/stores (1 KiB per wave
+// instruction), several loads in flight per lane, the per-packet max-|x|
+// reduce in registers + cross-lane (DPP/ds_swizzle via __shfl_xor), no LDS
+// round trip for the data, no MFMA (nothing here is a contraction).
+//
+// Work unit: a "tile" = 1024 consecutive elements of the slice = 4 x f4
+// per lane of one wave64.  Slice u of a tile (u = 0..3) is 256 consecutive
+// elements, lane l holds elements [u*256 + 4l, u*256 + 4l + 4).  A packet of
+// P elements therefore spans P/4 lanes of one slice (P <= 256) or P/256
+// whole slices (P = 512, 1024); every packet lies inside one tile.
+//
+// Arithmetic parity with the VCL=0 reference build:
+//  * exponent: integer max of (bits & 0x7fffffff) with NaN bit patterns
+//    mapped to 0 == the float '>' scan from 0 at ppp.cc:141-146; then
+//    ((m >> 23) & 0xff) - 126 truncated to int8 (ppp.cc:154).
+//  * scale: (float)(double(INT32_MAX) / ((float)W * 2^e)) (ppp.cc:257-258),
+//    computed once per workgroup into an LDS table.
+//  * quantize: roundf(x * s) half away from zero, then the x86-64
+//    cvttss2si-to-64-bit-then-truncate conversion (NaN/inf/|r| >= 2^63 -> 0,
+//    2^31 <= |r| < 2^63 wraps mod 2^32), then bswap (htonl) — ppp.cc:103.
+//  * dequantize: (float)(int32)ntohl(q) / s with IEEE division (ppp.cc:240-241).
+//  * f32 denormals are preserved (the kernels are built without
+//    -fgpu-flush-denormals-to-zero and without fast-math).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include "switchml_hip.h"
+
+namespace sml {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 mkf4(float a, float b, float c, float d) { return f4{a, b, c, d}; }
+__device__ __forceinline__ u4 mku4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return u4{a, b, c, d}; }
+
+constexpr int kWave = 64;
+constexpr int kBlockThreads = 256;
+constexpr int kWavesPerBlock = kBlockThreads / kWave;
+constexpr int kU = 4;                          // f4 slices per lane per tile
+constexpr int kTileElems = kWave * 4 * kU;     // 1024
+
+// ----------------------------------------------------------------- numerics
+
+// ppp.cc:257-258.  powf(2, e) is exactly 2^e for every int8 e (2^-127 and
+// 2^-128 are denormal but exact), so ldexp gives the same float; the product
+// with (float)W is a float multiply (overflow -> inf -> scale 0, as on x86);
+// the quotient is a correctly rounded double division, rounded to float.
+__device__ __forceinline__ float scale_of(uint32_t W, int e) {
+    float denom = (float)W * __builtin_ldexpf(1.0f, e);
+    return (float)(2147483647.0 / (double)denom);
+}
+
+// |x| bits with NaN mapped to 0: a NaN never wins the reference's '>' scan.
+__device__ __forceinline__ uint32_t absbits(float x) {
+    uint32_t a = __float_as_uint(x) & 0x7fffffffu;
+    return a > 0x7f800000u ? 0u : a;
+}
+
+__device__ __forceinline__ int exponent_of(uint32_t maxbits) {
+    // ppp.cc:154 computes in int and stores through int8_t*: 129 -> -127, 128 -> -128.
+    return (int)(int8_t)(uint8_t)(((maxbits >> 23) & 0xffu) - 126u);
+}
+
+// gcc/x86-64 lowering of the float -> uint32 conversion at ppp.cc:103:
+// cvttss2si into a 64-bit register, low 32 bits kept.  Needed only for
+// |r| >= 2^31 or NaN (r is already integral); below that it equals v_cvt_i32_f32.
+__device__ __forceinline__ uint32_t x86_wrap(float r) {
+    uint32_t b = __float_as_uint(r);
+    uint32_t E = (b >> 23) & 0xffu;
+    if (E >= 190u) return 0u;                  // |r| >= 2^63, inf, NaN -> 0x8000...0 -> low 0
+    uint32_t m = (b & 0x7fffffu) | 0x800000u;
+    uint32_t sh = E - 150u;                    // >= 8 here
+    uint32_t low = sh < 32u ? (m << sh) : 0u;
+    return (b >> 31) ? (0u - low) : low;
+}
+
+// Quantize 4 consecutive elements with one scale (host byte order result).
+// RNE_BODY: lanes [0, body) use the VCL=1 roundi() semantics (RNE, out of
+// range / NaN -> 0x80000000); the rest use the VCL=0 scalar path.  With
+// RNE == false every element takes the scalar path.
+template <bool RNE>
+__device__ __forceinline__ u4 quantize4(f4 x, float s, uint64_t idx, uint64_t body) {
+    const float p[4] = {x.x * s, x.y * s, x.z * s, x.w * s};
+    uint32_t q[4];
+    bool wide = false;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        if (RNE && idx + j < body) {
+            q[j] = fabsf(p[j]) < 0x1p31f ? (uint32_t)(int32_t)__builtin_rintf(p[j]) : 0x80000000u;
+        } else {
+            float r = __builtin_roundf(p[j]);      // half away from zero, like std::round(float)
+            q[j] = (uint32_t)(int32_t)r;           // exact whenever |r| < 2^31
+            wide |= !(fabsf(r) < 0x1p31f);
+        }
+    }
+    if (__builtin_expect(wide, 0)) {               // rare: out-of-range / NaN / inf products
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (RNE && idx + j < body) continue;
+            float r = __builtin_roundf(p[j]);
+            if (!(fabsf(r) < 0x1p31f)) q[j] = x86_wrap(r);
+        }
+    }
+    return mku4(q[0], q[1], q[2], q[3]);
+}
+
+__device__ __forceinline__ float dequantize1(uint32_t q_host_order, float s) {
+    return (float)(int32_t)q_host_order / s;
+}
+
+__device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
+
+// ------------------------------------------------------------- memory ops
+
+template <bool ALIGNED>
+__device__ __forceinline__ f4 load4(const float* p) {
+    if constexpr (ALIGNED) {
+        return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+    } else {
+        return mkf4(p[0], p[1], p[2], p[3]);
+    }
+}
+
+__device__ __forceinline__ f4 load4_guarded(const float* p, uint64_t idx, uint64_t numel) {
+    f4 v;
+    v.x = idx + 0 < numel ? p[0] : 0.0f;
+    v.y = idx + 1 < numel ? p[1] : 0.0f;
+    v.z = idx + 2 < numel ? p[2] : 0.0f;
+    v.w = idx + 3 < numel ? p[3] : 0.0f;
+    return v;
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ void store4(float* p, f4 v) {
+    if constexpr (ALIGNED) {
+        __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
+    } else {
+        p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void store4_guarded(float* p, f4 v, uint64_t idx, uint64_t numel) {
+    if (idx + 0 < numel) p[0] = v.x;
+    if (idx + 1 < numel) p[1] = v.y;
+    if (idx + 2 < numel) p[2] = v.z;
+    if (idx + 3 < numel) p[3] = v.w;
+}
+
+__device__ __forceinline__ void store_payload(u4* dst, u4 q) {
+    __builtin_nontemporal_store(q, dst);
+}
+
+// ---------------------------------------------------- per-packet reductions
+
+// Max of `m` over the P/4 lanes of this lane's packet (P <= 256), via
+// butterfly exchanges inside the lane group.
+template <int P>
+__device__ __forceinline__ uint32_t group_max(uint32_t m) {
+    constexpr int kLanes = P / 4 < kWave ? P / 4 : kWave;
+#pragma unroll
+    for (int off = 1; off < kLanes; off <<= 1) {
+        uint32_t o = (uint32_t)__shfl_xor((int)m, off, kWave);
+        m = m > o ? m : o;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t max4(f4 v) {
+    uint32_t a = absbits(v.x), b = absbits(v.y), c = absbits(v.z), d = absbits(v.w);
+    a = a > b ? a : b;
+    c = c > d ? c : d;
+    return a > c ? a : c;
+}
+
+// Exponents e[u] of the packet each lane's slice u belongs to.
+template <int P>
+__device__ __forceinline__ void tile_exponents(const f4 (&v)[kU], int (&e)[kU]) {
+    uint32_t m[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) m[u] = max4(v[u]);
+    if constexpr (P <= 256) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) e[u] = exponent_of(group_max<P>(m[u]));
+    } else if constexpr (P == 512) {
+        uint32_t a = group_max<256>(m[0] > m[1] ? m[0] : m[1]);
+        uint32_t b = group_max<256>(m[2] > m[3] ? m[2] : m[3]);
+        e[0] = e[1] = exponent_of(a);
+        e[2] = e[3] = exponent_of(b);
+    } else {
+        static_assert(P == 1024, "packet_numel must be 64..1024, power of two");
+        uint32_t a = m[0] > m[1] ? m[0] : m[1];
+        uint32_t b = m[2] > m[3] ? m[2] : m[3];
+        uint32_t t = group_max<256>(a > b ? a : b);
+        e[0] = e[1] = e[2] = e[3] = exponent_of(t);
+    }
+}
+
+// The lane that owns packet `pkt` of slice u writes its exponent byte.
+template <int P>
+__device__ __forceinline__ void store_exponents(int8_t* exps_out, uint64_t tile_base, int lane,
+                                                const int (&e)[kU], uint64_t nblocks) {
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+        bool leader;
+        if constexpr (P <= 256) leader = (lane % (P / 4)) == 0;
+        else leader = lane == 0 && (u % (P / 256)) == 0;
+        uint64_t pkt = (tile_base + (uint64_t)(u * kWave + lane) * 4) / P;
+        if (leader && pkt < nblocks) exps_out[pkt] = (int8_t)e[u];
+    }
+}
+
+// Per-workgroup scale table, lut[(uint8_t)e], built once per launch-block.
+__device__ __forceinline__ void build_lut(float* lut, uint32_t W) {
+    lut[threadIdx.x] = scale_of(W, (int)(int8_t)(uint8_t)threadIdx.x);
+    __syncthreads();
+}
+
+// -------------------------------------------------------------- kernels
+
+struct QuantArgs {
+    const float* in;
+    uint64_t numel;
+    uint64_t nblocks;       // B
+    uint64_t ntiles;        // ceil(B*P / 1024)
+    const int8_t* gexp;     // global exponents (K3) or nullptr (K1)
+    u4* payload;          // B*P words, 16-B aligned (nullptr: exponents only)
+    int8_t* exps_out;       // nullable
+    uint32_t W;
+};
+
+// K1 (fused exponent + quantize + pack), K2 (exponents only: payload == nullptr)
+// and K3 (given global exponents: GLOBAL = true).
+template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
+__global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
+    __shared__ float lut[256];
+    if (a.payload) build_lut(lut, a.W);
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t padded = a.nblocks * P;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
+        const uint64_t base = t * kTileElems;
+        f4 v[kU];
+        if (base + kTileElems <= a.numel) {
+#pragma unroll
+            for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
+        } else {
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+                v[u] = load4_guarded(a.in + idx, idx, a.numel);
+            }
+        }
+        int e[kU];
+        if constexpr (GLOBAL) {
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                uint64_t pkt = (base + (uint64_t)(u * kWave + lane) * 4) / P;
+                e[u] = pkt < a.nblocks ? (int)a.gexp[pkt] : 0;
+            }
+        } else {
+            tile_exponents<P>(v, e);
+            if (a.exps_out) store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
+        }
+        if (!a.payload) continue;
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            if (idx >= padded) continue;
+            const float s = lut[(uint8_t)e[u]];
+            uint64_t body = 0;
+            if constexpr (RNE) {
+                // VCL body = first n - n%16 elements of the block; only the last
+                // (partial) block has a scalar half-away tail.
+                const uint64_t blk0 = idx / P * P;
+                const uint64_t n = a.numel - blk0 < (uint64_t)P ? a.numel - blk0 : (uint64_t)P;
+                body = blk0 + (n - n % 16);
+            }
+            u4 q = quantize4<RNE>(v[u], s, idx, body);
+            if constexpr (BE) { q.x = bswap(q.x); q.y = bswap(q.y); q.z = bswap(q.z); q.w = bswap(q.w); }
+            store_payload(a.payload + idx / 4, q);
+        }
+    }
+}
+
+struct DequantArgs {
+    const u4* payload;
+    const int8_t* exps;
+    float* out;
+    uint64_t numel;
+    uint64_t ntiles;        // ceil(numel / 1024)
+    uint32_t W;
+};
+
+// K4: dequantize the aggregated payload (PostprocessSingle, ppp.cc:197-251).
+template <int P, bool ALIGNED, bool BE>
+__global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
+    __shared__ float lut[256];
+    build_lut(lut, a.W);
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
+        const uint64_t base = t * kTileElems;
+        const bool full = base + kTileElems <= a.numel;
+        u4 w[kU];
+        float s[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            if (full || idx < a.numel) {
+                w[u] = __builtin_nontemporal_load(a.payload + idx / 4);
+                s[u] = lut[(uint8_t)a.exps[idx / P]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            if (!full && idx >= a.numel) continue;
+            uint32_t q0 = (uint32_t)w[u].x, q1 = (uint32_t)w[u].y, q2 = (uint32_t)w[u].z, q3 = (uint32_t)w[u].w;
+            if constexpr (BE) { q0 = bswap(q0); q1 = bswap(q1); q2 = bswap(q2); q3 = bswap(q3); }
+            f4 o = mkf4(dequantize1(q0, s[u]), dequantize1(q1, s[u]),
+                                   dequantize1(q2, s[u]), dequantize1(q3, s[u]));
+            if (full) store4<ALIGNED>(a.out + idx, o);
+            else store4_guarded(a.out + idx, o, idx, a.numel);
+        }
+    }
+}
+
+struct RoundTripArgs {
+    const float* in;
+    float* out;
+    uint64_t numel;
+    uint64_t nblocks;
+    uint64_t ntiles;        // ceil(B*P / 1024)
+    u4* payload;          // nullable: on-wire plane as sent
+    int8_t* exps_out;       // nullable
+    uint32_t W;
+};
+
+// Fused dummy-backend round trip: PreprocessSingle -> ProcessPacket (x W) ->
+// PostprocessSingle for every packet of the slice in one HBM pass.
+template <int P, bool ALIGNED, bool BE, bool RNE>
+__global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
+    __shared__ float lut[256];
+    build_lut(lut, a.W);
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t padded = a.nblocks * P;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
+        const uint64_t base = t * kTileElems;
+        const bool full = base + kTileElems <= a.numel;
+        f4 v[kU];
+        if (full) {
+#pragma unroll
+            for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
+        } else {
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+                v[u] = load4_guarded(a.in + idx, idx, a.numel);
+            }
+        }
+        int e[kU];
+        tile_exponents<P>(v, e);
+        if (a.exps_out) store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            if (idx >= padded) continue;
+            const float s = lut[(uint8_t)e[u]];
+            uint64_t body = 0;
+            if constexpr (RNE) {
+                const uint64_t blk0 = idx / P * P;
+                const uint64_t n = a.numel - blk0 < (uint64_t)P ? a.numel - blk0 : (uint64_t)P;
+                body = blk0 + (n - n % 16);
+            }
+            const u4 qv = quantize4<RNE>(v[u], s, idx, body);
+            const uint32_t q[4] = {qv.x, qv.y, qv.z, qv.w};
+            if (a.payload) {
+                u4 wq = BE ? mku4(bswap(q[0]), bswap(q[1]), bswap(q[2]), bswap(q[3]))
+                              : mku4(q[0], q[1], q[2], q[3]);
+                store_payload(a.payload + idx / 4, wq);
+            }
+            // DummyBackend::ProcessPacket: int32 wrap multiply by W.
+            f4 o = mkf4(dequantize1(q[0] * a.W, s), dequantize1(q[1] * a.W, s),
+                                   dequantize1(q[2] * a.W, s), dequantize1(q[3] * a.W, s));
+            if (full) store4<ALIGNED>(a.out + idx, o);
+            else if (idx < a.numel) store4_guarded(a.out + idx, o, idx, a.numel);
+        }
+    }
+}
+
+// K5: DummyBackend::ProcessPacket over the payload plane (in place).
+template <bool BE>
+__global__ __launch_bounds__(kBlockThreads) void k_loopback(u4* p, uint64_t nvec, uint32_t W) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; i < nvec; i += stride) {
+        u4 v = __builtin_nontemporal_load(p + i);
+        uint32_t q[4] = {(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) q[j] = BE ? bswap(bswap(q[j]) * W) : q[j] * W;
+        __builtin_nontemporal_store(mku4(q[0], q[1], q[2], q[3]), p + i);
+    }
+}
+
+// INT32 path: byteswap (in may alias out).  Vector form when both are 16-B aligned.
+__global__ __launch_bounds__(kBlockThreads) void k_bswap_vec(const u4* in, u4* out, uint64_t nvec) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; i < nvec; i += stride) {
+        u4 v = in[i];
+        out[i] = mku4(bswap(v.x), bswap(v.y), bswap(v.z), bswap(v.w));
+    }
+}
+
+__global__ __launch_bounds__(kBlockThreads) void k_bswap_scalar(const int32_t* in, int32_t* out, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; i < n; i += stride)
+        out[i] = (int32_t)bswap((uint32_t)in[i]);
+}
+
+__global__ void k_scale_lut(float* lut, uint32_t W) {
+    lut[threadIdx.x] = scale_of(W, (int)(int8_t)(uint8_t)threadIdx.x);
+}
+
+// ------------------------------------------------------------ host side
+
+static thread_local char g_last_error[256] = "";
+static uint32_t g_grid_limit = 0;
+
+static sml_status_t hip_check(hipError_t err) {
+    if (err == hipSuccess) return SML_OK;
+    strncpy(g_last_error, hipGetErrorString(err), sizeof(g_last_error) - 1);
+    return SML_ERR_HIP;
+}
+
+static sml_status_t launch_check() { return hip_check(hipGetLastError()); }
+
+static inline bool valid_packet(uint32_t P) {
+    return P == 64 || P == 128 || P == 256 || P == 512 || P == 1024;
+}
+
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+static inline bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }
+
+static inline uint32_t grid_for_tiles(uint64_t ntiles) {
+    uint64_t g = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (g == 0) g = 1;
+    if (g_grid_limit && g > g_grid_limit) g = g_grid_limit;
+    if (g > 0x7fffffffull) g = 0x7fffffffull;
+    return (uint32_t)g;
+}
+
+static inline uint32_t grid_for_vec(uint64_t nvec) {
+    uint64_t g = (nvec + kBlockThreads - 1) / kBlockThreads;
+    uint64_t cap = g_grid_limit ? g_grid_limit : 8192;
+    if (g > cap) g = cap;
+    if (g == 0) g = 1;
+    return (uint32_t)g;
+}
+
+// Dispatch tables: runtime (P, alignment, mode) -> template instance.
+template <bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
+static void launch_quant_p(uint32_t P, dim3 grid, hipStream_t st, const QuantArgs& a) {
+    switch (P) {
+        case 64:   k_quantize_pack<64, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_quantize_pack<128, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_quantize_pack<256, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_quantize_pack<512, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_quantize_pack<1024, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
+template <bool ALIGNED, bool GLOBAL, bool BE>
+static void launch_quant_r(bool rne, uint32_t P, dim3 g, hipStream_t st, const QuantArgs& a) {
+    if (rne) launch_quant_p<ALIGNED, GLOBAL, BE, true>(P, g, st, a);
+    else launch_quant_p<ALIGNED, GLOBAL, BE, false>(P, g, st, a);
+}
+
+template <bool ALIGNED, bool GLOBAL>
+static void launch_quant_b(bool be, bool rne, uint32_t P, dim3 g, hipStream_t st, const QuantArgs& a) {
+    if (be) launch_quant_r<ALIGNED, GLOBAL, true>(rne, P, g, st, a);
+    else launch_quant_r<ALIGNED, GLOBAL, false>(rne, P, g, st, a);
+}
+
+template <bool ALIGNED, bool BE>
+static void launch_deq_p(uint32_t P, dim3 grid, hipStream_t st, const DequantArgs& a) {
+    switch (P) {
+        case 64:   k_dequantize<64, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_dequantize<128, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_dequantize<256, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_dequantize<512, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_dequantize<1024, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
+template <bool ALIGNED, bool BE, bool RNE>
+static void launch_rt_p(uint32_t P, dim3 grid, hipStream_t st, const RoundTripArgs& a) {
+    switch (P) {
+        case 64:   k_roundtrip<64, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_roundtrip<128, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_roundtrip<256, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_roundtrip<512, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_roundtrip<1024, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
+template <bool ALIGNED>
+static void launch_rt_a(bool be, bool rne, uint32_t P, dim3 g, hipStream_t st, const RoundTripArgs& a) {
+    if (be) { if (rne) launch_rt_p<ALIGNED, true, true>(P, g, st, a); else launch_rt_p<ALIGNED, true, false>(P, g, st, a); }
+    else    { if (rne) launch_rt_p<ALIGNED, false, true>(P, g, st, a); else launch_rt_p<ALIGNED, false, false>(P, g, st, a); }
+}
+
+}  // namespace sml
+
+using namespace sml;
+
+extern "C" {
+
+int sml_abi_version(void) { return SML_ABI_VERSION; }
+
+const char* sml_status_string(sml_status_t s) {
+    switch (s) {
+        case SML_OK: return "SML_OK";
+        case SML_ERR_INVALID_ARG: return "SML_ERR_INVALID_ARG";
+        case SML_ERR_UNSUPPORTED: return "SML_ERR_UNSUPPORTED";
+        case SML_ERR_ALIGNMENT: return "SML_ERR_ALIGNMENT";
+        case SML_ERR_HIP: return "SML_ERR_HIP";
+    }
+    return "SML_ERR_UNKNOWN";
+}
+
+const char* sml_last_error(void) { return g_last_error; }
+
+uint32_t sml_set_grid_limit(uint32_t max_workgroups) {
+    uint32_t prev = g_grid_limit;
+    g_grid_limit = max_workgroups;
+    return prev;
+}
+
+uint64_t sml_num_blocks(uint64_t numel, uint32_t packet_numel) {
+    if (packet_numel == 0) return 0;
+    return (numel * 4 + (uint64_t)packet_numel * 4 - 1) / ((uint64_t)packet_numel * 4);
+}
+
+sml_status_t sml_scale_lut(uint16_t num_workers, float lut[256]) {
+    if (num_workers == 0 || !lut) return SML_ERR_INVALID_ARG;
+    for (int i = 0; i < 256; i++) {
+        int e = (int)(int8_t)(uint8_t)i;
+        float denom = (float)num_workers * powf(2.0f, (float)e);
+        lut[i] = (float)((double)2147483647 / (double)denom);
+    }
+    return SML_OK;
+}
+
+sml_status_t sml_scale_lut_device(uint16_t num_workers, float* d_lut, void* stream) {
+    if (num_workers == 0 || !d_lut) return SML_ERR_INVALID_ARG;
+    k_scale_lut<<<1, 256, 0, (hipStream_t)stream>>>(d_lut, num_workers);
+    return launch_check();
+}
+
+static sml_status_t quantize_common(const float* d_in, uint64_t numel, uint32_t P, uint16_t W,
+                                    const int8_t* d_gexp, int32_t* d_payload, int8_t* d_exps_out,
+                                    uint32_t flags, void* stream) {
+    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
+    if (numel == 0) return SML_OK;
+    if (!d_in || !aligned4(d_in)) return SML_ERR_INVALID_ARG;
+    if (d_payload && !aligned16(d_payload)) return SML_ERR_ALIGNMENT;
+    QuantArgs a;
+    a.in = d_in;
+    a.numel = numel;
+    a.nblocks = sml_num_blocks(numel, P);
+    a.ntiles = (a.nblocks * P + kTileElems - 1) / kTileElems;
+    a.gexp = d_gexp;
+    a.payload = reinterpret_cast<u4*>(d_payload);
+    a.exps_out = d_gexp ? nullptr : d_exps_out;
+    a.W = W;
+    dim3 grid(grid_for_tiles(a.ntiles));
+    hipStream_t st = (hipStream_t)stream;
+    const bool al = aligned16(d_in), be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
+    if (d_gexp) {
+        if (al) launch_quant_b<true, true>(be, rne, P, grid, st, a);
+        else launch_quant_b<false, true>(be, rne, P, grid, st, a);
+    } else {
+        if (al) launch_quant_b<true, false>(be, rne, P, grid, st, a);
+        else launch_quant_b<false, false>(be, rne, P, grid, st, a);
+    }
+    return launch_check();
+}
+
+sml_status_t sml_exponents(const float* d_in, uint64_t numel, uint32_t packet_numel,
+                           int8_t* d_exps, void* stream) {
+    if (numel && !d_exps) return SML_ERR_INVALID_ARG;
+    return quantize_common(d_in, numel, packet_numel, 1, nullptr, nullptr, d_exps, 0, stream);
+}
+
+sml_status_t sml_quantize_pack(const float* d_in, uint64_t numel, uint32_t packet_numel,
+                               uint16_t num_workers, const int8_t* d_global_exps,
+                               int32_t* d_payload, int8_t* d_exps_out,
+                               uint32_t flags, void* stream) {
+    if (num_workers == 0) return SML_ERR_INVALID_ARG;
+    if (numel && !d_payload) return SML_ERR_INVALID_ARG;
+    if (d_global_exps && d_exps_out && d_exps_out != d_global_exps) return SML_ERR_INVALID_ARG;
+    return quantize_common(d_in, numel, packet_numel, num_workers, d_global_exps, d_payload,
+                           d_exps_out, flags, stream);
+}
+
+sml_status_t sml_dequantize(const int32_t* d_payload, const int8_t* d_exps, uint64_t numel,
+                            uint32_t packet_numel, uint16_t num_workers, float* d_out,
+                            uint32_t flags, void* stream) {
+    if (!valid_packet(packet_numel)) return SML_ERR_UNSUPPORTED;
+    if (num_workers == 0) return SML_ERR_INVALID_ARG;
+    if (numel == 0) return SML_OK;
+    if (!d_payload || !d_exps || !d_out || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
+    if (!aligned16(d_payload)) return SML_ERR_ALIGNMENT;
+    DequantArgs a;
+    a.payload = reinterpret_cast<const u4*>(d_payload);
+    a.exps = d_exps;
+    a.out = d_out;
+    a.numel = numel;
+    a.ntiles = (numel + kTileElems - 1) / kTileElems;
+    a.W = num_workers;
+    dim3 grid(grid_for_tiles(a.ntiles));
+    hipStream_t st = (hipStream_t)stream;
+    const bool al = aligned16(d_out), be = !(flags & SML_FLAG_PAYLOAD_LE);
+    if (al) { if (be) launch_deq_p<true, true>(packet_numel, grid, st, a); else launch_deq_p<true, false>(packet_numel, grid, st, a); }
+    else    { if (be) launch_deq_p<false, true>(packet_numel, grid, st, a); else launch_deq_p<false, false>(packet_numel, grid, st, a); }
+    return launch_check();
+}
+
+sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t numel,
+                                    uint32_t packet_numel, uint16_t num_workers,
+                                    int32_t* d_payload, int8_t* d_exps_out,
+                                    uint32_t flags, void* stream) {
+    if (!valid_packet(packet_numel)) return SML_ERR_UNSUPPORTED;
+    if (num_workers == 0) return SML_ERR_INVALID_ARG;
+    if (numel == 0) return SML_OK;
+    if (!d_in || !d_out || !aligned4(d_in) || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
+    if (d_payload && !aligned16(d_payload)) return SML_ERR_ALIGNMENT;
+    RoundTripArgs a;
+    a.in = d_in;
+    a.out = d_out;
+    a.numel = numel;
+    a.nblocks = sml_num_blocks(numel, packet_numel);
+    a.ntiles = (a.nblocks * packet_numel + kTileElems - 1) / kTileElems;
+    a.payload = reinterpret_cast<u4*>(d_payload);
+    a.exps_out = d_exps_out;
+    a.W = num_workers;
+    dim3 grid(grid_for_tiles(a.ntiles));
+    hipStream_t st = (hipStream_t)stream;
+    // in and out share the slice offset, so one alignment test covers both
+    // unless the caller passed differently aligned buffers.
+    const bool al = aligned16(d_in) && aligned16(d_out);
+    const bool be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
+    if (al) launch_rt_a<true>(be, rne, packet_numel, grid, st, a);
+    else launch_rt_a<false>(be, rne, packet_numel, grid, st, a);
+    return launch_check();
+}
+
+sml_status_t sml_bswap_i32(const int32_t* d_in, int32_t* d_out, uint64_t numel, void* stream) {
+    if (numel == 0) return SML_OK;
+    if (!d_in || !d_out || !aligned4(d_in) || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    if (aligned16(d_in) && aligned16(d_out)) {
+        uint64_t nvec = numel / 4;
+        if (nvec) k_bswap_vec<<<grid_for_vec(nvec), kBlockThreads, 0, st>>>(
+            reinterpret_cast<const u4*>(d_in), reinterpret_cast<u4*>(d_out), nvec);
+        uint64_t done = nvec * 4;
+        if (done < numel)
+            k_bswap_scalar<<<1, kBlockThreads, 0, st>>>(d_in + done, d_out + done, numel - done);
+    } else {
+        k_bswap_scalar<<<grid_for_vec((numel + 3) / 4), kBlockThreads, 0, st>>>(d_in, d_out, numel);
+    }
+    return launch_check();
+}
+
+sml_status_t sml_loopback_aggregate(int32_t* d_payload, uint64_t count, uint16_t num_workers,
+                                    uint32_t flags, void* stream) {
+    if (num_workers == 0) return SML_ERR_INVALID_ARG;
+    if (count == 0) return SML_OK;
+    if (!d_payload) return SML_ERR_INVALID_ARG;
+    if (!aligned16(d_payload) || (count & 3u)) return SML_ERR_ALIGNMENT;
+    hipStream_t st = (hipStream_t)stream;
+    uint64_t nvec = count / 4;
+    if (flags & SML_FLAG_PAYLOAD_LE)
+        k_loopback<false><<<grid_for_vec(nvec), kBlockThreads, 0, st>>>(reinterpret_cast<u4*>(d_payload), nvec, num_workers);
+    else
+        k_loopback<true><<<grid_for_vec(nvec), kBlockThreads, 0, st>>>(reinterpret_cast<u4*>(d_payload), nvec, num_workers);
+    return launch_check();
+}
+
+}  // extern "C"

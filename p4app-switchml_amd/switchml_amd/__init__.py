@@ -1,0 +1,204 @@
+"""switchml_amd — Python front end of the MI355X-native SwitchML end-host
+pre/post-processor (libswitchml_hip.so, C-ABI in include/switchml_hip.h).
+
+Thin ctypes layer over the C-ABI for tests, bench and the torch.distributed
+switch simulation.  Tensors are torch CUDA (HIP) tensors; every call is
+enqueued on torch's current stream unless a stream is given.  There is no CPU
+fallback: if the HIP library is missing or the tensor is not on the GPU, the
+call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libswitchml_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "switchml_hip.h")
+
+SML_OK = 0
+SML_ERR_INVALID_ARG = 1
+SML_ERR_UNSUPPORTED = 2
+SML_ERR_ALIGNMENT = 3
+SML_ERR_HIP = 4
+
+FLAG_PAYLOAD_LE = 0x1
+FLAG_ROUND_RNE = 0x2
+
+PACKET_NUMELS = (64, 128, 256, 512, 1024)
+
+_lib = None
+
+
+class SwitchMLError(RuntimeError):
+    def __init__(self, fn: str, status: int):
+        L = lib()
+        msg = L.sml_status_string(status).decode()
+        err = L.sml_last_error().decode()
+        super().__init__(f"{fn} failed: {msg}" + (f" ({err})" if err else ""))
+        self.status = status
+
+
+def lib():
+    """Load libswitchml_hip.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not found — build it with `make -C p4app-switchml_amd` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    u64, u32, u16, i32, vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint16, ctypes.c_int, ctypes.c_void_p
+    L.sml_abi_version.restype = i32
+    L.sml_status_string.restype = ctypes.c_char_p
+    L.sml_status_string.argtypes = [i32]
+    L.sml_last_error.restype = ctypes.c_char_p
+    L.sml_num_blocks.restype = u64
+    L.sml_num_blocks.argtypes = [u64, u32]
+    L.sml_scale_lut.restype = i32
+    L.sml_scale_lut.argtypes = [u16, vp]
+    L.sml_scale_lut_device.restype = i32
+    L.sml_scale_lut_device.argtypes = [u16, vp, vp]
+    L.sml_exponents.restype = i32
+    L.sml_exponents.argtypes = [vp, u64, u32, vp, vp]
+    L.sml_quantize_pack.restype = i32
+    L.sml_quantize_pack.argtypes = [vp, u64, u32, u16, vp, vp, vp, u32, vp]
+    L.sml_dequantize.restype = i32
+    L.sml_dequantize.argtypes = [vp, vp, u64, u32, u16, vp, u32, vp]
+    L.sml_bswap_i32.restype = i32
+    L.sml_bswap_i32.argtypes = [vp, vp, u64, vp]
+    L.sml_loopback_aggregate.restype = i32
+    L.sml_loopback_aggregate.argtypes = [vp, u64, u16, u32, vp]
+    L.sml_roundtrip_loopback.restype = i32
+    L.sml_roundtrip_loopback.argtypes = [vp, vp, u64, u32, u16, vp, vp, u32, vp]
+    L.sml_set_grid_limit.restype = u32
+    L.sml_set_grid_limit.argtypes = [u32]
+    _lib = L
+    return L
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Every function the C-ABI header declares (for the export test)."""
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(sml_[a-z0-9_]+)\s*\(", src)))
+
+
+def _check(fn: str, status: int):
+    if status != SML_OK:
+        raise SwitchMLError(fn, status)
+
+
+def num_blocks(numel: int, packet_numel: int = 256) -> int:
+    return int(lib().sml_num_blocks(numel, packet_numel))
+
+
+def set_grid_limit(max_workgroups: int) -> int:
+    return int(lib().sml_set_grid_limit(max_workgroups))
+
+
+# ------------------------------------------------------------- torch glue --
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream(stream):
+    torch = _torch()
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _dev(t, dtype, name):
+    torch = _torch()
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor — the HIP path has no CPU fallback")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def scale_lut(num_workers: int):
+    import numpy as np
+    out = np.empty(256, dtype=np.float32)
+    _check("sml_scale_lut", lib().sml_scale_lut(num_workers, out.ctypes.data))
+    return out
+
+
+def scale_lut_device(num_workers: int, device="cuda", stream=None):
+    torch = _torch()
+    out = torch.empty(256, dtype=torch.float32, device=device)
+    _check("sml_scale_lut_device", lib().sml_scale_lut_device(num_workers, _dev(out, torch.float32, "lut"), _stream(stream)))
+    return out
+
+
+def exponents(x, packet_numel: int = 256, out=None, stream=None):
+    torch = _torch()
+    B = num_blocks(x.numel(), packet_numel)
+    if out is None:
+        out = torch.empty(B, dtype=torch.int8, device=x.device)
+    _check("sml_exponents", lib().sml_exponents(_dev(x, torch.float32, "x"), x.numel(), packet_numel,
+                                                _dev(out, torch.int8, "exps"), _stream(stream)))
+    return out
+
+
+def quantize_pack(x, packet_numel: int = 256, num_workers: int = 1, global_exps=None,
+                  payload=None, exps_out=None, want_exps: bool = True, flags: int = 0, stream=None):
+    """Returns (payload int32[B*P] (BE words unless FLAG_PAYLOAD_LE), exps int8[B] or None)."""
+    torch = _torch()
+    B = num_blocks(x.numel(), packet_numel)
+    if payload is None:
+        payload = torch.empty(B * packet_numel, dtype=torch.int32, device=x.device)
+    if global_exps is None and want_exps and exps_out is None:
+        exps_out = torch.empty(B, dtype=torch.int8, device=x.device)
+    g = None if global_exps is None else _dev(global_exps, torch.int8, "global_exps")
+    e = None if exps_out is None else _dev(exps_out, torch.int8, "exps_out")
+    _check("sml_quantize_pack", lib().sml_quantize_pack(
+        _dev(x, torch.float32, "x"), x.numel(), packet_numel, num_workers, g,
+        _dev(payload, torch.int32, "payload"), e, flags, _stream(stream)))
+    return payload, (global_exps if global_exps is not None else exps_out)
+
+
+def dequantize(payload, exps, numel: int, packet_numel: int = 256, num_workers: int = 1,
+               out=None, flags: int = 0, stream=None):
+    torch = _torch()
+    if out is None:
+        out = torch.empty(numel, dtype=torch.float32, device=payload.device)
+    _check("sml_dequantize", lib().sml_dequantize(
+        _dev(payload, torch.int32, "payload"), _dev(exps, torch.int8, "exps"), numel, packet_numel,
+        num_workers, _dev(out, torch.float32, "out"), flags, _stream(stream)))
+    return out
+
+
+def bswap_i32(x, out=None, stream=None):
+    torch = _torch()
+    if out is None:
+        out = torch.empty_like(x)
+    _check("sml_bswap_i32", lib().sml_bswap_i32(_dev(x, torch.int32, "x"), _dev(out, torch.int32, "out"),
+                                                x.numel(), _stream(stream)))
+    return out
+
+
+def loopback_aggregate(payload, num_workers: int, flags: int = 0, stream=None):
+    torch = _torch()
+    _check("sml_loopback_aggregate", lib().sml_loopback_aggregate(
+        _dev(payload, torch.int32, "payload"), payload.numel(), num_workers, flags, _stream(stream)))
+    return payload
+
+
+def roundtrip_loopback(x, packet_numel: int = 256, num_workers: int = 1, out=None,
+                       payload=None, exps_out=None, flags: int = 0, stream=None):
+    torch = _torch()
+    if out is None:
+        out = torch.empty_like(x)
+    p = None if payload is None else _dev(payload, torch.int32, "payload")
+    e = None if exps_out is None else _dev(exps_out, torch.int8, "exps_out")
+    _check("sml_roundtrip_loopback", lib().sml_roundtrip_loopback(
+        _dev(x, torch.float32, "x"), _dev(out, torch.float32, "out"), x.numel(), packet_numel,
+        num_workers, p, e, flags, _stream(stream)))
+    return out
