@@ -132,10 +132,20 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
                                     int32_t* d_payload, int8_t* d_exps_out,
                                     uint32_t flags, void* stream);
 
+/* Measurement probe (not part of the PPP): copy `bytes` (a multiple of 4 KiB,
+ * 16-B aligned buffers) with the quantize kernel's tile shape and
+ * non-temporal 16-B accesses — the practical HBM ceiling bench.py reports. */
+sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void* stream);
+
 /* Launch-geometry knob for experiments: workgroups per launch for the
  * streaming kernels (0 = one 256-thread workgroup per 4 tiles of 1024
  * elements, i.e. no grid-stride).  Process-wide; returns the previous value. */
 uint32_t sml_set_grid_limit(uint32_t max_workgroups);
+
+/* Cache-policy knob for experiments on the quantize kernel: bit0 = default
+ * (cached) policy for the fp32 loads, bit1 = for the payload stores; 0 (the
+ * default) = non-temporal streaming for both.  Returns the previous value. */
+uint32_t sml_set_cache_policy(uint32_t policy);
 
 #ifdef __cplusplus
 }

@@ -236,6 +236,7 @@ struct QuantArgs {
     u4* payload;          // B*P words, 16-B aligned (nullptr: exponents only)
     int8_t* exps_out;       // nullable
     uint32_t W;
+    uint32_t policy;        // bit0: cached (default-policy) loads, bit1: cached stores
 };
 
 // K1 (fused exponent + quantize + pack), K2 (exponents only: payload == nullptr)
@@ -251,8 +252,14 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
         const uint64_t base = t * kTileElems;
         f4 v[kU];
         if (base + kTileElems <= a.numel) {
+            if (ALIGNED && (a.policy & 1u)) {
 #pragma unroll
-            for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
+                for (int u = 0; u < kU; u++)
+                    v[u] = *reinterpret_cast<const f4*>(a.in + base + (u * kWave + lane) * 4);
+            } else {
+#pragma unroll
+                for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
+            }
         } else {
 #pragma unroll
             for (int u = 0; u < kU; u++) {
@@ -269,7 +276,25 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
             }
         } else {
             tile_exponents<P>(v, e);
-            if (a.exps_out) store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
+            if (a.exps_out) {
+                constexpr int kPk = kTileElems / P;   // packets per tile
+                if (P >= 256 && ((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= a.nblocks * P) {
+                    // e[] is wave-uniform: lane 0 stores the tile's kPk exponent bytes at once.
+                    if (lane == 0) {
+                        int8_t* dst = a.exps_out + base / P;
+                        if constexpr (kPk == 4) {
+                            *reinterpret_cast<uint32_t*>(dst) = (uint32_t)(uint8_t)e[0] | ((uint32_t)(uint8_t)e[1] << 8) |
+                                                                ((uint32_t)(uint8_t)e[2] << 16) | ((uint32_t)(uint8_t)e[3] << 24);
+                        } else if constexpr (kPk == 2) {
+                            *reinterpret_cast<uint16_t*>(dst) = (uint16_t)((uint8_t)e[0] | ((uint8_t)e[2] << 8));
+                        } else {
+                            *dst = (int8_t)e[0];
+                        }
+                    }
+                } else {
+                    store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
+                }
+            }
         }
         if (!a.payload) continue;
 #pragma unroll
@@ -287,7 +312,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
             }
             u4 q = quantize4<RNE>(v[u], s, idx, body);
             if constexpr (BE) { q.x = bswap(q.x); q.y = bswap(q.y); q.z = bswap(q.z); q.w = bswap(q.w); }
-            store_payload(a.payload + idx / 4, q);
+            if (a.policy & 2u) a.payload[idx / 4] = q;
+            else store_payload(a.payload + idx / 4, q);
         }
     }
 }
@@ -427,6 +453,21 @@ __global__ __launch_bounds__(kBlockThreads) void k_bswap_scalar(const int32_t* i
         out[i] = (int32_t)bswap((uint32_t)in[i]);
 }
 
+// Measurement probe (not on the hot path): the same 1024-element tiles, the
+// same non-temporal 16-B loads/stores, no arithmetic — the practical HBM
+// ceiling the quantize kernel is compared against.
+__global__ __launch_bounds__(kBlockThreads) void k_stream_copy(const u4* in, u4* out, uint64_t ntiles) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        u4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) v[u] = __builtin_nontemporal_load(in + t * (kTileElems / 4) + u * kWave + lane);
+#pragma unroll
+        for (int u = 0; u < kU; u++) __builtin_nontemporal_store(v[u], out + t * (kTileElems / 4) + u * kWave + lane);
+    }
+}
+
 __global__ void k_scale_lut(float* lut, uint32_t W) {
     lut[threadIdx.x] = scale_of(W, (int)(int8_t)(uint8_t)threadIdx.x);
 }
@@ -435,6 +476,7 @@ __global__ void k_scale_lut(float* lut, uint32_t W) {
 
 static thread_local char g_last_error[256] = "";
 static uint32_t g_grid_limit = 0;
+static uint32_t g_cache_policy = 0;
 
 static sml_status_t hip_check(hipError_t err) {
     if (err == hipSuccess) return SML_OK;
@@ -546,6 +588,12 @@ uint32_t sml_set_grid_limit(uint32_t max_workgroups) {
     return prev;
 }
 
+uint32_t sml_set_cache_policy(uint32_t policy) {
+    uint32_t prev = g_cache_policy;
+    g_cache_policy = policy;
+    return prev;
+}
+
 uint64_t sml_num_blocks(uint64_t numel, uint32_t packet_numel) {
     if (packet_numel == 0) return 0;
     return (numel * 4 + (uint64_t)packet_numel * 4 - 1) / ((uint64_t)packet_numel * 4);
@@ -583,6 +631,7 @@ static sml_status_t quantize_common(const float* d_in, uint64_t numel, uint32_t 
     a.payload = reinterpret_cast<u4*>(d_payload);
     a.exps_out = d_gexp ? nullptr : d_exps_out;
     a.W = W;
+    a.policy = g_cache_policy;
     dim3 grid(grid_for_tiles(a.ntiles));
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_in), be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
@@ -662,6 +711,15 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
     const bool be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
     if (al) launch_rt_a<true>(be, rne, packet_numel, grid, st, a);
     else launch_rt_a<false>(be, rne, packet_numel, grid, st, a);
+    return launch_check();
+}
+
+sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void* stream) {
+    if (bytes == 0) return SML_OK;
+    if (!d_in || !d_out || !aligned16(d_in) || !aligned16(d_out) || bytes % (kTileElems * 4)) return SML_ERR_ALIGNMENT;
+    const uint64_t ntiles = bytes / (kTileElems * 4);
+    k_stream_copy<<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(
+        reinterpret_cast<const u4*>(d_in), reinterpret_cast<u4*>(d_out), ntiles);
     return launch_check();
 }
 

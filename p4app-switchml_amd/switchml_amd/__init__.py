@@ -74,6 +74,10 @@ def lib():
     L.sml_roundtrip_loopback.argtypes = [vp, vp, u64, u32, u16, vp, vp, u32, vp]
     L.sml_set_grid_limit.restype = u32
     L.sml_set_grid_limit.argtypes = [u32]
+    L.sml_stream_copy.restype = i32
+    L.sml_stream_copy.argtypes = [vp, vp, u64, vp]
+    L.sml_set_cache_policy.restype = u32
+    L.sml_set_cache_policy.argtypes = [u32]
     _lib = L
     return L
 
@@ -96,6 +100,10 @@ def num_blocks(numel: int, packet_numel: int = 256) -> int:
 
 def set_grid_limit(max_workgroups: int) -> int:
     return int(lib().sml_set_grid_limit(max_workgroups))
+
+
+def set_cache_policy(policy: int) -> int:
+    return int(lib().sml_set_cache_policy(policy))
 
 
 # ------------------------------------------------------------- torch glue --
@@ -202,3 +210,11 @@ def roundtrip_loopback(x, packet_numel: int = 256, num_workers: int = 1, out=Non
         _dev(x, torch.float32, "x"), _dev(out, torch.float32, "out"), x.numel(), packet_numel,
         num_workers, p, e, flags, _stream(stream)))
     return out
+
+
+def stream_copy(src, dst, stream=None):
+    """Measurement probe: non-temporal tile copy (src/dst same byte size)."""
+    nbytes = src.numel() * src.element_size()
+    _check("sml_stream_copy", lib().sml_stream_copy(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                                                    nbytes, _stream(stream)))
+    return dst

@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Summarise a profiles/run_profiles.sh run into committed evidence.
+
+Reads gpurun_out/prof_<tag>/{kt,pmc_fetch,pmc_write} (rocprofv3 CSV) and writes
+  profiles/<tag>/kernel_stats.csv     (rocprofv3 --kernel-trace --stats summary, sml kernels)
+  profiles/<tag>/summary.json         (per-kernel avg duration, PMC bytes per launch)
+  profiles/pmc_traffic.json           (what bench.py reports as roofline.traffic)
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM / rocprofv3:
+  FETCH_SIZE and WRITE_SIZE come from separate --pmc passes (TCC slots);
+  both are in KiB (x 1024); on gfx950 FETCH_SIZE reads exactly half of the
+  bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
+  WRITE_SIZE is exact for 16 B/lane streaming stores.
+Only launches of the full bench workload (grid = the bench's grid) are used.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rows(path):
+    with open(path, newline="") as f:
+        return list(csv.DictReader(f))
+
+
+def main(tag="r01", numel=64 * 1024 * 1024, packet_numel=256):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+
+    stats = rows(os.path.join(src, "kt", "kt_kernel_stats.csv"))
+    trace = rows(os.path.join(src, "kt", "kt_kernel_trace.csv"))
+    with open(os.path.join(dst, "kernel_stats.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(stats[0].keys()))
+        w.writeheader()
+        for r in stats:
+            if "sml::" in r["Name"] or "copyBuffer" in r["Name"]:
+                w.writerow(r)
+
+    # full-workload launches: the largest grid seen for the quantize kernel
+    q = [r for r in trace if "k_quantize_pack" in r["Kernel_Name"]]
+    gsz = lambda r: int(r.get("Grid_Size") or r["Grid_Size_X"])
+    grid = max(gsz(r) for r in q)
+    full = [r for r in q if gsz(r) == grid]
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in full]
+
+    def pmc(sub, counter):
+        rr = rows(os.path.join(src, sub, "pmc_counter_collection.csv"))
+        vals = [float(r["Counter_Value"]) for r in rr
+                if "k_quantize_pack" in r["Kernel_Name"] and int(r["Grid_Size"]) == grid
+                and r["Counter_Name"] == counter]
+        return vals
+
+    fetch = pmc("pmc_fetch", "FETCH_SIZE")
+    write = pmc("pmc_write", "WRITE_SIZE")
+    B = -(-numel // packet_numel)
+    alg_read, alg_write = 4 * numel, 4 * numel + B
+    fetch_b = 2 * 1024 * statistics.mean(fetch)
+    write_b = 1024 * statistics.mean(write)
+    summary = {
+        "tag": tag,
+        "kernel": full[0]["Kernel_Name"],
+        "grid_threads": grid,
+        "launches": len(full),
+        "avg_duration_ns": statistics.mean(durs),
+        "median_duration_ns": statistics.median(durs),
+        "algorithmic_bytes_per_launch": alg_read + alg_write,
+        "algorithmic_GBps_at_avg": (alg_read + alg_write) / statistics.mean(durs),
+        "pmc_fetch_size_kib_mean": statistics.mean(fetch),
+        "pmc_write_size_kib_mean": statistics.mean(write),
+        "hbm_read_bytes_per_launch (2 x FETCH_SIZE x 1024)": fetch_b,
+        "hbm_write_bytes_per_launch (WRITE_SIZE x 1024)": write_b,
+        "hbm_bytes_per_launch": fetch_b + write_b,
+        "traffic_over_algorithmic": (fetch_b + write_b) / (alg_read + alg_write),
+    }
+    with open(os.path.join(dst, "summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
+        json.dump({"source": f"profiles/{tag}/summary.json",
+                   "quantize_pack": {"numel": numel, "packet_numel": packet_numel,
+                                     "hbm_bytes_per_launch": round(fetch_b + write_b)}}, f, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main(*(sys.argv[1:2] or ["r01"]))

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Collect the rocprofv3 evidence for the bench's dominant kernel on a GPU box.
+#   1) kernel trace + stats (durations)      -> gpurun_out/prof_<tag>/kt
+#   2) PMC pass FETCH_SIZE (own pass)        -> gpurun_out/prof_<tag>/pmc_fetch
+#   3) PMC pass WRITE_SIZE (own pass)        -> gpurun_out/prof_<tag>/pmc_write
+# FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950 (TCC slots), and
+# --pmc is never combined with sys/runtime/hip traces (gpurun refuses that).
+set -euo pipefail
+TAG=${1:-r01}
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+ARGS="$ROOT/bench.py --steps 20 --warmup 5 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 $ARGS > "$OUT/kt.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_write.log" 2>&1
+echo "profiles done: $OUT"
