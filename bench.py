@@ -241,9 +241,71 @@ def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
     res["roundtrip_fused_GBps"] = round(8 * N / t / 1e9, 1)
     t = timeit(lambda: out.copy_(x))
     res["torch_copy_GBps"] = round(8 * N / t / 1e9, 1)
+    res.update(host_inclusive(sw, torch, x, N, P))
     t = timeit(lambda: sw.stream_copy(x, out, stream=stream))
     res["nt_tile_copy_GBps"] = round(8 * N / t / 1e9, 1)
     return res
+
+
+def host_inclusive(sw, torch, x, N, P, chunk=8 * 1024 * 1024, reps=5):
+    """The path as the reference runs it: the bucket starts in (pinned) host
+    memory — a DPDK mbuf / RDMA buffer — and the packets end there.  Timed:
+    H2D of the fp32 bucket, K1 quantize+pack, D2H of payload + exponents.
+    'serial' = one stream; 'pipelined' = chunks of `chunk` elements on three
+    streams (H2D / kernel / D2H overlap; PCIe is full duplex).  Rates are fp32
+    input bytes per second (4N / t)."""
+    dev = x.device
+    hx = torch.empty(N, dtype=torch.float32, pin_memory=True)
+    hx.copy_(x.cpu())
+    B = sw.num_blocks(N, P)
+    hp = torch.empty(B * P, dtype=torch.int32, pin_memory=True)
+    he = torch.empty(B, dtype=torch.int8, pin_memory=True)
+    dx = torch.empty_like(x)
+    dp = torch.empty(B * P, dtype=torch.int32, device=dev)
+    de = torch.empty(B, dtype=torch.int8, device=dev)
+    s0 = torch.cuda.current_stream()
+
+    def serial():
+        dx.copy_(hx, non_blocking=True)
+        sw.quantize_pack(dx, P, 1, payload=dp, exps_out=de, stream=s0)
+        hp.copy_(dp, non_blocking=True)
+        he.copy_(de, non_blocking=True)
+
+    sa, sb, sc = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    assert chunk % P == 0 and N % chunk == 0
+
+    def pipelined():
+        evs = []
+        for c in range(N // chunk):
+            lo, hi = c * chunk, (c + 1) * chunk
+            blo, bhi = lo // P, hi // P
+            with torch.cuda.stream(sa):
+                dx[lo:hi].copy_(hx[lo:hi], non_blocking=True)
+                e1 = torch.cuda.Event()
+                e1.record(sa)
+            sb.wait_event(e1)
+            sw.quantize_pack(dx[lo:hi], P, 1, payload=dp[lo:hi], exps_out=de[blo:bhi], stream=sb)
+            e2 = torch.cuda.Event()
+            e2.record(sb)
+            sc.wait_event(e2)
+            with torch.cuda.stream(sc):
+                hp[lo:hi].copy_(dp[lo:hi], non_blocking=True)
+                he[blo:bhi].copy_(de[blo:bhi], non_blocking=True)
+            evs.append(e2)
+
+    out = {}
+    for name, fn in (("serial", serial), ("pipelined", pipelined)):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        out[f"host_inclusive_{name}_input_GBps"] = round(4 * N / t / 1e9, 2)
+    ok = bool(torch.equal(hp[: 4 * P].to(dev), sw.quantize_pack(x[: 4 * P], P, 1)[0]))
+    out["host_inclusive_check"] = ok
+    return out
 
 
 if __name__ == "__main__":

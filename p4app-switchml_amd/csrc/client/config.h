@@ -1,0 +1,68 @@
+// config.h — the configuration keys of the SwitchML client that the
+// pre/post-processor path reads (client_lib/src/config.h:35-113 for the
+// general section; backend.dummy keys from configs/dummy.cfg), plus this
+// build's backend.hip section.  The reference parses INI with
+// boost::program_options; here a small INI reader accepts the same files
+// (unknown keys such as backend.dpdk.* are ignored with a warning).
+#ifndef SWITCHML_AMD_CONFIG_H_
+#define SWITCHML_AMD_CONFIG_H_
+
+#include <cstdint>
+#include <string>
+
+namespace switchml {
+
+struct GeneralConfig {
+    uint16_t rank = 0;
+    uint16_t num_workers = 1;
+    uint16_t num_worker_threads = 4;
+    uint32_t max_outstanding_packets = 256;
+    uint64_t packet_numel = 1024;          // code default (config.cc:51); general.cfg ships 256
+    std::string backend = "dummy";
+    std::string scheduler = "fifo";
+    std::string prepostprocessor = "cpu_exponent_quantizer";
+    bool instant_job_completion = false;
+    std::string controller_ip_str = "127.0.0.1";
+    uint16_t controller_port = 50099;
+};
+
+struct DummyBackendConfig {
+    float bandwidth = 1000.0f;             // Mbps; <= 0 disables the simulated wire time
+    bool process_packets = true;           // multiply payloads by num_workers (the "switch")
+};
+
+// MI355X-specific knobs of the loopback backend.
+struct HipBackendConfig {
+    int device = -1;                       // -1: the caller's current HIP device
+    // How a worker thread runs a FLOAT32 job slice:
+    //  "bulk"   : K1 quantize+pack -> K5 x num_workers -> K4 dequantize (planes in HBM)
+    //  "fused"  : one round-trip kernel, no planes (fastest)
+    //  "packet" : the reference's per-LTU PreprocessSingle/PostprocessSingle loop
+    //             (DummyWorkerThread order) — API-parity mode, slow by design
+    std::string mode = "bulk";
+};
+
+struct BackendConfig {
+    DummyBackendConfig dummy;
+    HipBackendConfig hip;
+};
+
+class Config {
+  public:
+    GeneralConfig general_;
+    BackendConfig backend_;
+
+    // Same search order as the reference (config.cc:103-144) when path is
+    // empty: /etc/switchml.cfg, ./switchml.cfg, ./switchml-<hostname>.cfg.
+    bool LoadFromFile(std::string path = "");
+    bool LoadFromString(const std::string& ini);
+    // config.cc:154-213 (general part): mop must give every worker thread a
+    // packet; mop is rounded to a multiple of num_worker_threads.
+    void Validate();
+    std::string ToString() const;
+    void PrintConfig() const;
+};
+
+}  // namespace switchml
+
+#endif  // SWITCHML_AMD_CONFIG_H_

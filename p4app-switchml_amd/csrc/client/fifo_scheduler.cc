@@ -1,0 +1,108 @@
+// fifo_scheduler.cc — see fifo_scheduler.h.
+#include "fifo_scheduler.h"
+
+namespace switchml {
+
+bool Barrier::Wait() {
+    std::unique_lock<std::mutex> lock(m_);
+    if (destroyed_) return false;
+    const uint64_t gen = generation_;
+    if (++count_ == n_) {
+        count_ = 0;
+        generation_++;
+        cv_.notify_all();
+        return true;
+    }
+    cv_.wait(lock, [&] { return generation_ != gen || destroyed_; });
+    return !destroyed_ || generation_ != gen;
+}
+
+void Barrier::Destroy() {
+    std::unique_lock<std::mutex> lock(m_);
+    destroyed_ = true;
+    cv_.notify_all();
+}
+
+void FifoSliceGeometry(Numel numel, int T, int t, Numel* offset, Numel* slice_numel) {
+    Numel n = numel / (Numel)T;
+    const Numel rem = numel % (Numel)T;
+    if (rem > (Numel)t) {
+        n++;
+        *offset = (Numel)t * n;        // every earlier slice also got an extra element
+    } else {
+        *offset = (Numel)t * n + rem;  // the rem extra elements sit before this slice
+    }
+    *slice_numel = n;
+}
+
+FifoScheduler::FifoScheduler(const Config& config)
+    : config_(config), barrier_(config.general_.num_worker_threads) {}
+
+bool FifoScheduler::EnqueueJob(std::shared_ptr<Job> job) {
+    std::unique_lock<std::mutex> lock(access_mutex_);
+    if (stopped_) {
+        job->SetJobStatus(FAILED);
+        return false;
+    }
+    job->SetJobStatus(QUEUED);
+    finished_job_slices_[job->id_] = 0;
+    undispatched_job_slices_[job->id_] = config_.general_.num_worker_threads;
+    queue_.push(job);
+    job_submitted_event_.notify_all();
+    return true;
+}
+
+bool FifoScheduler::GetJobSlice(WorkerTid tid, JobSlice& job_slice) {
+    {
+        std::unique_lock<std::mutex> lock(access_mutex_);
+        if (stopped_) return false;
+    }
+    // All worker threads meet here so that they take slices of the same job.
+    if (!barrier_.Wait()) return false;
+    std::unique_lock<std::mutex> lock(access_mutex_);
+    job_submitted_event_.wait(lock, [this] { return stopped_ || !queue_.empty(); });
+    if (stopped_) return false;
+
+    std::shared_ptr<Job> job = queue_.front();
+    int& left = undispatched_job_slices_.at(job->id_);
+    if (--left == 0) {
+        queue_.pop();
+        undispatched_job_slices_.erase(job->id_);
+    }
+    job_slice.job = job;
+    job_slice.slice = job->tensor_;
+    Numel offset, n;
+    FifoSliceGeometry(job->tensor_.numel, config_.general_.num_worker_threads, tid, &offset, &n);
+    job_slice.slice.numel = n;
+    job_slice.slice.OffsetPtrs(offset);
+    job->SetJobStatus(RUNNING);
+    return true;
+}
+
+bool FifoScheduler::NotifyJobSliceCompletion(WorkerTid, const JobSlice& job_slice) {
+    std::unique_lock<std::mutex> lock(access_mutex_);
+    if (stopped_) {
+        job_slice.job->SetJobStatus(FAILED);
+        return false;
+    }
+    int& done = finished_job_slices_.at(job_slice.job->id_);
+    if (++done == config_.general_.num_worker_threads) {
+        finished_job_slices_.erase(job_slice.job->id_);
+        return true;
+    }
+    return false;
+}
+
+void FifoScheduler::Stop() {
+    std::unique_lock<std::mutex> lock(access_mutex_);
+    stopped_ = true;
+    barrier_.Destroy();
+    while (!queue_.empty()) {
+        queue_.front()->SetJobStatus(FAILED);
+        queue_.pop();
+    }
+    undispatched_job_slices_.clear();
+    job_submitted_event_.notify_all();
+}
+
+}  // namespace switchml

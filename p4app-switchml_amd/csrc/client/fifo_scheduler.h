@@ -1,0 +1,67 @@
+// fifo_scheduler.h — FIFO job scheduler (client_lib/src/scheduler.h:74-112,
+// schedulers/fifo_scheduler.{h,cc}).  Every job is cut into one contiguous
+// slice per worker thread; the slice geometry decides where packets (blocks)
+// start, so it is part of the parity contract.
+#ifndef SWITCHML_AMD_FIFO_SCHEDULER_H_
+#define SWITCHML_AMD_FIFO_SCHEDULER_H_
+
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <queue>
+
+#include "config.h"
+#include "job.h"
+
+namespace switchml {
+
+// Reusable thread barrier that can be torn down to release waiters
+// (the role of utils.cc:43-72 Barrier).
+class Barrier {
+  public:
+    explicit Barrier(int n) : n_(n) {}
+    // Returns false if the barrier was destroyed while waiting.
+    bool Wait();
+    void Destroy();
+
+  private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    int n_;
+    int count_ = 0;
+    uint64_t generation_ = 0;
+    bool destroyed_ = false;
+};
+
+// Slice t of T of a job of numel elements (fifo_scheduler.cc:93-109): the
+// first numel % T slices get one extra element.
+void FifoSliceGeometry(Numel numel, int T, int t, Numel* offset, Numel* slice_numel);
+
+class FifoScheduler {
+  public:
+    explicit FifoScheduler(const Config& config);
+
+    bool EnqueueJob(std::shared_ptr<Job> job);
+    // Blocks (after a barrier with the other worker threads) until a job is
+    // queued or the scheduler stops; false when stopped.
+    bool GetJobSlice(WorkerTid worker_thread_id, JobSlice& job_slice);
+    // True when this completed the job's last slice.
+    bool NotifyJobSliceCompletion(WorkerTid worker_thread_id, const JobSlice& job_slice);
+    // Fail every queued job and wake all waiting worker threads.
+    void Stop();
+
+  private:
+    const Config& config_;
+    std::mutex access_mutex_;
+    std::condition_variable job_submitted_event_;
+    std::queue<std::shared_ptr<Job>> queue_;
+    std::map<JobId, int> undispatched_job_slices_;
+    std::map<JobId, int> finished_job_slices_;
+    Barrier barrier_;
+    bool stopped_ = false;
+};
+
+}  // namespace switchml
+
+#endif  // SWITCHML_AMD_FIFO_SCHEDULER_H_

@@ -1,0 +1,186 @@
+// hip_exponent_quantizer_ppp.cc — see hip_exponent_quantizer_ppp.h.
+#include "hip_exponent_quantizer_ppp.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <string>
+
+#include "switchml_hip.h"
+
+namespace switchml {
+
+static void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw SwitchMLFatal(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+HipExponentQuantizerPPP::HipExponentQuantizerPPP(Config& config, WorkerTid worker_tid, Numel ltu_size,
+                                                 Numel batch_num_ltus)
+    : PrePostProcessor(config, worker_tid, ltu_size, batch_num_ltus) {
+    ltu_numel_ = ltu_size / 4;
+    if (ltu_size % 4 || !(ltu_numel_ == 64 || ltu_numel_ == 128 || ltu_numel_ == 256 || ltu_numel_ == 512 ||
+                          ltu_numel_ == 1024))
+        throw SwitchMLFatal("hip_exponent_quantizer supports packet_numel 64, 128, 256, 512, 1024; got " +
+                            std::to_string(ltu_numel_));
+    hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+}
+
+HipExponentQuantizerPPP::~HipExponentQuantizerPPP() {
+    CleanupJobSlice();
+    if (d_recv_exps_) (void)hipFree(d_recv_exps_);
+    if (d_stage_) (void)hipFree(d_stage_);
+    if (d_stage_exp_) (void)hipFree(d_stage_exp_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void HipExponentQuantizerPPP::check(int status, const char* what) const {
+    if (status != SML_OK)
+        throw SwitchMLFatal(std::string(what) + " failed: " + sml_status_string((sml_status_t)status) + " " +
+                            sml_last_error());
+}
+
+uint64_t HipExponentQuantizerPPP::SetupJobSlice(JobSlice* job_slice) {
+    // ppp.cc:54-62
+    job_slice_ = job_slice;
+    const uint64_t bytes = job_slice->slice.numel * DataTypeSize(job_slice->slice.data_type);
+    total_main_num_ltus_ = (bytes + ltu_size_ - 1) / ltu_size_;
+    batch_num_ltus_ = std::min<uint64_t>(total_main_num_ltus_, batch_max_num_ltus_);
+    return total_main_num_ltus_;
+}
+
+bool HipExponentQuantizerPPP::NeedsExtraBatch() { return job_slice_->slice.data_type == FLOAT32; }
+
+void HipExponentQuantizerPPP::CleanupJobSlice() { job_slice_ = nullptr; }
+
+void HipExponentQuantizerPPP::ensure_single_buffers() {
+    if (!d_stage_) {
+        hip_ok(hipMalloc(&d_stage_, ltu_size_), "hipMalloc");
+        hip_ok(hipMalloc(&d_stage_exp_, 16), "hipMalloc");
+    }
+    if (d_recv_exps_cap_ < total_main_num_ltus_) {
+        if (d_recv_exps_) hip_ok(hipFree(d_recv_exps_), "hipFree");
+        d_recv_exps_cap_ = std::max<uint64_t>(total_main_num_ltus_, 1);
+        hip_ok(hipMalloc(&d_recv_exps_, d_recv_exps_cap_), "hipMalloc");
+    }
+}
+
+// PreprocessSingle — ppp.cc:69-192.
+void HipExponentQuantizerPPP::PreprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
+    const Tensor& s = job_slice_->slice;
+    const uint32_t P = (uint32_t)ltu_numel_;
+    ensure_single_buffers();
+    if (s.data_type == FLOAT32) {
+        if (ltu_id >= batch_num_ltus_) {
+            const uint64_t k = ltu_id - batch_num_ltus_;
+            const uint64_t off = k * P, n = std::min<uint64_t>(P, s.numel - off);
+            check(sml_quantize_pack(static_cast<const float*>(s.in_ptr) + off, n, P, config_.general_.num_workers,
+                                    d_recv_exps_ + k, d_stage_, nullptr, 0, stream_),
+                  "sml_quantize_pack");
+            // only the block's n words are written, as ppp.cc:102-109
+            hip_ok(hipMemcpyAsync(entries_ptr, d_stage_, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+            ltu_id = k + batch_num_ltus_;
+        }
+        if (ltu_id < total_main_num_ltus_) {
+            const uint64_t off = ltu_id * P, n = std::min<uint64_t>(P, s.numel - off);
+            check(sml_exponents(static_cast<const float*>(s.in_ptr) + off, n, P, d_stage_exp_, stream_),
+                  "sml_exponents");
+            hip_ok(hipMemcpyAsync(extra_info, d_stage_exp_, 1, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+        }
+    } else if (s.data_type == INT32) {
+        const uint64_t off = ltu_id * P, n = std::min<uint64_t>(P, s.numel - off);
+        check(sml_bswap_i32(static_cast<const int32_t*>(s.in_ptr) + off, d_stage_, n, stream_), "sml_bswap_i32");
+        hip_ok(hipMemcpyAsync(entries_ptr, d_stage_, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+    } else {
+        throw SwitchMLFatal("unsupported data type");
+    }
+    hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+// PostprocessSingle — ppp.cc:194-299.
+void HipExponentQuantizerPPP::PostprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
+    const Tensor& s = job_slice_->slice;
+    const uint32_t P = (uint32_t)ltu_numel_;
+    ensure_single_buffers();
+    if (s.data_type == FLOAT32) {
+        if (ltu_id >= batch_num_ltus_) {
+            const uint64_t k = ltu_id - batch_num_ltus_;
+            const uint64_t off = k * P, n = std::min<uint64_t>(P, s.numel - off);
+            hip_ok(hipMemcpyAsync(d_stage_, entries_ptr, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+            check(sml_dequantize(d_stage_, d_recv_exps_ + k, n, P, config_.general_.num_workers,
+                                 static_cast<float*>(s.out_ptr) + off, 0, stream_),
+                  "sml_dequantize");
+            ltu_id = k + batch_num_ltus_;
+        }
+        if (ltu_id < total_main_num_ltus_) {
+            // ppp.cc:254-260 stores the scale of the received exponent; the
+            // kernels derive the same scale from the stored exponent.
+            hip_ok(hipMemcpyAsync(d_recv_exps_ + ltu_id, extra_info, 1, hipMemcpyDefault, stream_),
+                   "hipMemcpyAsync");
+        }
+    } else if (s.data_type == INT32) {
+        const uint64_t off = ltu_id * P, n = std::min<uint64_t>(P, s.numel - off);
+        hip_ok(hipMemcpyAsync(d_stage_, entries_ptr, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+        check(sml_bswap_i32(d_stage_, static_cast<int32_t*>(s.out_ptr) + off, n, stream_), "sml_bswap_i32");
+    } else {
+        throw SwitchMLFatal("unsupported data type");
+    }
+    hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+void HipExponentQuantizerPPP::ExponentsBulk(void* exps_plane) {
+    const Tensor& s = job_slice_->slice;
+    if (s.data_type != FLOAT32) return;
+    check(sml_exponents(static_cast<const float*>(s.in_ptr), s.numel, (uint32_t)ltu_numel_,
+                        static_cast<int8_t*>(exps_plane), stream_),
+          "sml_exponents");
+}
+
+void HipExponentQuantizerPPP::PreprocessBulk(void* payload_plane, void* exps_plane, const void* global_exps,
+                                             bool payload_le) {
+    const Tensor& s = job_slice_->slice;
+    if (s.data_type == FLOAT32) {
+        check(sml_quantize_pack(static_cast<const float*>(s.in_ptr), s.numel, (uint32_t)ltu_numel_,
+                                config_.general_.num_workers, static_cast<const int8_t*>(global_exps),
+                                static_cast<int32_t*>(payload_plane),
+                                global_exps ? nullptr : static_cast<int8_t*>(exps_plane),
+                                payload_le ? SML_FLAG_PAYLOAD_LE : 0u, stream_),
+              "sml_quantize_pack");
+    } else {
+        if (payload_le)
+            hip_ok(hipMemcpyAsync(payload_plane, s.in_ptr, s.numel * 4, hipMemcpyDeviceToDevice, stream_),
+                   "hipMemcpyAsync");
+        else
+            check(sml_bswap_i32(static_cast<const int32_t*>(s.in_ptr), static_cast<int32_t*>(payload_plane),
+                                s.numel, stream_),
+                  "sml_bswap_i32");
+    }
+}
+
+void HipExponentQuantizerPPP::PostprocessBulk(const void* payload_plane, const void* global_exps, bool payload_le) {
+    const Tensor& s = job_slice_->slice;
+    if (s.data_type == FLOAT32) {
+        check(sml_dequantize(static_cast<const int32_t*>(payload_plane), static_cast<const int8_t*>(global_exps),
+                             s.numel, (uint32_t)ltu_numel_, config_.general_.num_workers,
+                             static_cast<float*>(s.out_ptr), payload_le ? SML_FLAG_PAYLOAD_LE : 0u, stream_),
+              "sml_dequantize");
+    } else {
+        if (payload_le)
+            hip_ok(hipMemcpyAsync(s.out_ptr, payload_plane, s.numel * 4, hipMemcpyDeviceToDevice, stream_),
+                   "hipMemcpyAsync");
+        else
+            check(sml_bswap_i32(static_cast<const int32_t*>(payload_plane), static_cast<int32_t*>(s.out_ptr),
+                                s.numel, stream_),
+                  "sml_bswap_i32");
+    }
+}
+
+std::shared_ptr<PrePostProcessor> PrePostProcessor::CreateInstance(Config& config, WorkerTid worker_tid,
+                                                                   Numel ltu_size, Numel batch_num_ltus) {
+    const std::string& name = config.general_.prepostprocessor;
+    if (name == "hip_exponent_quantizer" || name == "cpu_exponent_quantizer")
+        return std::make_shared<HipExponentQuantizerPPP>(config, worker_tid, ltu_size, batch_num_ltus);
+    if (name == "bypass") return std::make_shared<BypassPPP>(config, worker_tid, ltu_size, batch_num_ltus);
+    throw SwitchMLFatal("'" + name + "' is not a valid prepostprocessor.");
+}
+
+}  // namespace switchml

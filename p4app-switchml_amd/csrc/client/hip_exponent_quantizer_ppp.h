@@ -1,0 +1,62 @@
+// hip_exponent_quantizer_ppp.h — SwitchML's exponent quantizer PPP on MI355X.
+//
+// Same contract as CpuExponentQuantizerPPP
+// (client_lib/src/prepostprocessors/cpu_exponent_quantizer_ppp.{h,cc}), with
+// the arithmetic done by the gfx950 kernels behind include/switchml_hip.h:
+//   * per-LTU calls keep the reference's packet semantics exactly (packet p
+//     carries the exponent of block p, p < B, and the payload of block p - b,
+//     p >= b; the scale of block k comes from the exponent received with
+//     packet k) — one small kernel launch per call, for packet-driven callers;
+//   * bulk calls process the whole slice in one launch (the fast path).
+// The job slice's in_ptr / out_ptr must be DEVICE memory (the loopback
+// backend stages host tensors); entries / extra-info pointers of the
+// per-LTU calls may be host or device memory.
+#ifndef SWITCHML_AMD_HIP_EXPONENT_QUANTIZER_PPP_H_
+#define SWITCHML_AMD_HIP_EXPONENT_QUANTIZER_PPP_H_
+
+#include <hip/hip_runtime_api.h>
+
+#include "prepostprocessor.h"
+
+namespace switchml {
+
+class HipExponentQuantizerPPP : public PrePostProcessor {
+  public:
+    HipExponentQuantizerPPP(Config& config, WorkerTid worker_tid, Numel ltu_size, Numel batch_num_ltus);
+    ~HipExponentQuantizerPPP() override;
+
+    uint64_t SetupJobSlice(JobSlice* job_slice) override;
+    bool NeedsExtraBatch() override;
+    void PreprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) override;
+    void PostprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) override;
+    void CleanupJobSlice() override;
+
+    void ExponentsBulk(void* exps_plane) override;
+    void PreprocessBulk(void* payload_plane, void* exps_plane, const void* global_exps, bool payload_le) override;
+    void PostprocessBulk(const void* payload_plane, const void* global_exps, bool payload_le) override;
+
+    hipStream_t stream() const { return stream_; }
+    uint64_t total_main_num_ltus() const { return total_main_num_ltus_; }
+    uint64_t batch_num_ltus() const { return batch_num_ltus_; }
+    Numel ltu_numel() const { return ltu_numel_; }
+
+  private:
+    void check(int status, const char* what) const;
+    void ensure_single_buffers();
+
+    JobSlice* job_slice_ = nullptr;
+    uint64_t total_main_num_ltus_ = 0;  // B
+    uint64_t batch_num_ltus_ = 0;       // b
+    Numel ltu_numel_ = 0;               // P (elements per LTU)
+    hipStream_t stream_ = nullptr;
+    // per-LTU mode state: received (global) exponents of the slice, and
+    // device staging for one LTU of entries / one exponent byte
+    int8_t* d_recv_exps_ = nullptr;
+    uint64_t d_recv_exps_cap_ = 0;
+    int32_t* d_stage_ = nullptr;
+    int8_t* d_stage_exp_ = nullptr;
+};
+
+}  // namespace switchml
+
+#endif  // SWITCHML_AMD_HIP_EXPONENT_QUANTIZER_PPP_H_

@@ -1,0 +1,48 @@
+// job.h — Job / JobSlice (client_lib/src/job.h:51-148).
+#ifndef SWITCHML_AMD_JOB_H_
+#define SWITCHML_AMD_JOB_H_
+
+#include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+
+#include "common.h"
+
+namespace switchml {
+
+enum JobStatus { INIT, QUEUED, RUNNING, FINISHED, FAILED };
+
+class Job {
+  public:
+    Job(Tensor tensor, JobType job_type, ExtraJobInfo extra_job_info);
+    Job(const Job&) = delete;
+    Job& operator=(const Job&) = delete;
+
+    // Block until the job is FINISHED or FAILED.
+    void WaitToComplete();
+    JobStatus GetJobStatus() const { return job_status_.load(); }
+    // Statuses only move forward; FINISHED/FAILED wake waiters (job.cc:49-57).
+    void SetJobStatus(JobStatus status);
+
+    const JobId id_;
+    const Tensor tensor_;
+    const JobType job_type_;
+    const ExtraJobInfo extra_job_info_;
+
+  private:
+    static std::atomic<JobId> next_id_;
+    std::atomic<JobStatus> job_status_;
+    std::mutex access_mutex_;
+    std::condition_variable job_finished_event_;
+};
+
+// What a worker thread receives from the scheduler: its contiguous slice.
+struct JobSlice {
+    std::shared_ptr<Job> job;
+    Tensor slice;
+};
+
+}  // namespace switchml
+
+#endif  // SWITCHML_AMD_JOB_H_

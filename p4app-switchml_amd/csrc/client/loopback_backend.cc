@@ -1,0 +1,191 @@
+// loopback_backend.cc — see loopback_backend.h.
+#include "loopback_backend.h"
+
+#include <hip/hip_runtime_api.h>
+#include <time.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <memory>
+#include <string>
+
+#include "context.h"
+#include "hip_exponent_quantizer_ppp.h"
+#include "prepostprocessor.h"
+#include "switchml_hip.h"
+
+namespace switchml {
+
+namespace {
+
+void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw SwitchMLFatal(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void sml_ok(int s, const char* what) {
+    if (s != SML_OK)
+        throw SwitchMLFatal(std::string(what) + ": " + sml_status_string((sml_status_t)s) + " " + sml_last_error());
+}
+
+// Grow-only device buffer owned by one worker thread.
+struct DeviceBuffer {
+    void* p = nullptr;
+    size_t cap = 0;
+    void* get(size_t bytes) {
+        if (bytes > cap) {
+            if (p) hip_ok(hipFree(p), "hipFree");
+            cap = std::max<size_t>(bytes, 4096);
+            hip_ok(hipMalloc(&p, cap), "hipMalloc");
+        }
+        return p;
+    }
+    ~DeviceBuffer() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct WorkerState {
+    DeviceBuffer in, out, payload, exps, ring, ring_extra;
+};
+
+// DummyWorkerThread's per-packet loop (dummy_worker_thread.cc:86-177) with
+// in-order delivery over a device-resident ring of b packets.
+void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerState& ws, bool extra_batch) {
+    const uint64_t P = ppp.ltu_numel();
+    const uint64_t B = ppp.total_main_num_ltus();
+    const uint64_t b = ppp.batch_num_ltus();
+    const uint64_t total = B + (extra_batch ? b : 0);
+    int32_t* ring = static_cast<int32_t*>(ws.ring.get(b * P * 4));
+    uint8_t* extra = static_cast<uint8_t*>(ws.ring_extra.get(b * 2));
+    hip_ok(hipMemsetAsync(ring, 0, b * P * 4, ppp.stream()), "hipMemsetAsync");
+    for (uint64_t p = 0; p < b; p++) ppp.PreprocessSingle(p, ring + (p % b) * P, extra + (p % b) * 2);
+    for (uint64_t p = 0; p < total; p++) {
+        int32_t* ent = ring + (p % b) * P;
+        uint8_t* ex = extra + (p % b) * 2;
+        if (cfg.backend_.dummy.process_packets)  // ProcessPacket: every entry of the packet x W
+            sml_ok(sml_loopback_aggregate(ent, P, cfg.general_.num_workers, 0, ppp.stream()),
+                   "sml_loopback_aggregate");
+        ppp.PostprocessSingle(p, ent, ex);
+        const uint64_t np = p + b;
+        if (np < total) ppp.PreprocessSingle(np, ent, ex);
+    }
+}
+
+uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, JobSlice& js) {
+    auto* ppp = dynamic_cast<HipExponentQuantizerPPP*>(&base);
+    if (!ppp) {  // bypass: count packets, move nothing (bypass_ppp.h)
+        const uint64_t B = base.SetupJobSlice(&js);
+        base.CleanupJobSlice();
+        return B;
+    }
+    hipStream_t st = ppp->stream();
+    Tensor& t = js.slice;
+    const size_t bytes = t.numel * DataTypeSize(t.data_type);
+    const bool in_dev = IsDevicePointer(t.in_ptr);
+    const bool out_dev = IsDevicePointer(t.out_ptr);
+
+    JobSlice staged = js;
+    if (!in_dev) {
+        staged.slice.in_ptr = ws.in.get(bytes);
+        hip_ok(hipMemcpyAsync(staged.slice.in_ptr, t.in_ptr, bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync H2D");
+    }
+    if (!out_dev) staged.slice.out_ptr = (t.out_ptr == t.in_ptr) ? staged.slice.in_ptr : ws.out.get(bytes);
+
+    const uint64_t B = ppp->SetupJobSlice(&staged);
+    const uint64_t P = ppp->ltu_numel();
+    const uint16_t W = cfg.general_.num_workers;
+    const std::string& mode = cfg.backend_.hip.mode;
+    const bool is_float = t.data_type == FLOAT32;
+    uint64_t packets = B + (ppp->NeedsExtraBatch() ? ppp->batch_num_ltus() : 0);
+
+    if (mode == "packet") {
+        run_packet_loop(*ppp, cfg, ws, ppp->NeedsExtraBatch());
+    } else if (mode == "fused" && is_float && cfg.backend_.dummy.process_packets) {
+        sml_ok(sml_roundtrip_loopback(static_cast<const float*>(staged.slice.in_ptr),
+                                      static_cast<float*>(staged.slice.out_ptr), t.numel, (uint32_t)P, W, nullptr,
+                                      nullptr, 0, st),
+               "sml_roundtrip_loopback");
+    } else {  // bulk
+        void* payload = ws.payload.get(B * P * 4);
+        void* exps = ws.exps.get(B);
+        ppp->PreprocessBulk(payload, exps, nullptr, false);
+        if (cfg.backend_.dummy.process_packets)
+            sml_ok(sml_loopback_aggregate(static_cast<int32_t*>(payload), B * P, W, 0, st), "sml_loopback_aggregate");
+        ppp->PostprocessBulk(payload, exps, false);
+    }
+    if (!out_dev)
+        hip_ok(hipMemcpyAsync(t.out_ptr, staged.slice.out_ptr, bytes, hipMemcpyDeviceToHost, st), "hipMemcpyAsync D2H");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    ppp->CleanupJobSlice();
+    return packets;
+}
+
+}  // namespace
+
+bool IsDevicePointer(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+LoopbackBackend::~LoopbackBackend() { CleanupWorker(); }
+
+void LoopbackBackend::SetupWorker() {
+    for (int i = 0; i < config_.general_.num_worker_threads; i++)
+        threads_.emplace_back(&LoopbackBackend::WorkerMain, this, (WorkerTid)i);
+}
+
+void LoopbackBackend::CleanupWorker() {
+    for (auto& t : threads_)
+        if (t.joinable()) t.join();
+    threads_.clear();
+}
+
+void LoopbackBackend::WorkerMain(WorkerTid tid) {
+    const GeneralConfig& g = config_.general_;
+    const bool bypass = g.prepostprocessor == "bypass";
+    std::shared_ptr<PrePostProcessor> ppp;
+    std::string setup_error;
+    try {
+        if (!bypass) hip_ok(hipSetDevice(context_.device()), "hipSetDevice");
+        // dummy_worker_thread.cc:59-62: ltu = packet_numel * 4 bytes, b_max = mop / T
+        ppp = PrePostProcessor::CreateInstance(config_, tid, g.packet_numel * 4,
+                                               g.max_outstanding_packets / g.num_worker_threads);
+    } catch (const std::exception& e) {
+        setup_error = e.what();
+        fprintf(stderr, "[switchml] worker thread %d: %s\n", tid, e.what());
+    }
+    WorkerState ws;
+    JobSlice js;
+    while (context_.GetContextState() == Context::RUNNING) {
+        if (!context_.GetJobSlice(tid, js)) continue;
+        // empty slices and instant_job_completion never touch the PPP
+        // (dummy_worker_thread.cc:87-93)
+        const bool work = js.slice.numel > 0 && !g.instant_job_completion;
+        bool ok = !work || ppp != nullptr;
+        uint64_t packets = 0;
+        if (ok && work) {
+            try {
+                packets = run_slice(*ppp, config_, ws, js);
+            } catch (const std::exception& e) {
+                fprintf(stderr, "[switchml] worker thread %d: job %llu failed: %s\n", tid,
+                        (unsigned long long)js.job->id_, e.what());
+                ok = false;
+            }
+            const float bw = config_.backend_.dummy.bandwidth;
+            if (ok && bw > 0) {  // the dummy backend's simulated wire time (dummy_backend.cc:124-133)
+                const double ns = 1000.0 * (double)packets * g.packet_numel * 4 * 8 * g.num_worker_threads / bw;
+                struct timespec req = {(time_t)(ns / 1e9), (long)((uint64_t)ns % 1000000000ull)};
+                nanosleep(&req, nullptr);
+            }
+            context_.GetStats().AddSlice(tid, packets, js.slice.numel * DataTypeSize(js.slice.data_type));
+        }
+        context_.NotifyJobSliceCompletion(tid, js, ok);
+        js = JobSlice();
+    }
+}
+
+}  // namespace switchml

@@ -1,0 +1,47 @@
+// loopback_backend.h — the "dummy" backend on MI355X
+// (client_lib/src/backends/dummy/dummy_backend.cc, dummy_worker_thread.cc).
+//
+// Each worker thread owns one PrePostProcessor (and its HIP stream) and runs
+// its FIFO slice of every job: pre-process, the loopback "switch" (every
+// payload word x num_workers, exponents unchanged: dummy_backend.cc:72-84),
+// post-process.  Where the reference moves one 1 KiB packet per call through a
+// host ring, this backend moves the whole slice through HBM planes
+// (backend.hip.mode = bulk | fused), or — for API parity — runs the
+// reference's per-packet call sequence over a device ring (mode = packet).
+// Host tensors are staged through device buffers (H2D / D2H on the worker's
+// stream); device tensors are used in place.
+#ifndef SWITCHML_AMD_LOOPBACK_BACKEND_H_
+#define SWITCHML_AMD_LOOPBACK_BACKEND_H_
+
+#include <thread>
+#include <vector>
+
+#include "config.h"
+#include "job.h"
+
+namespace switchml {
+
+class Context;
+class PrePostProcessor;
+
+class LoopbackBackend {
+  public:
+    LoopbackBackend(Context& context, Config& config) : context_(context), config_(config) {}
+    ~LoopbackBackend();
+    void SetupWorker();    // start num_worker_threads worker threads
+    void CleanupWorker();  // join them
+
+  private:
+    void WorkerMain(WorkerTid tid);
+
+    Context& context_;
+    Config& config_;
+    std::vector<std::thread> threads_;
+};
+
+// True if p is HIP device (or managed) memory; false for host memory.
+bool IsDevicePointer(const void* p);
+
+}  // namespace switchml
+
+#endif  // SWITCHML_AMD_LOOPBACK_BACKEND_H_

@@ -1,0 +1,86 @@
+// prepostprocessor.h — the PrePostProcessor (PPP) interface
+// (client_lib/src/prepostprocessor.h:44-147) with the bulk hooks the
+// reference reserved but never defined (prepostprocessor.h:112-116).
+//
+// Per-LTU calls (PreprocessSingle / PostprocessSingle) keep the reference's
+// exact contract so packet-driven backends can call them; the bulk calls are
+// how a GPU PPP is driven: one call per job slice, planes in HBM.
+#ifndef SWITCHML_AMD_PREPOSTPROCESSOR_H_
+#define SWITCHML_AMD_PREPOSTPROCESSOR_H_
+
+#include <memory>
+
+#include "common.h"
+#include "config.h"
+#include "job.h"
+
+namespace switchml {
+
+class PrePostProcessor {
+  public:
+    // Factory keyed by config.general_.prepostprocessor (prepostprocessor.cc:32-41):
+    //   "hip_exponent_quantizer"  -> HipExponentQuantizerPPP (MI355X kernels)
+    //   "cpu_exponent_quantizer"  -> HipExponentQuantizerPPP as well: the drop-in
+    //                                name of the reference's quantizer, same bytes
+    //   "bypass"                  -> BypassPPP
+    // Anything else throws SwitchMLFatal (the reference: LOG(FATAL)).
+    static std::shared_ptr<PrePostProcessor> CreateInstance(Config& config, WorkerTid worker_tid,
+                                                            Numel ltu_size, Numel batch_num_ltus);
+    virtual ~PrePostProcessor() = default;
+    PrePostProcessor(const PrePostProcessor&) = delete;
+    PrePostProcessor& operator=(const PrePostProcessor&) = delete;
+
+    // Returns the number of LTUs (packets) of the slice, excluding the extra batch.
+    virtual uint64_t SetupJobSlice(JobSlice* job_slice) = 0;
+    virtual bool NeedsExtraBatch() = 0;
+    virtual void PreprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info = nullptr) = 0;
+    virtual void PostprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info = nullptr) = 0;
+    virtual void CleanupJobSlice() = 0;
+
+    // ---- bulk hooks (one call per job slice; planes are DEVICE memory) ----
+    // The planes: exps[B] (int8) and payload[B * ltu_numel] (int32, big-endian
+    // wire words unless payload_le), see include/switchml_hip.h.
+    //
+    // Exponent plane only (the values the first batch of packets would carry).
+    virtual void ExponentsBulk(void* exps_plane) { (void)exps_plane; }
+    // Quantize + pack every LTU of the slice.  global_exps == nullptr: use the
+    // slice's own exponents (loopback: the switch returns them unchanged) and
+    // write them to exps_plane; otherwise quantize with the aggregated ones.
+    virtual void PreprocessBulk(void* payload_plane, void* exps_plane, const void* global_exps,
+                                bool payload_le = false) = 0;
+    // Dequantize the aggregated payload with the aggregated exponents into
+    // the slice's out_ptr.
+    virtual void PostprocessBulk(const void* payload_plane, const void* global_exps,
+                                 bool payload_le = false) = 0;
+
+    Numel ltu_size() const { return ltu_size_; }
+
+  protected:
+    PrePostProcessor(Config& config, WorkerTid worker_tid, Numel ltu_size, Numel batch_num_ltus)
+        : config_(config), worker_tid_(worker_tid), ltu_size_(ltu_size), batch_max_num_ltus_(batch_num_ltus) {}
+
+    Config& config_;
+    WorkerTid worker_tid_;
+    Numel ltu_size_;            // bytes per LTU
+    Numel batch_max_num_ltus_;  // max LTUs per batch
+};
+
+// bypass_ppp.h:40-105: counts LTUs, moves no data (packets carry garbage).
+class BypassPPP : public PrePostProcessor {
+  public:
+    BypassPPP(Config& c, WorkerTid t, Numel ltu, Numel batch) : PrePostProcessor(c, t, ltu, batch) {}
+    uint64_t SetupJobSlice(JobSlice* s) override {
+        const uint64_t bytes = s->slice.numel * DataTypeSize(s->slice.data_type);
+        return (bytes + ltu_size_ - 1) / ltu_size_;
+    }
+    bool NeedsExtraBatch() override { return false; }
+    void PreprocessSingle(uint64_t, void*, void*) override {}
+    void PostprocessSingle(uint64_t, void*, void*) override {}
+    void CleanupJobSlice() override {}
+    void PreprocessBulk(void*, void*, const void*, bool) override {}
+    void PostprocessBulk(const void*, const void*, bool) override {}
+};
+
+}  // namespace switchml
+
+#endif  // SWITCHML_AMD_PREPOSTPROCESSOR_H_

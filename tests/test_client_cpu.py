@@ -1,0 +1,117 @@
+"""CPU tests of the C++ client (Context / FIFO scheduler / loopback backend)
+through include/switchml_client.h.  They use the reference's `bypass` PPP
+(bypass_ppp.h: counts packets, moves no data) or instant_job_completion, so
+no GPU is touched: job lifecycle, slicing into packets, config validation."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+
+@pytest.fixture(scope="module")
+def client():
+    from switchml_amd import client as C
+    return C
+
+
+@pytest.fixture
+def ctx(client):
+    yield client
+    if client.state() == client.RUNNING:
+        client.stop()
+
+
+def test_start_stop_states(ctx):
+    C = ctx
+    assert C.state() in (C.CREATED, C.STOPPED)
+    C.start(C.make_config(prepostprocessor="bypass", num_worker_threads=2, bandwidth=0))
+    assert C.state() == C.RUNNING
+    with pytest.raises(C.ContextError):
+        C.start(C.make_config(prepostprocessor="bypass"))   # already running
+    C.stop()
+    assert C.state() == C.STOPPED
+    with pytest.raises(C.ContextError):
+        C.stop()
+
+
+@pytest.mark.parametrize("T", [1, 3, 4, 8])
+@pytest.mark.parametrize("numel", [1, 255, 256, 257, 1_000_003])
+def test_bypass_jobs_slices_and_packet_counts(ctx, T, numel):
+    """Every job is cut into T FIFO slices (fifo_scheduler.cc:93-109); each
+    slice needs ceil(slice_bytes / ltu) packets (bypass has no extra batch)."""
+    C = ctx
+    P = 256
+    C.start(C.make_config(prepostprocessor="bypass", num_worker_threads=T, packet_numel=P,
+                          max_outstanding_packets=256, bandwidth=0))
+    x = np.zeros(numel, dtype=np.float32)
+    jobs = [C.allreduce_async(x) for _ in range(3)]
+    C.wait_for_all_jobs()
+    assert all(j.status() == C.JOB_FINISHED for j in jobs)
+    assert len({j.id for j in jobs}) == 3
+    st = C.stats()
+    expect_packets = 0
+    nonempty = 0
+    for t in range(T):
+        off, n = O.slice_geometry(numel, T, t)
+        expect_packets += O.num_blocks(n, P)
+        nonempty += n > 0
+    assert st["jobs_submitted"] == 3 and st["jobs_finished"] == 3
+    assert st["numel_submitted"] == 3 * numel
+    assert st["slices"] == 3 * nonempty
+    assert st["packets"] == 3 * expect_packets
+    C.stop()
+
+
+def test_instant_job_completion(ctx):
+    C = ctx
+    C.start(C.make_config(prepostprocessor="hip_exponent_quantizer", instant_job_completion=True,
+                          num_worker_threads=4, bandwidth=0, device=0))
+    x = np.ones(1000, dtype=np.float32)
+    j = C.allreduce_async(x)
+    j.wait()
+    assert j.status() == C.JOB_FINISHED
+    assert np.all(x == 1)   # untouched
+    C.stop()
+
+
+def test_config_validation(ctx):
+    C = ctx
+    # max_outstanding_packets rounded to a multiple of num_worker_threads (config.cc:160-170)
+    C.start(C.make_config(prepostprocessor="bypass", num_worker_threads=3, max_outstanding_packets=256, bandwidth=0))
+    assert "max_outstanding_packets = 255" in C.config_text()
+    C.stop()
+    C.start(C.make_config(prepostprocessor="bypass", num_worker_threads=4, max_outstanding_packets=255, bandwidth=0))
+    assert "max_outstanding_packets = 256" in C.config_text()
+    C.stop()
+    for bad in (dict(prepostprocessor="nope"), dict(backend="dpdk"), dict(mode="turbo"),
+                dict(num_worker_threads=8, max_outstanding_packets=4)):
+        kw = dict(prepostprocessor="bypass", bandwidth=0)
+        kw.update(bad)
+        with pytest.raises(C.ContextError):
+            C.start(C.make_config(**kw))
+        if C.state() == C.RUNNING:   # a bad PPP name fails in the workers, not at Start
+            C.stop()
+
+
+def test_bad_ppp_name_fails_jobs_not_process(ctx):
+    C = ctx
+    try:
+        C.start(C.make_config(prepostprocessor="no_such_ppp", bandwidth=0))
+    except C.ContextError:
+        return  # rejected up front is fine too
+    j = C.allreduce_async(np.ones(10, dtype=np.float32))
+    with pytest.raises(C.ContextError):
+        j.wait()
+    assert j.status() == C.JOB_FAILED
+    C.stop()
+
+
+def test_job_wait_after_stop_fails_queued(ctx):
+    C = ctx
+    C.start(C.make_config(prepostprocessor="bypass", num_worker_threads=2, bandwidth=1e-3))  # slow "wire"
+    x = np.zeros(1 << 16, dtype=np.float32)
+    jobs = [C.allreduce_async(x) for _ in range(4)]
+    C.stop()
+    states = [j.status() for j in jobs]
+    assert all(s in (C.JOB_FINISHED, C.JOB_FAILED) for s in states)
+    assert C.JOB_FAILED in states

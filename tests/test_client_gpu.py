@@ -1,0 +1,99 @@
+"""GPU tests of the C++ client: Context::AllReduce through the loopback
+("dummy") backend and the HIP pre/post-processor, in every backend mode,
+against the oracle's restatement of the reference packet loop
+(DummyWorkerThread + CpuExponentQuantizerPPP, T worker-thread slices).
+Bit-exact on the fp32 output words."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "p4app-switchml_amd", "bin")
+
+
+@pytest.fixture
+def C(cuda):
+    from switchml_amd import client
+    yield client
+    if client.state() == client.RUNNING:
+        client.stop()
+
+
+def bits_equal(a, b):
+    return np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32))
+
+
+@pytest.mark.parametrize("mode", ["bulk", "fused", "packet"])
+@pytest.mark.parametrize("T,W,P", [(1, 1, 256), (4, 2, 256), (3, 3, 64), (2, 8, 1024)])
+def test_allreduce_float_host_tensors(C, mode, T, W, P):
+    n = 100_003 if mode != "packet" else 20_011
+    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, max_outstanding_packets=64 * T,
+                          mode=mode, bandwidth=0))
+    x = O.splitmix_normal(T * 100 + W, n)
+    ref = O.dummy_allreduce(x, P=P, max_outstanding_packets=64 * T, num_worker_threads=T, num_workers=W)
+    out = np.empty_like(x)
+    C.allreduce(x, out)
+    assert bits_equal(out, ref)
+    # in place, twice (the allreduce_benchmark --inplace pattern)
+    y = x.copy()
+    C.allreduce(y)
+    C.allreduce(y)
+    ref2 = O.dummy_allreduce(ref, P=P, max_outstanding_packets=64 * T, num_worker_threads=T, num_workers=W)
+    assert bits_equal(y, ref2)
+    C.stop()
+
+
+@pytest.mark.parametrize("mode", ["bulk", "fused"])
+def test_allreduce_device_tensors(C, mode):
+    import torch
+    T, W, P, n = 4, 2, 256, 1_000_003
+    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, mode=mode, bandwidth=0))
+    x = O.splitmix_normal(5, n)
+    xd = torch.from_numpy(x).cuda()
+    outd = torch.empty_like(xd)
+    jobs = [C.allreduce_async(xd, outd) for _ in range(3)]
+    C.wait_for_all_jobs()
+    assert all(j.status() == C.JOB_FINISHED for j in jobs)
+    ref = O.dummy_allreduce(x, P=P, max_outstanding_packets=256, num_worker_threads=T, num_workers=W)
+    assert bits_equal(outd.cpu().numpy(), ref)
+    C.stop()
+
+
+@pytest.mark.parametrize("mode", ["bulk", "packet"])
+def test_allreduce_int32(C, mode):
+    """INT32 jobs: byteswap pre/post, loopback x W with int32 wrap (dummy_backend.cc:72-84)."""
+    T, W, n = 4, 3, 50_001
+    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=256, mode=mode, bandwidth=0))
+    rng = np.random.default_rng(1)
+    x = rng.integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+    out = np.empty_like(x)
+    C.allreduce(x, out)
+    expect = (x.astype(np.int64) * W).astype(np.int32)   # wraps
+    assert np.array_equal(out, expect)
+    C.stop()
+
+
+def test_hello_world_binary(cuda):
+    r = subprocess.run([os.path.join(BIN, "hello_world")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Data verified successfully" in r.stdout
+
+
+@pytest.mark.parametrize("device", ["cpu", "gpu"])
+def test_allreduce_benchmark_cfg1(cuda, device):
+    """configs[0]: allreduce benchmark, loopback backend, 4 MiB float tensor,
+    num_workers = 2 (each of the reference's 2 processes is independent under
+    the dummy backend), --verify with the reference's formula."""
+    r = subprocess.run([os.path.join(BIN, "allreduce_benchmark"), "--tensor-numel", "1048576",
+                        "--tensor-type", "float", "--verify", "true", "--num-workers", "2",
+                        "--bandwidth", "0", "--device", device, "--mode", "bulk"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Data verified successfully." in r.stdout
+    assert "Median" in r.stdout and "Gbps" in r.stdout
