@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--extra", action="store_true", help="also time dequantize / fused round trip / copy")
+    ap.add_argument("--graph-steps", type=int, default=1,
+                    help="capture this many steps per hipGraph replay (1 = eager launches)")
     return ap.parse_args()
 
 
@@ -112,10 +114,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SML_BENCH_REHEARSE=1: rehearse the N>1 path on a 1-GPU box (all ranks on
+    # device local % device_count, gloo instead of RCCL).  Never used for numbers.
+    rehearse = os.environ.get("SML_BENCH_REHEARSE") == "1"
+    ndev = torch.cuda.device_count()
+    local_dev = local % ndev if rehearse else local
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     sw.lib()
     if args.grid_limit:
         sw.set_grid_limit(args.grid_limit)
@@ -130,10 +140,24 @@ def main():
     stream = torch.cuda.current_stream()
     alg_bytes = 8 * N + B
 
-    def step():
-        sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=stream)
+    def launch():
+        sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=torch.cuda.current_stream())
 
-    for _ in range(args.warmup):
+    step, per_call = launch, 1
+    if args.graph_steps > 1:
+        # G consecutive steps captured into one hipGraph (G kernel nodes, the
+        # same launch each time): the Python/ctypes launch path leaves the
+        # timed loop; each replay still runs exactly G full steps.
+        launch()
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(args.graph_steps):
+                launch()
+        step, per_call = graph.replay, args.graph_steps
+        assert args.steps % per_call == 0 and args.warmup % per_call == 0, "steps/warmup must be multiples of --graph-steps"
+
+    for _ in range(args.warmup // per_call):
         step()
     torch.cuda.synchronize()
 
@@ -149,7 +173,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
+    for _ in range(args.steps // per_call):
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
@@ -166,8 +190,15 @@ def main():
     ok = bool(torch.equal(exps[:4].cpu(), sw.exponents(x[:4 * P], P).cpu()))
 
     extra = {}
+    if world > 1 or args.extra:
+        # Switch-sim mode (not the headline): W = world workers all-reduce their
+        # buckets through K2 -> RCCL int8 MAX -> K3 -> RCCL int32 SUM -> K4.
+        try:
+            extra["switchsim"] = switchsim_measure(sw, torch, dist, x, N, P, world, dev)
+        except Exception as e:  # reported, never fatal to the headline line
+            extra["switchsim"] = {"error": repr(e)[:300]}
     if args.extra and rank == 0:
-        extra = extra_measurements(sw, torch, x, payload, exps, N, P, stream)
+        extra.update(extra_measurements(sw, torch, x, payload, exps, N, P, stream))
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
@@ -194,6 +225,7 @@ def main():
                 "num_blocks_per_gpu": B,
                 "parallelism": f"shard{world} (FIFO slices, no data-path collective)",
                 "bytes_per_step_per_gpu": alg_bytes,
+                "launch": "eager" if args.graph_steps <= 1 else f"hipGraph replay, {args.graph_steps} steps per graph",
             },
             "input_GBps": round(world * 4 * N / (elapsed / args.steps) / 1e9, 2),
             "kernel_ms": round(kern_ms_max, 5),
@@ -215,6 +247,28 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def switchsim_measure(sw, torch, dist, x, N, P, world, dev, reps=5):
+    """Time the switch-sim all-reduce of the same 256 MiB bucket per GPU
+    (switchml_amd/switchsim.py); max over ranks.  algbw = 4N / t."""
+    from switchml_amd.switchsim import SwitchSimAllReduce
+    if world == 1 and not dist.is_initialized():
+        return {"note": "single rank: no exchange to time"}
+    ar = SwitchSimAllReduce(N, P, dev)
+    out = torch.empty_like(x)
+    ar(x, out)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ar(x, out)
+    torch.cuda.synchronize()
+    t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = float(t[0])
+    return {"workers": world, "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * N / t / 1e9, 2),
+            "pipeline": "K2 exps -> all_reduce(int8, MAX) -> K3 LE payload -> all_reduce(int32, SUM) -> K4"}
 
 
 def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):

@@ -1,0 +1,124 @@
+"""Multi-process tests of the switch-sim exchange (W workers, world_size 2..3).
+
+CPU (gloo): the exchange steps of switchml_amd.switchsim — the switch's signed
+int8 exponent max and wrapping int32 payload sum — on planes whose values the
+oracle produced per worker, checked against the oracle's software switch
+(orc_switch_exps / orc_switch_payload, p4/exponents.p4:48-54,
+p4/processor.p4:48-54) and against the reference's dequantized sum.
+
+GPU (gloo over one MI355X, both ranks on cuda:0): the full switch-sim
+all-reduce — K2, exchange, K3, exchange, K4 — bit-exact against the oracle's
+lockstep W-worker restatement.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "p4app-switchml_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def worker_data(rank, n):
+    # distinct per-rank magnitudes so the exponent max actually differs
+    return O.splitmix_normal(1000 + rank, n) * np.float32(4.0 ** (rank - 1))
+
+
+def _cpu_exchange(rank, world, port, n, P, q):
+    try:
+        dist = _init(rank, world, port)
+        from switchml_amd import switchsim
+        xs = [worker_data(r, n) for r in range(world)]
+        local_exps = [O.exponents(x, P) for x in xs]
+        e = torch.from_numpy(local_exps[rank].copy())
+        switchsim.exchange_exponents(e)
+        g = O.switch_exps(local_exps)
+        ok_e = np.array_equal(e.numpy(), g)
+        pls_be = [O.quantize(x, P, world, global_exps=g) for x in xs]
+        le = torch.from_numpy(O.bswap32(pls_be[rank]).view(np.int32).copy())
+        switchsim.exchange_payload(le)
+        agg_be = O.switch_payload(pls_be)
+        ok_p = np.array_equal(O.bswap32(le.numpy().view(np.uint32)), agg_be)
+        out = O.dequantize(agg_be, g, n, P, world)
+        ref = np.sum(np.stack(xs).astype(np.float64), axis=0)
+        rel = np.max(np.abs(out - ref)) / np.max(np.abs(ref))
+        q.put((rank, ok_e, ok_p, float(rel)))
+        dist.destroy_process_group()
+    except Exception as ex:  # pragma: no cover - reported to the parent
+        q.put((rank, False, False, repr(ex)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_gloo_cpu(world):
+    n, P = 20_011, 256
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cpu_exchange, args=(r, world, port, n, P, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok_e, ok_p, rel in res:
+        assert ok_e and ok_p, (rank, rel)
+        assert rel < 1e-6
+
+
+def _gpu_switchsim(rank, world, port, n, P, q):
+    try:
+        dist = _init(rank, world, port)
+        from switchml_amd import switchsim
+        dev = torch.device("cuda:0")
+        x = worker_data(rank, n)
+        out = switchsim.allreduce(torch.from_numpy(x).to(dev), P)
+        xs = [worker_data(r, n) for r in range(world)]
+        g = O.switch_exps([O.exponents(xx, P) for xx in xs])
+        agg = O.switch_payload([O.quantize(xx, P, world, global_exps=g) for xx in xs])
+        ref = O.dequantize(agg, g, n, P, world)
+        ok = np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        q.put((rank, ok, ""))
+        dist.destroy_process_group()
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, False, repr(ex)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [64, 256, 1024])
+def test_switchsim_allreduce_two_workers_one_gpu(cuda, P):
+    world, n = 2, 100_003
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_switchsim, args=(r, world, port, n, P, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, err in res:
+        assert ok, (rank, err)
