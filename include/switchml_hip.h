@@ -142,10 +142,9 @@ sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void
  * elements, i.e. no grid-stride).  Process-wide; returns the previous value. */
 uint32_t sml_set_grid_limit(uint32_t max_workgroups);
 
-/* Cache-policy knob for experiments on the quantize kernel: bit0 = default
- * (cached) policy for the fp32 loads, bit1 = for the payload stores; 0 (the
- * default) = non-temporal streaming for both.  Returns the previous value. */
-uint32_t sml_set_cache_policy(uint32_t policy);
+/* Experiment knob: tiles (1024 elements) per wave per loop iteration of the
+ * quantize kernel, 1 (default) or 2.  Returns the previous value. */
+uint32_t sml_set_tiles_per_wave(uint32_t tiles);
 
 #ifdef __cplusplus
 }

@@ -162,17 +162,30 @@ __device__ __forceinline__ void store_payload(u4* dst, u4 q) {
 
 // ---------------------------------------------------- per-packet reductions
 
-// Max of `m` over the P/4 lanes of this lane's packet (P <= 256), via
-// butterfly exchanges inside the lane group.
+// Max of `m` over the P/4 lanes of this lane's packet (P <= 256).
+// Inside each 16-lane row: four DPP steps (quad_perm xor 1, quad_perm xor 2,
+// row_half_mirror, row_mirror) leave the row max in every lane of the row,
+// with no LDS traffic.  Across rows: v_readlane of lanes 0/16/32/48 into
+// SGPRs — for P >= 256 the packet max is then wave-uniform (scalar).
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
 template <int P>
 __device__ __forceinline__ uint32_t group_max(uint32_t m) {
-    constexpr int kLanes = P / 4 < kWave ? P / 4 : kWave;
-#pragma unroll
-    for (int off = 1; off < kLanes; off <<= 1) {
-        uint32_t o = (uint32_t)__shfl_xor((int)m, off, kWave);
-        m = m > o ? m : o;
-    }
-    return m;
+    static_assert(P == 64 || P == 128 || P == 256, "row-based reduce covers 16..64 lanes");
+    m = umax(m, dpp<0xB1>(m));    // quad_perm [1,0,3,2]
+    m = umax(m, dpp<0x4E>(m));    // quad_perm [2,3,0,1]
+    m = umax(m, dpp<0x141>(m));   // row_half_mirror
+    m = umax(m, dpp<0x140>(m));   // row_mirror
+    if constexpr (P == 64) return m;
+    const uint32_t r0 = __builtin_amdgcn_readlane(m, 0), r1 = __builtin_amdgcn_readlane(m, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(m, 32), r3 = __builtin_amdgcn_readlane(m, 48);
+    if constexpr (P == 128) return (threadIdx.x & 32) ? umax(r2, r3) : umax(r0, r1);
+    return umax(umax(r0, r1), umax(r2, r3));
 }
 
 __device__ __forceinline__ uint32_t max4(f4 v) {
@@ -219,9 +232,25 @@ __device__ __forceinline__ void store_exponents(int8_t* exps_out, uint64_t tile_
     }
 }
 
+// scale_of for W = 2^k without the double division: 2147483647 / 2^(e+k)
+// rounds to 2^(31-e-k) (normal range for every int8 e and k <= 16), +inf when
+// 31-e-k > 127, and 0 when W * 2^e overflows float (e + k >= 128).
+__device__ __forceinline__ float scale_of_pow2(uint32_t log2W, int e) {
+    const int m = e + (int)log2W;
+    if (m >= 128) return 0.0f;
+    const int x = 31 - m;                      // result 2^x
+    if (x > 127) return __builtin_huge_valf();
+    return __uint_as_float((uint32_t)(x + 127) << 23);
+}
+
+// The scale every kernel uses (power-of-two W takes the division-free form).
+__device__ __forceinline__ float scale_for(uint32_t W, int e) {
+    return (W & (W - 1)) == 0 ? scale_of_pow2(31 - __builtin_clz(W), e) : scale_of(W, e);
+}
+
 // Per-workgroup scale table, lut[(uint8_t)e], built once per launch-block.
 __device__ __forceinline__ void build_lut(float* lut, uint32_t W) {
-    lut[threadIdx.x] = scale_of(W, (int)(int8_t)(uint8_t)threadIdx.x);
+    lut[threadIdx.x] = scale_for(W, (int)(int8_t)(uint8_t)threadIdx.x);
     __syncthreads();
 }
 
@@ -236,85 +265,95 @@ struct QuantArgs {
     u4* payload;          // B*P words, 16-B aligned (nullptr: exponents only)
     int8_t* exps_out;       // nullable
     uint32_t W;
-    uint32_t policy;        // bit0: cached (default-policy) loads, bit1: cached stores
 };
 
+template <bool ALIGNED>
+__device__ __forceinline__ void load_tile(const QuantArgs& a, uint64_t base, int lane, f4 (&v)[kU]) {
+    if (base + kTileElems <= a.numel) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
+    } else {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            v[u] = load4_guarded(a.in + idx, idx, a.numel);
+        }
+    }
+}
+
+// Exponents, quantize and pack of one loaded tile.
+template <int P, bool GLOBAL, bool BE, bool RNE>
+__device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, int lane, const f4 (&v)[kU],
+                                           const float* lut) {
+    const uint64_t padded = a.nblocks * P;
+    int e[kU];
+    if constexpr (GLOBAL) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            uint64_t pkt = (base + (uint64_t)(u * kWave + lane) * 4) / P;
+            e[u] = pkt < a.nblocks ? (int)a.gexp[pkt] : 0;
+        }
+    } else {
+        tile_exponents<P>(v, e);
+        if (a.exps_out) {
+            constexpr int kPk = kTileElems / P;   // packets per tile
+            if (P >= 256 && ((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= padded) {
+                // e[] is wave-uniform: lane 0 stores the tile's kPk exponent bytes at once
+                // (per-packet byte stores cost ~10 %: partial-line writes).
+                if (lane == 0) {
+                    int8_t* dst = a.exps_out + base / P;
+                    if constexpr (kPk == 4) {
+                        *reinterpret_cast<uint32_t*>(dst) = (uint32_t)(uint8_t)e[0] | ((uint32_t)(uint8_t)e[1] << 8) |
+                                                            ((uint32_t)(uint8_t)e[2] << 16) | ((uint32_t)(uint8_t)e[3] << 24);
+                    } else if constexpr (kPk == 2) {
+                        *reinterpret_cast<uint16_t*>(dst) = (uint16_t)((uint8_t)e[0] | ((uint8_t)e[2] << 8));
+                    } else {
+                        *dst = (int8_t)e[0];
+                    }
+                }
+            } else {
+                store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
+            }
+        }
+    }
+    if (!a.payload) return;
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+        const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+        if (idx >= padded) continue;
+        const float s = lut[(uint8_t)e[u]];
+        uint64_t body = 0;
+        if constexpr (RNE) {
+            // VCL body = first n - n%16 elements of the block; only the last
+            // (partial) block has a scalar half-away tail.
+            const uint64_t blk0 = idx / P * P;
+            const uint64_t n = a.numel - blk0 < (uint64_t)P ? a.numel - blk0 : (uint64_t)P;
+            body = blk0 + (n - n % 16);
+        }
+        u4 q = quantize4<RNE>(v[u], s, idx, body);
+        if constexpr (BE) { q.x = bswap(q.x); q.y = bswap(q.y); q.z = bswap(q.z); q.w = bswap(q.w); }
+        store_payload(a.payload + idx / 4, q);
+    }
+}
+
 // K1 (fused exponent + quantize + pack), K2 (exponents only: payload == nullptr)
-// and K3 (given global exponents: GLOBAL = true).
-template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
+// and K3 (given global exponents: GLOBAL = true).  TPW consecutive tiles per
+// wave per iteration: all their loads are issued before any arithmetic.
+template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE, int TPW>
 __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
     __shared__ float lut[256];
     if (a.payload) build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t padded = a.nblocks * P;
-    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
-        const uint64_t base = t * kTileElems;
-        f4 v[kU];
-        if (base + kTileElems <= a.numel) {
-            if (ALIGNED && (a.policy & 1u)) {
+    const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    for (uint64_t t = wave * TPW; t < a.ntiles; t += nwaves * TPW) {
+        f4 v[TPW][kU];
 #pragma unroll
-                for (int u = 0; u < kU; u++)
-                    v[u] = *reinterpret_cast<const f4*>(a.in + base + (u * kWave + lane) * 4);
-            } else {
+        for (int k = 0; k < TPW; k++)
+            if (k == 0 || t + k < a.ntiles) load_tile<ALIGNED>(a, (t + k) * kTileElems, lane, v[k]);
 #pragma unroll
-                for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kU; u++) {
-                uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-                v[u] = load4_guarded(a.in + idx, idx, a.numel);
-            }
-        }
-        int e[kU];
-        if constexpr (GLOBAL) {
-#pragma unroll
-            for (int u = 0; u < kU; u++) {
-                uint64_t pkt = (base + (uint64_t)(u * kWave + lane) * 4) / P;
-                e[u] = pkt < a.nblocks ? (int)a.gexp[pkt] : 0;
-            }
-        } else {
-            tile_exponents<P>(v, e);
-            if (a.exps_out) {
-                constexpr int kPk = kTileElems / P;   // packets per tile
-                if (P >= 256 && ((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= a.nblocks * P) {
-                    // e[] is wave-uniform: lane 0 stores the tile's kPk exponent bytes at once.
-                    if (lane == 0) {
-                        int8_t* dst = a.exps_out + base / P;
-                        if constexpr (kPk == 4) {
-                            *reinterpret_cast<uint32_t*>(dst) = (uint32_t)(uint8_t)e[0] | ((uint32_t)(uint8_t)e[1] << 8) |
-                                                                ((uint32_t)(uint8_t)e[2] << 16) | ((uint32_t)(uint8_t)e[3] << 24);
-                        } else if constexpr (kPk == 2) {
-                            *reinterpret_cast<uint16_t*>(dst) = (uint16_t)((uint8_t)e[0] | ((uint8_t)e[2] << 8));
-                        } else {
-                            *dst = (int8_t)e[0];
-                        }
-                    }
-                } else {
-                    store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
-                }
-            }
-        }
-        if (!a.payload) continue;
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-            if (idx >= padded) continue;
-            const float s = lut[(uint8_t)e[u]];
-            uint64_t body = 0;
-            if constexpr (RNE) {
-                // VCL body = first n - n%16 elements of the block; only the last
-                // (partial) block has a scalar half-away tail.
-                const uint64_t blk0 = idx / P * P;
-                const uint64_t n = a.numel - blk0 < (uint64_t)P ? a.numel - blk0 : (uint64_t)P;
-                body = blk0 + (n - n % 16);
-            }
-            u4 q = quantize4<RNE>(v[u], s, idx, body);
-            if constexpr (BE) { q.x = bswap(q.x); q.y = bswap(q.y); q.z = bswap(q.z); q.w = bswap(q.w); }
-            if (a.policy & 2u) a.payload[idx / 4] = q;
-            else store_payload(a.payload + idx / 4, q);
-        }
+        for (int k = 0; k < TPW; k++)
+            if (k == 0 || t + k < a.ntiles) quant_tile<P, GLOBAL, BE, RNE>(a, (t + k) * kTileElems, lane, v[k], lut);
     }
 }
 
@@ -469,14 +508,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_stream_copy(const u4* in, u4*
 }
 
 __global__ void k_scale_lut(float* lut, uint32_t W) {
-    lut[threadIdx.x] = scale_of(W, (int)(int8_t)(uint8_t)threadIdx.x);
+    lut[threadIdx.x] = scale_for(W, (int)(int8_t)(uint8_t)threadIdx.x);
 }
 
 // ------------------------------------------------------------ host side
 
 static thread_local char g_last_error[256] = "";
 static uint32_t g_grid_limit = 0;
-static uint32_t g_cache_policy = 0;
 
 static sml_status_t hip_check(hipError_t err) {
     if (err == hipSuccess) return SML_OK;
@@ -510,14 +548,26 @@ static inline uint32_t grid_for_vec(uint64_t nvec) {
 }
 
 // Dispatch tables: runtime (P, alignment, mode) -> template instance.
+template <bool ALIGNED, bool GLOBAL, bool BE, bool RNE, int TPW>
+static void launch_quant_t(uint32_t P, dim3 grid, hipStream_t st, const QuantArgs& a) {
+    switch (P) {
+        case 64:   k_quantize_pack<64, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_quantize_pack<128, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_quantize_pack<256, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_quantize_pack<512, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_quantize_pack<1024, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
+static uint32_t g_tiles_per_wave = 1;
+
 template <bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
 static void launch_quant_p(uint32_t P, dim3 grid, hipStream_t st, const QuantArgs& a) {
-    switch (P) {
-        case 64:   k_quantize_pack<64, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_quantize_pack<128, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_quantize_pack<256, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_quantize_pack<512, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_quantize_pack<1024, ALIGNED, GLOBAL, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+    if (g_tiles_per_wave == 2) {
+        dim3 g2((grid.x + 1) / 2);
+        launch_quant_t<ALIGNED, GLOBAL, BE, RNE, 2>(P, g2, st, a);
+    } else {
+        launch_quant_t<ALIGNED, GLOBAL, BE, RNE, 1>(P, grid, st, a);
     }
 }
 
@@ -588,9 +638,9 @@ uint32_t sml_set_grid_limit(uint32_t max_workgroups) {
     return prev;
 }
 
-uint32_t sml_set_cache_policy(uint32_t policy) {
-    uint32_t prev = g_cache_policy;
-    g_cache_policy = policy;
+uint32_t sml_set_tiles_per_wave(uint32_t tpw) {
+    uint32_t prev = g_tiles_per_wave;
+    g_tiles_per_wave = tpw == 2 ? 2 : 1;
     return prev;
 }
 
@@ -631,7 +681,6 @@ static sml_status_t quantize_common(const float* d_in, uint64_t numel, uint32_t 
     a.payload = reinterpret_cast<u4*>(d_payload);
     a.exps_out = d_gexp ? nullptr : d_exps_out;
     a.W = W;
-    a.policy = g_cache_policy;
     dim3 grid(grid_for_tiles(a.ntiles));
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_in), be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;

@@ -76,8 +76,8 @@ def lib():
     L.sml_set_grid_limit.argtypes = [u32]
     L.sml_stream_copy.restype = i32
     L.sml_stream_copy.argtypes = [vp, vp, u64, vp]
-    L.sml_set_cache_policy.restype = u32
-    L.sml_set_cache_policy.argtypes = [u32]
+    L.sml_set_tiles_per_wave.restype = u32
+    L.sml_set_tiles_per_wave.argtypes = [u32]
     _lib = L
     return L
 
@@ -102,8 +102,8 @@ def set_grid_limit(max_workgroups: int) -> int:
     return int(lib().sml_set_grid_limit(max_workgroups))
 
 
-def set_cache_policy(policy: int) -> int:
-    return int(lib().sml_set_cache_policy(policy))
+def set_tiles_per_wave(tiles: int) -> int:
+    return int(lib().sml_set_tiles_per_wave(tiles))
 
 
 # ------------------------------------------------------------- torch glue --

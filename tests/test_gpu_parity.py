@@ -84,7 +84,7 @@ SIZES = (1, 3, 63, 64, 65, 255, 256, 257, 1000, 1023, 1024, 1025, 4096 + 17, 100
 
 # ---------------------------------------------------------------- scales --
 
-@pytest.mark.parametrize("W", [1, 2, 3, 5, 7, 8, 255, 1000, 65535])
+@pytest.mark.parametrize("W", [1, 2, 3, 4, 5, 7, 8, 16, 255, 256, 1000, 1024, 32768, 65535])
 def test_scale_lut_device_equals_host_and_oracle(cuda, W):
     dev = host(sw().scale_lut_device(W, device=cuda))
     hst = sw().scale_lut(W)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Interleaved A/B sweep of launch geometry and cache policy for the bench
+"""Interleaved A/B sweep of launch geometry (grid cap, tiles per wave) for the bench
 kernel (sml_quantize_pack, K1) on one GPU: every variant is timed in each
 round, rounds repeat, medians reported (cdna_hip_programming.md §5.4 rule 24).
 Also times a torch device copy of the same bytes as a practical ceiling."""
@@ -20,6 +20,7 @@ def main():
     N = int(os.environ.get("SWEEP_NUMEL", 64 * 1024 * 1024))
     P = int(os.environ.get("SWEEP_P", 256))
     rounds = int(os.environ.get("SWEEP_ROUNDS", 7))
+    W = int(os.environ.get("SWEEP_W", 1))
     reps = 10
     dev = torch.device("cuda:0")
     x = torch.randn(N, device=dev)
@@ -29,11 +30,11 @@ def main():
     out = torch.empty_like(x)
     st = torch.cuda.current_stream()
     alg = 8 * N + B
-    grids = [0, 512, 1024, 2048, 4096, 8192]
-    policies = [0, 1, 2, 3]
-    variants = list(itertools.product(grids, policies))
+    grids = [int(g) for g in os.environ.get("SWEEP_GRIDS", "0,4096,8192").split(",")]
+    tpws = [int(t) for t in os.environ.get("SWEEP_TPW", "1,2").split(",")]
+    variants = list(itertools.product(grids, tpws))
     res = {v: [] for v in variants}
-    copy = []
+    copy, ntcopy = [], []
 
     def t_of(fn):
         fn()
@@ -46,22 +47,24 @@ def main():
         return a.elapsed_time(b) / reps * 1e-3
 
     for _ in range(rounds):
-        for g, pol in variants:
+        for g, tpw in variants:
             sw.set_grid_limit(g)
-            sw.set_cache_policy(pol)
-            res[(g, pol)].append(t_of(lambda: sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=st)))
+            sw.set_tiles_per_wave(tpw)
+            res[(g, tpw)].append(t_of(lambda: sw.quantize_pack(x, P, W, payload=payload, exps_out=exps, stream=st)))
+        sw.set_grid_limit(0)
+        sw.set_tiles_per_wave(1)
         copy.append(t_of(lambda: out.copy_(x)))
-    sw.set_grid_limit(0)
-    sw.set_cache_policy(0)
+        ntcopy.append(t_of(lambda: sw.stream_copy(x, out, stream=st)))
     rows = []
-    for (g, pol), ts in res.items():
+    for (g, tpw), ts in res.items():
         m = statistics.median(ts)
-        rows.append({"grid_limit": g, "policy": pol, "median_us": round(m * 1e6, 2),
+        rows.append({"grid_limit": g, "tiles_per_wave": tpw, "median_us": round(m * 1e6, 2),
                      "min_us": round(min(ts) * 1e6, 2), "GBps": round(alg / m / 1e9, 1)})
     rows.sort(key=lambda r: r["median_us"])
-    cm = statistics.median(copy)
-    print(json.dumps({"numel": N, "P": P, "copy_us": round(cm * 1e6, 2), "copy_GBps": round(8 * N / cm / 1e9, 1),
-                      "variants": rows}, indent=1))
+    cm, nm = statistics.median(copy), statistics.median(ntcopy)
+    print(json.dumps({"numel": N, "P": P, "W": W, "torch_copy_us": round(cm * 1e6, 2),
+                      "torch_copy_GBps": round(8 * N / cm / 1e9, 1), "nt_tile_copy_us": round(nm * 1e6, 2),
+                      "nt_tile_copy_GBps": round(8 * N / nm / 1e9, 1), "variants": rows}, indent=1))
 
 
 if __name__ == "__main__":
