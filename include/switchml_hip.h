@@ -133,8 +133,9 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
                                     uint32_t flags, void* stream);
 
 /* Measurement probe (not part of the PPP): copy `bytes` (a multiple of 4 KiB,
- * 16-B aligned buffers) with the quantize kernel's tile shape and
- * non-temporal 16-B accesses — the practical HBM ceiling bench.py reports. */
+ * 16-B aligned buffers) with the quantize kernel's tile shape and access
+ * policy (non-temporal loads, default-policy stores) — the practical HBM
+ * ceiling bench.py reports. */
 sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void* stream);
 
 /* Launch-geometry knob for experiments: workgroups per launch for the

@@ -26,6 +26,8 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=9, reps=10):
         libs.append(L)
     st = torch.cuda.current_stream()
     res = {p: [] for p in paths}
+    cres = {p: [] for p in paths}
+    out = torch.empty_like(x)
     for p, L in zip(paths, libs):  # correctness: identical bytes
         assert L.sml_quantize_pack(x.data_ptr(), N, P, 1, None, payload.data_ptr(), exps.data_ptr(), 0, st.cuda_stream) == 0
         torch.cuda.synchronize()
@@ -42,9 +44,23 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=9, reps=10):
             b.record(st)
             torch.cuda.synchronize()
             res[p].append(a.elapsed_time(b) / reps * 1e3)
+            if hasattr(L, "sml_stream_copy"):
+                L.sml_stream_copy.restype = ctypes.c_int
+                L.sml_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+                a.record(st)
+                for _ in range(reps):
+                    L.sml_stream_copy(x.data_ptr(), out.data_ptr(), 4 * N, st.cuda_stream)
+                b.record(st)
+                torch.cuda.synchronize()
+                cres[p].append(a.elapsed_time(b) / reps * 1e3)
     alg = 8 * N + B
-    print(json.dumps({p: {"median_us": round(statistics.median(v), 2), "min_us": round(min(v), 2),
-                          "GBps": round(alg / statistics.median(v) / 1e3, 1)} for p, v in res.items()}, indent=1))
+    rep = {}
+    for p, v in res.items():
+        rep[p] = {"median_us": round(statistics.median(v), 2), "min_us": round(min(v), 2),
+                  "GBps": round(alg / statistics.median(v) / 1e3, 1)}
+        if cres[p]:
+            rep[p]["copy_probe_GBps"] = round(8 * N / statistics.median(cres[p]) / 1e3, 1)
+    print(json.dumps(rep, indent=1))
 
 
 if __name__ == "__main__":
