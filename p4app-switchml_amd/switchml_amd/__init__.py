@@ -122,8 +122,9 @@ def _stream(stream):
 
 def _dev(t, dtype, name):
     torch = _torch()
-    if not isinstance(t, torch.Tensor) or not t.is_cuda:
-        raise TypeError(f"{name} must be a CUDA (HIP) tensor — the HIP path has no CPU fallback")
+    if not isinstance(t, torch.Tensor) or not (t.is_cuda or t.is_pinned()):
+        raise TypeError(f"{name} must be a CUDA (HIP) tensor or pinned host memory (read by the "
+                        "kernel over PCIe) — the HIP path has no CPU fallback")
     if t.dtype != dtype:
         raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
     if not t.is_contiguous():
