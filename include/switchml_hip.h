@@ -132,6 +132,44 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
                                     int32_t* d_payload, int8_t* d_exps_out,
                                     uint32_t flags, void* stream);
 
+/* ---- DPDK/UDP wire frames --------------------------------
+ * The DPDK backend builds one Ethernet frame per packet
+ * (client_lib/src/backends/dpdk/dpdk_worker_thread_utils.inc:67-135,
+ * BuildPacket): Eth(14) + IPv4(20) + UDP(8) + SwitchML header(8:
+ * job_type_size, short_job_id, pkt_id (host order), switch_pool_index (BE))
+ * + 2-byte extra info (byte 0 = exponent) + packet_numel BE int32 words at
+ * offset 52.  Frame p of a job slice (p in [0, B + b), b = min(batch_max, B))
+ * carries exps[p] (p < B) and payload block p - b (p >= b), its pool index
+ * PktId2PoolIndex(p, start, shift, max_outstanding) (:42-52).
+ * Addresses are given in network byte order, as DpdkBackend::E2eAddress. */
+typedef struct sml_frame_params {
+    uint8_t dst_mac[6];               /* the switch's MAC */
+    uint8_t src_mac[6];               /* the worker thread's MAC */
+    uint32_t src_ip_be, dst_ip_be;    /* worker, switch (network order) */
+    uint16_t src_port_be, dst_port_be;
+    uint64_t job_id;                  /* low 8 bits -> short_job_id */
+    uint32_t pool_index_start;        /* switch_pool_index_start of the worker thread */
+    uint32_t pool_index_shift;        /* switch_pool_index_shift carried across jobs */
+    uint32_t max_outstanding_pkts;    /* per worker thread */
+} sml_frame_params;
+
+/* Bytes of one frame: 52 + 4 * packet_numel. */
+uint64_t sml_frame_bytes(uint32_t packet_numel);
+
+/* Fused K1 -> frames: quantize + pack one job slice straight into B + b
+ * frames at `frame_stride` bytes apart (>= sml_frame_bytes, multiple of 4).
+ * `frames` may be device memory or pinned, device-mapped host memory (the
+ * NIC's buffers: the kernel then writes them over PCIe).  d_global_exps as
+ * for sml_quantize_pack.  Bytes the reference leaves stale (extra-info byte
+ * 1, the exponent of frames p >= B, the payload of frames p < b, IPv4
+ * identification/TOS/fragment) are written as 0; IPv4 and UDP checksums are
+ * left for NIC offload exactly as BuildPacket does (IP 0, UDP = pseudo-header
+ * sum, rte_ipv4_phdr_cksum). */
+sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_t packet_numel,
+                                      uint16_t num_workers, const int8_t* d_global_exps,
+                                      uint32_t batch_max, const sml_frame_params* params,
+                                      void* frames, uint64_t frame_stride, void* stream);
+
 /* Measurement probe (not part of the PPP): copy `bytes` (a multiple of 4 KiB,
  * 16-B aligned buffers) with the quantize kernel's tile shape and access
  * policy (non-temporal loads, default-policy stores) — the practical HBM

@@ -63,6 +63,10 @@ def lib():
         L.orc_dummy_allreduce.argtypes = [vp, vp, u64, u64, u32, i32, u16, i32, i32]
         L.orc_dummy_packet_stream.restype = i32
         L.orc_dummy_packet_stream.argtypes = [vp, u64, u64, u32, u16, vp, vp, vp]
+        L.orc_build_frames.restype = i32
+        L.orc_build_frames.argtypes = [vp, u64, u64, u16, vp, u32, vp, vp, u64]
+        L.orc_pkt_id_to_pool_index.restype = ctypes.c_uint16
+        L.orc_pkt_id_to_pool_index.argtypes = [u64, u32, u32, u32]
         L.orc_glibc_rand.argtypes = [u32, u64, vp]
         L.orc_ref_random_floats.argtypes = [u32, u64, vp]
         _lib = L
@@ -171,6 +175,27 @@ def dummy_packet_stream(x: np.ndarray, P: int = 256, batch_max: int = 64, num_wo
     if rc != 0:
         raise RuntimeError("orc_dummy_packet_stream failed")
     return pe, pp.reshape(B + b, P), out, b
+
+
+def build_frames(x: np.ndarray, params, P: int = 256, num_workers: int = 1, batch_max: int = 64,
+                 global_exps=None, stride: int | None = None) -> np.ndarray:
+    """DPDK frames of one slice (BuildPacket + PreprocessSingle per packet).
+    `params` is a ctypes structure with sml_frame_params' layout."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    B = num_blocks(x.size, P)
+    b = min(B, batch_max)
+    stride = stride or 52 + 4 * P
+    out = np.zeros((B + b) * stride, dtype=np.uint8)
+    ge = None if global_exps is None else np.ascontiguousarray(global_exps, dtype=np.int8)
+    rc = lib().orc_build_frames(_p(x), x.size, P, num_workers, None if ge is None else _p(ge), batch_max,
+                                ctypes.cast(ctypes.byref(params), ctypes.c_void_p), _p(out), stride)
+    if rc != 0:
+        raise RuntimeError("orc_build_frames failed")
+    return out
+
+
+def pool_index(pkt_id, start, shift, mop) -> int:
+    return int(lib().orc_pkt_id_to_pool_index(pkt_id, start, shift, mop))
 
 
 # ------------------------------------------- independent numpy restatement --

@@ -383,3 +383,91 @@ void orc_ref_random_floats(uint32_t seed, uint64_t n, float* out) {
     }
     free(r);
 }
+
+/* ------------------------------------------------------------------------ */
+/* DPDK frames.                                               */
+
+uint16_t orc_pkt_id_to_pool_index(uint64_t pkt_id, uint32_t start, uint32_t shift, uint32_t mop) {
+    /* dpdk_worker_thread_utils.inc:42-52 */
+    uint32_t i = (uint32_t)((pkt_id + shift) % (2ull * mop));
+    if (i < mop) return (uint16_t)(start + i);
+    return (uint16_t)((start + (i - mop)) | 0x8000);
+}
+
+/* rte_raw_cksum over a buffer: sum of the 16-bit words as they sit in memory
+ * (little-endian host), folded twice; rte_ipv4_phdr_cksum returns it as is. */
+static uint16_t raw_cksum(const uint8_t* b, size_t len) {
+    uint32_t sum = 0;
+    for (size_t i = 0; i + 1 < len; i += 2) sum += (uint32_t)b[i] | ((uint32_t)b[i + 1] << 8);
+    if (len & 1) sum += b[len - 1];
+    sum = (sum & 0xffff) + (sum >> 16);
+    sum = (sum & 0xffff) + (sum >> 16);
+    return (uint16_t)sum;
+}
+
+static void put16be(uint8_t* p, uint16_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+
+int orc_build_frames(const float* in, uint64_t numel, uint64_t P, uint16_t W, const int8_t* global_exps,
+                     uint32_t batch_max, const orc_frame_params* prm, uint8_t* frames, uint64_t stride) {
+    const uint64_t B = orc_num_blocks(numel, P);
+    const uint64_t b = B < batch_max ? B : batch_max;
+    const uint64_t data_len = 14 + 20 + 8 + 8 + P * 4 + 2;
+    if (stride < data_len) return -1;
+    float lut[256];
+    orc_scale_lut(W, lut);
+    for (uint64_t p = 0; p < B + b; p++) {
+        uint8_t* f = frames + p * stride;
+        memset(f, 0, data_len);
+        /* 1. Ethernet */
+        memcpy(f + 0, prm->dst_mac, 6);
+        memcpy(f + 6, prm->src_mac, 6);
+        put16be(f + 12, 0x0800);
+        /* 2. IPv4 */
+        uint8_t* ip = f + 14;
+        ip[0] = 0x45;
+        put16be(ip + 2, (uint16_t)(data_len - 14));
+        ip[8] = 128;          /* ttl */
+        ip[9] = 17;           /* IPPROTO_UDP */
+        memcpy(ip + 12, &prm->src_ip_be, 4);
+        memcpy(ip + 16, &prm->dst_ip_be, 4);
+        /* 3. UDP */
+        uint8_t* udp = ip + 20;
+        memcpy(udp + 0, &prm->src_port_be, 2);
+        memcpy(udp + 2, &prm->dst_port_be, 2);
+        put16be(udp + 4, (uint16_t)(data_len - 34));
+        uint8_t psd[12];
+        memcpy(psd + 0, ip + 12, 4);
+        memcpy(psd + 4, ip + 16, 4);
+        psd[8] = 0;
+        psd[9] = ip[9];
+        put16be(psd + 10, (uint16_t)(data_len - 14 - 20)); /* l3 len - ihl*4 */
+        uint16_t ck = raw_cksum(psd, 12);
+        memcpy(udp + 6, &ck, 2);
+        /* 4. SwitchML header */
+        uint8_t* h = udp + 8;
+        uint8_t len_enum = P < 64 ? 0 : P < 128 ? 1 : P < 256 ? 2 : 3;
+        h[0] = (uint8_t)((1 << 4) + len_enum);
+        h[1] = (uint8_t)prm->job_id;
+        uint32_t pid = (uint32_t)p;
+        memcpy(h + 2, &pid, 4); /* host order */
+        put16be(h + 6, orc_pkt_id_to_pool_index(p, prm->pool_index_start, prm->pool_index_shift,
+                                                prm->max_outstanding_pkts));
+        /* PreprocessSingle(p, entries = h + 10, extra = h + 8) — ppp.cc:69-156 */
+        uint8_t* extra = h + 8;
+        uint8_t* entries = h + 10;
+        if (p >= b) {
+            uint64_t k = p - b, off = k * P, n = numel - off < P ? numel - off : P;
+            int8_t e = global_exps ? global_exps[k] : orc_block_exponent(in + off, n);
+            float sc = lut[(uint8_t)e];
+            for (uint64_t i = 0; i < n; i++) {
+                uint32_t w = orc_quantize_value(in[off + i], sc);
+                memcpy(entries + 4 * i, &w, 4);
+            }
+        }
+        if (p < B) {
+            uint64_t off = p * P, n = numel - off < P ? numel - off : P;
+            extra[0] = (uint8_t)orc_block_exponent(in + off, n);
+        }
+    }
+    return 0;
+}

@@ -103,6 +103,26 @@ int orc_dummy_packet_stream(const float* in, uint64_t numel, uint64_t P,
                             uint32_t batch_max, uint16_t num_workers,
                             int8_t* pkt_exps, uint32_t* pkt_payload, float* out);
 
+/* DPDK frame builder restatement — BuildPacket
+ * (backends/dpdk/dpdk_worker_thread_utils.inc:67-135), PktId2PoolIndex (:42-52),
+ * DPDK's rte_ipv4_phdr_cksum / rte_raw_cksum (DPDK 20.x, the reference's
+ * un-vendored submodule; published algorithm: ones-complement 16-bit sum of
+ * the 12-byte pseudo header, folded, not inverted) and PreprocessSingle per
+ * packet.  params layout = sml_frame_params of include/switchml_hip.h.
+ * Bytes the reference leaves stale are written as 0. */
+typedef struct orc_frame_params {
+    uint8_t dst_mac[6];
+    uint8_t src_mac[6];
+    uint32_t src_ip_be, dst_ip_be;
+    uint16_t src_port_be, dst_port_be;
+    uint64_t job_id;
+    uint32_t pool_index_start, pool_index_shift, max_outstanding_pkts;
+} orc_frame_params;
+uint16_t orc_pkt_id_to_pool_index(uint64_t pkt_id, uint32_t start, uint32_t shift, uint32_t mop);
+int orc_build_frames(const float* in, uint64_t numel, uint64_t P, uint16_t num_workers,
+                     const int8_t* global_exps, uint32_t batch_max, const orc_frame_params* prm,
+                     uint8_t* frames, uint64_t stride);
+
 /* glibc random()/rand() TYPE_3 generator restated (srand(seed) then n calls),
  * and the reference's random-float generator built on it:
  * bits = (r%2)<<31 | (r%254)<<23 | r%(1<<23)  (allreduce_benchmark/main.cc:197-205). */

@@ -358,6 +358,99 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
     }
 }
 
+// ---------------------------------------------------------- DPDK frames
+
+struct FrameArgs {
+    const float* in;
+    uint64_t numel;
+    uint64_t nblocks;       // B
+    uint64_t ntiles;        // ceil(B*P / 1024)
+    uint64_t b;             // extra-batch size = min(batch_max, B)
+    const int8_t* gexp;     // global exponents or nullptr
+    uint8_t* frames;        // B + b frames, 4-byte aligned
+    uint64_t stride;        // bytes between frames, multiple of 4
+    uint32_t W;
+    uint32_t pool_start, pool_shift, mop;
+    uint32_t hdr[11];       // frame bytes 0..43: Eth, IPv4, UDP, job_type_size, short_job_id
+};
+
+// PktId2PoolIndex, dpdk_worker_thread_utils.inc:42-52.
+__device__ __forceinline__ uint32_t pool_index(uint64_t p, const FrameArgs& a) {
+    const uint32_t i = (uint32_t)((p + a.pool_shift) % (2ull * a.mop));
+    return i < a.mop ? ((a.pool_start + i) & 0xffffu) : (((a.pool_start + (i - a.mop)) | 0x8000u) & 0xffffu);
+}
+
+// Lanes 0..12 write the 52 header bytes of frame p (one dword each):
+// dwords 0-10 constant, 11 = pkt_id (host order), 12 = pool index (BE16),
+// exponent byte, zero byte.
+__device__ __forceinline__ void write_frame_header(const FrameArgs& a, uint64_t p, int lane, uint32_t exp_byte) {
+    if (lane > 12) return;
+    uint32_t dw = a.hdr[0];
+#pragma unroll
+    for (int i = 1; i < 11; i++) dw = lane == i ? a.hdr[i] : dw;
+    if (lane == 11) dw = (uint32_t)p;
+    if (lane == 12) {
+        const uint32_t pool = pool_index(p, a);
+        dw = (pool >> 8) | ((pool & 0xffu) << 8) | ((exp_byte & 0xffu) << 16);
+    }
+    *reinterpret_cast<uint32_t*>(a.frames + p * a.stride + 4 * lane) = dw;
+}
+
+// Fused quantize + pack into DPDK frames (BuildPacket + PreprocessSingle for
+// every packet of the slice, dpdk_worker_thread_utils.inc:67-135 + ppp.cc:69-156).
+template <int P, bool ALIGNED, bool GLOBAL>
+__global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) {
+    __shared__ float lut[256];
+    build_lut(lut, a.W);
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t padded = a.nblocks * P;
+    constexpr int kPk = kTileElems / P;        // packets per tile
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
+        const uint64_t base = t * kTileElems;
+        QuantArgs qa;                           // reuse the K1 tile loader
+        qa.in = a.in;
+        qa.numel = a.numel;
+        f4 v[kU];
+        load_tile<ALIGNED>(qa, base, lane, v);
+        int eloc[kU];
+        tile_exponents<P>(v, eloc);
+        // headers (and the zero payload of extra-batch frames) of this tile's packets
+#pragma unroll
+        for (int j = 0; j < kPk; j++) {
+            const uint64_t pk = base / P + j;
+            if (pk >= a.nblocks) break;
+            // the exponent of packet pk: slice u = j*P/256, lane (j*P/4) % 64
+            constexpr int kLanesPerPk = P / 4 < kWave ? P / 4 : kWave;
+            const int u = (j * P) / 256;
+            uint32_t e = 0;
+#pragma unroll
+            for (int uu = 0; uu < kU; uu++)
+                if (uu == u) e = (uint32_t)__builtin_amdgcn_readlane(eloc[uu], (j * kLanesPerPk) % kWave);
+            write_frame_header(a, pk, lane, e);
+            if (pk + a.b >= a.nblocks) write_frame_header(a, pk + a.b, lane, 0u);
+            if (pk < a.b) {
+                uint32_t* pl = reinterpret_cast<uint32_t*>(a.frames + pk * a.stride + 52);
+                for (int i = lane; i < P; i += kWave) pl[i] = 0u;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            if (idx >= padded) continue;
+            const uint64_t k = idx / P;
+            int e = eloc[u];
+            if constexpr (GLOBAL) e = a.gexp[k];
+            const u4 q = quantize4<false>(v[u], lut[(uint8_t)e], idx, 0);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(a.frames + (k + a.b) * a.stride + 52) + (idx - k * P);
+            dst[0] = bswap(q.x);
+            dst[1] = bswap(q.y);
+            dst[2] = bswap(q.z);
+            dst[3] = bswap(q.w);
+        }
+    }
+}
+
 struct DequantArgs {
     const u4* payload;
     const int8_t* exps;
@@ -613,6 +706,17 @@ static void launch_rt_a(bool be, bool rne, uint32_t P, dim3 g, hipStream_t st, c
     else    { if (rne) launch_rt_p<ALIGNED, false, true>(P, g, st, a); else launch_rt_p<ALIGNED, false, false>(P, g, st, a); }
 }
 
+template <bool ALIGNED, bool GLOBAL>
+static void launch_frames_p(uint32_t P, dim3 grid, hipStream_t st, const FrameArgs& a) {
+    switch (P) {
+        case 64:   k_quantize_frames<64, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_quantize_frames<128, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_quantize_frames<256, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_quantize_frames<512, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_quantize_frames<1024, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
 }  // namespace sml
 
 using namespace sml;
@@ -762,6 +866,64 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
     const bool be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
     if (al) launch_rt_a<true>(be, rne, packet_numel, grid, st, a);
     else launch_rt_a<false>(be, rne, packet_numel, grid, st, a);
+    return launch_check();
+}
+
+uint64_t sml_frame_bytes(uint32_t packet_numel) { return 52ull + 4ull * packet_numel; }
+
+sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_t P, uint16_t W,
+                                      const int8_t* d_global_exps, uint32_t batch_max,
+                                      const sml_frame_params* prm, void* frames, uint64_t stride, void* stream) {
+    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
+    if (W == 0 || !prm || batch_max == 0) return SML_ERR_INVALID_ARG;
+    if (numel == 0) return SML_OK;
+    if (!d_in || !aligned4(d_in) || !frames) return SML_ERR_INVALID_ARG;
+    if (!aligned4(frames) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
+    FrameArgs a;
+    a.in = d_in;
+    a.numel = numel;
+    a.nblocks = sml_num_blocks(numel, P);
+    a.ntiles = (a.nblocks * P + kTileElems - 1) / kTileElems;
+    a.b = a.nblocks < batch_max ? a.nblocks : batch_max;
+    a.gexp = d_global_exps;
+    a.frames = static_cast<uint8_t*>(frames);
+    a.stride = stride;
+    a.W = W;
+    a.pool_start = prm->pool_index_start;
+    a.pool_shift = prm->pool_index_shift;
+    a.mop = prm->max_outstanding_pkts ? prm->max_outstanding_pkts : 1;
+    // Constant header bytes 0..43 (BuildPacket, dpdk_worker_thread_utils.inc:76-126).
+    uint8_t h[44];
+    memset(h, 0, sizeof(h));
+    const uint32_t data_len = (uint32_t)sml_frame_bytes(P);
+    memcpy(h + 0, prm->dst_mac, 6);
+    memcpy(h + 6, prm->src_mac, 6);
+    h[12] = 0x08; h[13] = 0x00;                              // RTE_ETHER_TYPE_IPV4
+    h[14] = 0x45;                                            // version_ihl
+    h[16] = (uint8_t)((data_len - 14) >> 8); h[17] = (uint8_t)(data_len - 14);
+    h[22] = 128;                                             // time_to_live
+    h[23] = 17;                                              // IPPROTO_UDP
+    memcpy(h + 26, &prm->src_ip_be, 4);
+    memcpy(h + 30, &prm->dst_ip_be, 4);
+    memcpy(h + 34, &prm->src_port_be, 2);
+    memcpy(h + 36, &prm->dst_port_be, 2);
+    h[38] = (uint8_t)((data_len - 34) >> 8); h[39] = (uint8_t)(data_len - 34);
+    // udp->dgram_cksum = rte_ipv4_phdr_cksum(ip, ol_flags): raw 16-bit sum of the pseudo header
+    uint8_t psd[12] = {h[26], h[27], h[28], h[29], h[30], h[31], h[32], h[33], 0, 17,
+                       (uint8_t)((data_len - 34) >> 8), (uint8_t)(data_len - 34)};
+    uint32_t sum = 0;
+    for (int i = 0; i < 12; i += 2) sum += (uint32_t)psd[i] | ((uint32_t)psd[i + 1] << 8);
+    sum = (sum & 0xffff) + (sum >> 16);
+    sum = (sum & 0xffff) + (sum >> 16);
+    h[40] = (uint8_t)sum; h[41] = (uint8_t)(sum >> 8);
+    h[42] = (uint8_t)((1 << 4) + (P < 64 ? 0 : P < 128 ? 1 : P < 256 ? 2 : 3));  // job_type_size
+    h[43] = (uint8_t)prm->job_id;                                                // short_job_id
+    memcpy(a.hdr, h, 44);
+    dim3 grid(grid_for_tiles(a.ntiles));
+    hipStream_t st = (hipStream_t)stream;
+    const bool al = aligned16(d_in);
+    if (d_global_exps) { if (al) launch_frames_p<true, true>(P, grid, st, a); else launch_frames_p<false, true>(P, grid, st, a); }
+    else               { if (al) launch_frames_p<true, false>(P, grid, st, a); else launch_frames_p<false, false>(P, grid, st, a); }
     return launch_check();
 }
 

@@ -31,6 +31,34 @@ PACKET_NUMELS = (64, 128, 256, 512, 1024)
 _lib = None
 
 
+class FrameParams(ctypes.Structure):
+    """sml_frame_params (include/switchml_hip.h): addresses in network byte order."""
+    _fields_ = [("dst_mac", ctypes.c_uint8 * 6), ("src_mac", ctypes.c_uint8 * 6),
+                ("src_ip_be", ctypes.c_uint32), ("dst_ip_be", ctypes.c_uint32),
+                ("src_port_be", ctypes.c_uint16), ("dst_port_be", ctypes.c_uint16),
+                ("job_id", ctypes.c_uint64), ("pool_index_start", ctypes.c_uint32),
+                ("pool_index_shift", ctypes.c_uint32), ("max_outstanding_pkts", ctypes.c_uint32)]
+
+
+def frame_params(dst_mac=b"\x02\x00\x00\x00\x00\x01", src_mac=b"\x02\x00\x00\x00\x00\x02",
+                 src_ip="10.0.0.1", dst_ip="10.0.0.253", src_port=4000, dst_port=48879, job_id=0,
+                 pool_index_start=0, pool_index_shift=0, max_outstanding_pkts=64) -> FrameParams:
+    import socket
+    import struct
+    fp = FrameParams()
+    fp.dst_mac[:] = list(dst_mac)
+    fp.src_mac[:] = list(src_mac)
+    fp.src_ip_be = struct.unpack("<I", socket.inet_aton(src_ip))[0]
+    fp.dst_ip_be = struct.unpack("<I", socket.inet_aton(dst_ip))[0]
+    fp.src_port_be = socket.htons(src_port)
+    fp.dst_port_be = socket.htons(dst_port)
+    fp.job_id = job_id
+    fp.pool_index_start = pool_index_start
+    fp.pool_index_shift = pool_index_shift
+    fp.max_outstanding_pkts = max_outstanding_pkts
+    return fp
+
+
 class SwitchMLError(RuntimeError):
     def __init__(self, fn: str, status: int):
         L = lib()
@@ -76,6 +104,10 @@ def lib():
     L.sml_set_grid_limit.argtypes = [u32]
     L.sml_stream_copy.restype = i32
     L.sml_stream_copy.argtypes = [vp, vp, u64, vp]
+    L.sml_frame_bytes.restype = u64
+    L.sml_frame_bytes.argtypes = [u32]
+    L.sml_quantize_pack_frames.restype = i32
+    L.sml_quantize_pack_frames.argtypes = [vp, u64, u32, u16, vp, u32, ctypes.POINTER(FrameParams), vp, u64, vp]
     L.sml_set_tiles_per_wave.restype = u32
     L.sml_set_tiles_per_wave.argtypes = [u32]
     _lib = L
@@ -219,3 +251,26 @@ def stream_copy(src, dst, stream=None):
     _check("sml_stream_copy", lib().sml_stream_copy(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
                                                     nbytes, _stream(stream)))
     return dst
+
+
+def frame_bytes(packet_numel: int = 256) -> int:
+    return int(lib().sml_frame_bytes(packet_numel))
+
+
+def quantize_pack_frames(x, params: FrameParams, packet_numel: int = 256, num_workers: int = 1,
+                         batch_max: int = 64, global_exps=None, frames=None, stride: int | None = None,
+                         stream=None):
+    """Fused quantize + pack straight into DPDK frames (B + b frames of
+    `stride` bytes, uint8).  `frames` may be a device tensor or pinned host
+    memory (the NIC's buffers)."""
+    torch = _torch()
+    B = num_blocks(x.numel(), packet_numel)
+    b = min(B, batch_max)
+    stride = stride or frame_bytes(packet_numel)
+    if frames is None:
+        frames = torch.empty((B + b) * stride, dtype=torch.uint8, device=x.device)
+    g = None if global_exps is None else _dev(global_exps, torch.int8, "global_exps")
+    _check("sml_quantize_pack_frames", lib().sml_quantize_pack_frames(
+        _dev(x, torch.float32, "x"), x.numel(), packet_numel, num_workers, g, batch_max,
+        ctypes.byref(params), _dev(frames, torch.uint8, "frames"), stride, _stream(stream)))
+    return frames

@@ -1,0 +1,119 @@
+"""DPDK wire frames: the fused quantize-into-frames kernel
+against the oracle's restatement of BuildPacket + PreprocessSingle
+(client_lib/src/backends/dpdk/dpdk_worker_thread_utils.inc:42-135,
+ppp.cc:69-156).  Byte-exact over every frame's data_len bytes.
+
+DPDK itself is an un-vendored submodule (DPDK 20.x, make-based build; commit
+not recorded) and is not in the image, so its two helpers on this path are
+restated from their published algorithms: rte_ipv4_phdr_cksum = rte_raw_cksum
+(ones-complement 16-bit sum, folded, not inverted) of the 12-byte pseudo
+header; header field layouts = rte_ether_hdr / rte_ipv4_hdr / rte_udp_hdr.
+"""
+import socket
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+
+def params(**kw):
+    import switchml_amd as sw
+    return sw.frame_params(**kw)
+
+
+# ---------------------------------------------------------------- CPU --
+
+def test_oracle_frame_fields():
+    P, n, W = 256, 3000, 2
+    fp = params(job_id=0x1234, pool_index_start=64, pool_index_shift=10, max_outstanding_pkts=8,
+                src_ip="10.0.0.1", dst_ip="10.0.0.253", src_port=4000, dst_port=48879)
+    x = O.splitmix_normal(1, n)
+    f = O.build_frames(x, fp, P=P, num_workers=W, batch_max=8)
+    fb = 52 + 4 * P
+    B = O.num_blocks(n, P)
+    b = min(B, 8)
+    assert f.size == (B + b) * fb
+    exps = O.exponents(x, P)
+    q = O.quantize(x, P, W)
+    for p in range(B + b):
+        fr = f[p * fb:(p + 1) * fb].tobytes()
+        assert fr[0:6] == bytes([2, 0, 0, 0, 0, 1]) and fr[6:12] == bytes([2, 0, 0, 0, 0, 2])
+        assert fr[12:14] == b"\x08\x00"
+        ver, tos, tot = struct.unpack(">BBH", fr[14:18])
+        assert (ver, tot) == (0x45, fb - 14)
+        assert fr[22] == 128 and fr[23] == 17
+        assert fr[26:30] == socket.inet_aton("10.0.0.1") and fr[30:34] == socket.inet_aton("10.0.0.253")
+        sport, dport, ulen = struct.unpack(">HHH", fr[34:40])
+        assert (sport, dport, ulen) == (4000, 48879, fb - 34)
+        # pseudo-header sum, stored as rte_raw_cksum leaves it (memory-order words)
+        psd = fr[26:34] + bytes([0, 17]) + struct.pack(">H", fb - 34)
+        s = sum(struct.unpack("<6H", psd))
+        s = (s & 0xFFFF) + (s >> 16)
+        s = (s & 0xFFFF) + (s >> 16)
+        assert struct.unpack("<H", fr[40:42])[0] == s
+        assert fr[42] == (1 << 4) + 3 and fr[43] == 0x34
+        assert struct.unpack("<I", fr[44:48])[0] == p
+        assert struct.unpack(">H", fr[48:50])[0] == O.pool_index(p, 64, 10, 8)
+        assert fr[50] == (int(exps[p]) & 0xFF if p < B else 0) and fr[51] == 0
+        payload = np.frombuffer(fr[52:], dtype=np.uint32)
+        if p >= b:
+            k = p - b
+            valid = min(P, n - k * P)
+            assert np.array_equal(payload[:valid], q[k * P:k * P + valid])
+        else:
+            assert not payload.any()
+
+
+def test_pool_index_alternates_shadow_pools():
+    """PktId2PoolIndex: ids cycle over 2*mop slots, the upper half with the MSB set."""
+    mop, start = 4, 100
+    got = [O.pool_index(p, start, 0, mop) for p in range(10)]
+    assert got == [100, 101, 102, 103, 0x8064, 0x8065, 0x8066, 0x8067, 100, 101]
+    assert O.pool_index(0, start, 5, mop) == 0x8065
+
+
+# ---------------------------------------------------------------- GPU --
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [64, 256, 1024])
+@pytest.mark.parametrize("n", [1, 300, 50_003])
+@pytest.mark.parametrize("where", ["device", "pinned"])
+def test_frames_match_oracle(cuda, P, n, where):
+    import torch
+    import switchml_amd as sw
+    W, bm = 3, 16
+    fp = params(job_id=7, pool_index_start=16, pool_index_shift=3, max_outstanding_pkts=bm)
+    x = O.splitmix_normal(n + P, n)
+    ref = O.build_frames(x, fp, P=P, num_workers=W, batch_max=bm)
+    B = O.num_blocks(n, P)
+    b = min(B, bm)
+    stride = 52 + 4 * P + 12   # mbuf-like padding between frames; padding bytes untouched
+    if where == "device":
+        frames = torch.full(((B + b) * stride,), 0xAB, dtype=torch.uint8, device=cuda)
+    else:
+        frames = torch.full(((B + b) * stride,), 0xAB, dtype=torch.uint8).pin_memory()
+    sw.quantize_pack_frames(torch.from_numpy(x).to(cuda), fp, P, W, batch_max=bm, frames=frames, stride=stride)
+    torch.cuda.synchronize()
+    got = frames.cpu().numpy().reshape(B + b, stride)
+    exp = ref.reshape(B + b, 52 + 4 * P)
+    assert np.array_equal(got[:, :52 + 4 * P], exp)
+    assert np.all(got[:, 52 + 4 * P:] == 0xAB)
+
+
+@pytest.mark.gpu
+def test_frames_global_exponents_and_misaligned_slice(cuda):
+    import torch
+    import switchml_amd as sw
+    P, n, W, bm = 256, 40_001, 2, 64
+    fp = params(job_id=300, max_outstanding_pkts=bm)
+    xfull = O.splitmix_normal(5, n + 3)
+    x = xfull[3:]
+    B = O.num_blocks(n, P)
+    ge = np.clip(O.exponents(x, P).astype(np.int32) + 1, -128, 127).astype(np.int8)
+    ref = O.build_frames(x, fp, P=P, num_workers=W, batch_max=bm, global_exps=ge)
+    xd = torch.from_numpy(xfull).to(cuda)[3:]
+    assert xd.data_ptr() % 16 != 0
+    got = sw.quantize_pack_frames(xd, fp, P, W, batch_max=bm, global_exps=torch.from_numpy(ge).to(cuda))
+    assert np.array_equal(got.cpu().numpy(), ref)
