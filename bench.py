@@ -296,6 +296,16 @@ def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
     t = timeit(lambda: out.copy_(x))
     res["torch_copy_GBps"] = round(8 * N / t / 1e9, 1)
     res.update(host_inclusive(sw, torch, x, N, P))
+    # DPDK frames (F3): fused quantize straight into Eth/IP/UDP/SwitchML frames
+    fp = sw.frame_params(max_outstanding_pkts=64)
+    fbytes = (B + min(B, 64)) * sw.frame_bytes(P)
+    frames = torch.empty(fbytes, dtype=torch.uint8, device=x.device)
+    t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=frames, stream=stream))
+    res["frames_device_GBps"] = round((4 * N + fbytes) / t / 1e9, 1)
+    del frames
+    hframes = torch.empty(fbytes, dtype=torch.uint8).pin_memory()
+    t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=hframes, stream=stream))
+    res["frames_to_pinned_host_input_GBps"] = round(4 * N / t / 1e9, 2)
     t = timeit(lambda: sw.stream_copy(x, out, stream=stream))
     res["nt_tile_copy_GBps"] = round(8 * N / t / 1e9, 1)
     return res

@@ -170,6 +170,17 @@ sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_
                                       uint32_t batch_max, const sml_frame_params* params,
                                       void* frames, uint64_t frame_stride, void* stream);
 
+/* ---- RDMA messages --------------------------------------
+ * The RDMA backend's LTU is a message of msg_numel (1024) elements
+ * (rdma_worker_thread.cc:86-88): its payload is block m of the planes built
+ * with packet_numel = msg_numel.  The exponent travels in the 32-bit
+ * immediate: imm = (msg_id & 0xFFFF) | (exponent byte << 16), byte 3 = 0
+ * (rdma_worker_thread.cc:341-356; PreprocessSingle writes byte 2).  Message
+ * m in [0, B + b) carries exps[m] for m < B; the byte is 0 for m >= B.
+ * d_imm: uint32[B + b] (host byte order, as ibv_send_wr.imm_data is filled). */
+sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t num_blocks, uint32_t batch_max,
+                          uint32_t* d_imm, void* stream);
+
 /* Measurement probe (not part of the PPP): copy `bytes` (a multiple of 4 KiB,
  * 16-B aligned buffers) with the quantize kernel's tile shape and access
  * policy (non-temporal loads, default-policy stores) — the practical HBM

@@ -602,6 +602,16 @@ __global__ __launch_bounds__(kBlockThreads) void k_stream_copy(const u4* in, u4*
     }
 }
 
+// RDMA immediates: (msg_id & 0xFFFF) | exponent byte << 16 (rdma_worker_thread.cc:341-356).
+__global__ __launch_bounds__(kBlockThreads) void k_rdma_imm(const int8_t* exps, uint64_t B, uint64_t total,
+                                                            uint32_t* imm) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t m = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; m < total; m += stride) {
+        const uint32_t e = m < B ? (uint32_t)(uint8_t)exps[m] : 0u;
+        imm[m] = (uint32_t)(m & 0xFFFFu) | (e << 16);
+    }
+}
+
 __global__ void k_scale_lut(float* lut, uint32_t W) {
     lut[threadIdx.x] = scale_for(W, (int)(int8_t)(uint8_t)threadIdx.x);
 }
@@ -866,6 +876,14 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
     const bool be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
     if (al) launch_rt_a<true>(be, rne, packet_numel, grid, st, a);
     else launch_rt_a<false>(be, rne, packet_numel, grid, st, a);
+    return launch_check();
+}
+
+sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t B, uint32_t batch_max, uint32_t* d_imm, void* stream) {
+    if (B == 0) return SML_OK;
+    if (!d_exps || !d_imm || batch_max == 0) return SML_ERR_INVALID_ARG;
+    const uint64_t total = B + (B < batch_max ? B : batch_max);
+    k_rdma_imm<<<grid_for_vec(total), kBlockThreads, 0, (hipStream_t)stream>>>(d_exps, B, total, d_imm);
     return launch_check();
 }
 

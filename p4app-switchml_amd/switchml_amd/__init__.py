@@ -104,6 +104,8 @@ def lib():
     L.sml_set_grid_limit.argtypes = [u32]
     L.sml_stream_copy.restype = i32
     L.sml_stream_copy.argtypes = [vp, vp, u64, vp]
+    L.sml_rdma_imm.restype = i32
+    L.sml_rdma_imm.argtypes = [vp, u64, u32, vp, vp]
     L.sml_frame_bytes.restype = u64
     L.sml_frame_bytes.argtypes = [u32]
     L.sml_quantize_pack_frames.restype = i32
@@ -274,3 +276,14 @@ def quantize_pack_frames(x, params: FrameParams, packet_numel: int = 256, num_wo
         _dev(x, torch.float32, "x"), x.numel(), packet_numel, num_workers, g, batch_max,
         ctypes.byref(params), _dev(frames, torch.uint8, "frames"), stride, _stream(stream)))
     return frames
+
+
+def rdma_imm(exps, batch_max: int = 64, stream=None):
+    """RDMA immediates of one slice's B + b messages (uint32 in host order, as
+    int32 tensor): (msg_id & 0xFFFF) | exponent << 16."""
+    torch = _torch()
+    B = exps.numel()
+    out = torch.empty(B + min(B, batch_max), dtype=torch.int32, device=exps.device)
+    _check("sml_rdma_imm", lib().sml_rdma_imm(_dev(exps, torch.int8, "exps"), B, batch_max,
+                                             _dev(out, torch.int32, "imm"), _stream(stream)))
+    return out

@@ -117,3 +117,34 @@ def test_frames_global_exponents_and_misaligned_slice(cuda):
     assert xd.data_ptr() % 16 != 0
     got = sw.quantize_pack_frames(xd, fp, P, W, batch_max=bm, global_exps=torch.from_numpy(ge).to(cuda))
     assert np.array_equal(got.cpu().numpy(), ref)
+
+
+# ------------------------------------------------------- RDMA (F4) -----
+
+def rdma_imm_reference(exps, batch_max):
+    """rdma_worker_thread.cc:341-356: imm = msg_id & 0xFFFF, then
+    PreprocessSingle writes the exponent into byte 2 (messages m < B)."""
+    B = exps.size
+    total = B + min(B, batch_max)
+    imm = np.zeros(total, dtype=np.uint32)
+    for m in range(total):
+        word = bytearray(struct.pack("<I", m & 0xFFFF))
+        if m < B:
+            word[2] = int(exps[m]) & 0xFF
+        imm[m] = struct.unpack("<I", bytes(word))[0]
+    return imm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1000, 1024 * 70_000 + 5])
+def test_rdma_messages(cuda, n):
+    """1024-element RDMA messages: payload = the P = 1024 planes, exponent in
+    the immediate's byte 2; msg ids past 65535 wrap in the low 16 bits."""
+    import torch
+    import switchml_amd as sw
+    P, W, bm = 1024, 2, 32
+    x = O.splitmix_normal(11, n)
+    payload, exps = sw.quantize_pack(torch.from_numpy(x).to(cuda), P, W)
+    assert np.array_equal(payload.cpu().numpy().view(np.uint32), O.quantize(x, P, W))
+    imm = sw.rdma_imm(exps, bm).cpu().numpy().view(np.uint32)
+    assert np.array_equal(imm, rdma_imm_reference(O.exponents(x, P), bm))
