@@ -1,0 +1,225 @@
+// switchml_collnet.cc — SwitchML as an RCCL CollNet plugin on MI355X
+// (the reference's frameworks_integration/nccl_plugin/
+// switchml_plugin.cc, rebuilt for the v6 plugin ABI RCCL 7.2 loads).
+//
+// RCCL hands a CollNet all-reduce to iallreduce(); the plugin submits it to
+// the SwitchML Context (AllReduceAsync) and test() polls the Job, exactly as
+// switchml_plugin.cc:293-387 does.  Differences, all deliberate:
+//  * ptrSupport = NCCL_PTR_HOST | NCCL_PTR_CUDA (the reference: HOST only,
+//    with "TODO | NCCL_PTR_CUDA" at :161) — device buffers go straight to the
+//    GPU quantizer, no bounce copy;
+//  * no p2p side channel: the reference forwarded listen/connect to NCCL's
+//    internal IB net (:179-237) only to hold a ring neighbour it never used
+//    for data; the switch (here: the Context's backend) does the reduction;
+//  * a FAILED job makes test() return ncclInternalError (the reference kept
+//    reporting "not done");
+//  * ncclUint8 is widened to int32 on the host as in :318-337, for host
+//    buffers; device uint8 buffers are rejected (ncclInvalidArgument).
+// Configuration: SWITCHML_CONFIG_INI (INI text) or SWITCHML_CONFIG (path),
+// else the reference's search path (/etc/switchml.cfg, ./switchml.cfg, ...).
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "collnet_abi.h"
+#include "context.h"
+#include "loopback_backend.h"
+
+namespace {
+
+ncclDebugLogger_t g_logger = nullptr;
+
+void log_info(const char* msg) {
+    if (g_logger) g_logger(NCCL_LOG_INFO, 0, __FILE__, __LINE__, "%s", msg);
+}
+
+struct ListenComm {
+    int dev;
+};
+
+struct CollComm {
+    int nranks;
+    int rank;
+};
+
+struct MemHandle {
+    int type;
+};
+
+struct Request {
+    std::shared_ptr<switchml::Job> job;
+    ncclDataType_t dtype;
+    int count;
+    void* recv;            // caller's recv buffer (uint8 case)
+    int32_t* widened;      // temp int32 buffer (uint8 case)
+};
+
+int type_size(ncclDataType_t t) {
+    switch (t) {
+        case ncclUint8: return 1;
+        case ncclInt32:
+        case ncclFloat32: return 4;
+        default: return 0;
+    }
+}
+
+ncclResult_t sml_init(ncclDebugLogger_t logger) {
+    g_logger = logger;
+    try {
+        switchml::Context& ctx = switchml::Context::GetInstance();
+        if (ctx.GetContextState() == switchml::Context::RUNNING) return ncclSuccess;
+        switchml::Config cfg;
+        bool have = false;
+        if (const char* ini = getenv("SWITCHML_CONFIG_INI")) have = cfg.LoadFromString(ini);
+        else if (const char* path = getenv("SWITCHML_CONFIG")) have = cfg.LoadFromFile(path);
+        else have = cfg.LoadFromFile();
+        if (!have) {
+            log_info("SwitchML CollNet: no switchml.cfg found");
+            return ncclInvalidUsage;
+        }
+        return ctx.Start(&cfg) ? ncclSuccess : ncclInternalError;
+    } catch (const std::exception& e) {
+        if (g_logger) g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__, "SwitchML CollNet init failed: %s", e.what());
+        return ncclInternalError;
+    }
+}
+
+ncclResult_t sml_devices(int* ndev) {
+    *ndev = 1;
+    return ncclSuccess;
+}
+
+char g_name[] = "SWITCHML";
+char g_pci[] = "/sys/devices/virtual/switchml";
+
+ncclResult_t sml_get_properties(int dev, ncclNetProperties_v6_t* props) {
+    if (dev != 0 || !props) return ncclInvalidArgument;
+    memset(props, 0, sizeof(*props));
+    props->name = g_name;
+    props->pciPath = g_pci;
+    props->guid = 0x53574d4cull;  // "SWML"
+    props->ptrSupport = NCCL_PTR_HOST | NCCL_PTR_CUDA;
+    props->speed = 100000;
+    props->port = 0;
+    props->latency = 0.0f;
+    props->maxComms = 1;         // switchml_plugin.cc:162
+    props->maxRecvs = 1;
+    return ncclSuccess;
+}
+
+ncclResult_t sml_listen(int dev, void* handle, void** listen_comm) {
+    if (!handle || !listen_comm) return ncclInvalidArgument;
+    memset(handle, 0, NCCL_NET_HANDLE_MAXSIZE);
+    memcpy(handle, "SWITCHML", 8);
+    *listen_comm = new ListenComm{dev};
+    return ncclSuccess;
+}
+
+ncclResult_t sml_connect(void* handles[], int nranks, int rank, void* listen_comm, void** coll_comm) {
+    (void)handles;
+    (void)listen_comm;
+    if (rank < 0 || rank >= nranks) return ncclInternalError;  // switchml_plugin.cc:210-213
+    *coll_comm = new CollComm{nranks, rank};
+    return ncclSuccess;
+}
+
+ncclResult_t sml_reduce_support(ncclDataType_t dtype, ncclRedOp_t op, int* supported) {
+    *supported = (dtype == ncclFloat32 || dtype == ncclInt32 || dtype == ncclUint8) && op == ncclSum;
+    return ncclSuccess;
+}
+
+ncclResult_t sml_reg_mr(void*, void*, int, int type, void** mhandle) {
+    *mhandle = new MemHandle{type};
+    return ncclSuccess;
+}
+
+ncclResult_t sml_reg_mr_dmabuf(void*, void*, size_t, int type, uint64_t, int, void** mhandle) {
+    *mhandle = new MemHandle{type};
+    return ncclSuccess;
+}
+
+ncclResult_t sml_dereg_mr(void*, void* mhandle) {
+    delete static_cast<MemHandle*>(mhandle);
+    return ncclSuccess;
+}
+
+ncclResult_t sml_iallreduce(void*, void* send, void* recv, int count, ncclDataType_t dtype, ncclRedOp_t op,
+                            void*, void*, void** request) {
+    if (op != ncclSum || type_size(dtype) == 0 || count < 0) return ncclInvalidArgument;
+    switchml::Context& ctx = switchml::Context::GetInstance();
+    if (ctx.GetContextState() != switchml::Context::RUNNING) return ncclInvalidUsage;
+    auto* r = new Request{nullptr, dtype, count, recv, nullptr};
+    switchml::DataType sdt = dtype == ncclFloat32 ? switchml::FLOAT32 : switchml::INT32;
+    try {
+        if (dtype == ncclUint8) {
+            if (switchml::IsDevicePointer(send) || switchml::IsDevicePointer(recv)) {
+                delete r;
+                return ncclInvalidArgument;
+            }
+            r->widened = new int32_t[count > 0 ? count : 1];
+            const uint8_t* s8 = static_cast<const uint8_t*>(send);
+            for (int i = 0; i < count; i++) r->widened[i] = s8[i];
+            send = recv = r->widened;
+        }
+        r->job = ctx.AllReduceAsync(send, recv, (uint64_t)count, sdt, switchml::SUM);
+    } catch (const std::exception& e) {
+        delete[] r->widened;
+        delete r;
+        return ncclInternalError;
+    }
+    *request = r;
+    return ncclSuccess;
+}
+
+ncclResult_t sml_iflush(void*, void*, int, void*, void** request) {
+    // Results are written by the GPU stream of the worker thread and
+    // synchronised before the job is marked FINISHED: nothing to flush.
+    *request = nullptr;
+    return ncclSuccess;
+}
+
+ncclResult_t sml_test(void* request, int* done, int* size) {
+    Request* r = static_cast<Request*>(request);
+    const switchml::JobStatus st = r->job->GetJobStatus();
+    if (st == switchml::FAILED) {
+        *done = 0;
+        delete[] r->widened;
+        delete r;
+        return ncclInternalError;
+    }
+    if (st != switchml::FINISHED) {
+        *done = 0;
+        return ncclSuccess;
+    }
+    if (r->dtype == ncclUint8) {   // switchml_plugin.cc:370-378
+        uint8_t* out = static_cast<uint8_t*>(r->recv);
+        for (int i = 0; i < r->count; i++) out[i] = (uint8_t)r->widened[i];
+        delete[] r->widened;
+    }
+    *done = 1;
+    if (size) *size = r->count * type_size(r->dtype);
+    delete r;
+    return ncclSuccess;
+}
+
+ncclResult_t sml_close_coll(void* coll_comm) {
+    delete static_cast<CollComm*>(coll_comm);
+    return ncclSuccess;
+}
+
+ncclResult_t sml_close_listen(void* listen_comm) {
+    delete static_cast<ListenComm*>(listen_comm);
+    return ncclSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+__attribute__((visibility("default"))) ncclCollNet_v6_t ncclCollNetPlugin_v6 = {
+    "SWITCHMLv1",       sml_init,        sml_devices,       sml_get_properties, sml_listen,
+    sml_connect,        sml_reduce_support, sml_reg_mr,     sml_reg_mr_dmabuf,  sml_dereg_mr,
+    sml_iallreduce,     sml_iflush,      sml_test,          sml_close_coll,     sml_close_listen};
+}
