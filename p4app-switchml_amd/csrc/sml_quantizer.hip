@@ -255,6 +255,23 @@ __device__ __forceinline__ void build_lut(float* lut, uint32_t W) {
     __syncthreads();
 }
 
+// Dequantize table: for power-of-two W every scale is 2^x, +inf or 0, so
+// q / s == q * (1 / s) exactly (1/s is exact: 2^-x, 0 or +inf, and both sides
+// are the correctly rounded value of the same real; inf/0 specials agree) —
+// the table then holds 1/s and the kernel multiplies; other W keep the
+// division.  Returns true when the table holds reciprocals.
+__device__ __forceinline__ bool build_dequant_lut(float* lut, uint32_t W) {
+    const bool pow2 = (W & (W - 1)) == 0;
+    const float s = scale_for(W, (int)(int8_t)(uint8_t)threadIdx.x);
+    lut[threadIdx.x] = pow2 ? 1.0f / s : s;
+    __syncthreads();
+    return pow2;
+}
+
+__device__ __forceinline__ float dequantize_lut(uint32_t q_host_order, float t, bool rcp) {
+    return rcp ? (float)(int32_t)q_host_order * t : (float)(int32_t)q_host_order / t;
+}
+
 // -------------------------------------------------------------- kernels
 
 struct QuantArgs {
@@ -464,7 +481,7 @@ struct DequantArgs {
 template <int P, bool ALIGNED, bool BE>
 __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
     __shared__ float lut[256];
-    build_lut(lut, a.W);
+    const bool rcp = build_dequant_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
@@ -486,8 +503,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
             if (!full && idx >= a.numel) continue;
             uint32_t q0 = (uint32_t)w[u].x, q1 = (uint32_t)w[u].y, q2 = (uint32_t)w[u].z, q3 = (uint32_t)w[u].w;
             if constexpr (BE) { q0 = bswap(q0); q1 = bswap(q1); q2 = bswap(q2); q3 = bswap(q3); }
-            f4 o = mkf4(dequantize1(q0, s[u]), dequantize1(q1, s[u]),
-                                   dequantize1(q2, s[u]), dequantize1(q3, s[u]));
+            f4 o = mkf4(dequantize_lut(q0, s[u], rcp), dequantize_lut(q1, s[u], rcp),
+                        dequantize_lut(q2, s[u], rcp), dequantize_lut(q3, s[u], rcp));
             if (full) store4<ALIGNED>(a.out + idx, o);
             else store4_guarded(a.out + idx, o, idx, a.numel);
         }
@@ -510,7 +527,9 @@ struct RoundTripArgs {
 template <int P, bool ALIGNED, bool BE, bool RNE>
 __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
     __shared__ float lut[256];
+    __shared__ float dlut[256];
     build_lut(lut, a.W);
+    const bool rcp = build_dequant_lut(dlut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t padded = a.nblocks * P;
@@ -536,6 +555,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
             const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
             if (idx >= padded) continue;
             const float s = lut[(uint8_t)e[u]];
+            const float ds = dlut[(uint8_t)e[u]];
             uint64_t body = 0;
             if constexpr (RNE) {
                 const uint64_t blk0 = idx / P * P;
@@ -550,8 +570,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
                 store_payload(a.payload + idx / 4, wq);
             }
             // DummyBackend::ProcessPacket: int32 wrap multiply by W.
-            f4 o = mkf4(dequantize1(q[0] * a.W, s), dequantize1(q[1] * a.W, s),
-                                   dequantize1(q[2] * a.W, s), dequantize1(q[3] * a.W, s));
+            f4 o = mkf4(dequantize_lut(q[0] * a.W, ds, rcp), dequantize_lut(q[1] * a.W, ds, rcp),
+                        dequantize_lut(q[2] * a.W, ds, rcp), dequantize_lut(q[3] * a.W, ds, rcp));
             if (full) store4<ALIGNED>(a.out + idx, o);
             else if (idx < a.numel) store4_guarded(a.out + idx, o, idx, a.numel);
         }

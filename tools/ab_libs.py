@@ -27,6 +27,8 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=9, reps=10):
     st = torch.cuda.current_stream()
     res = {p: [] for p in paths}
     cres = {p: [] for p in paths}
+    dres = {p: [] for p in paths}
+    rres = {p: [] for p in paths}
     out = torch.empty_like(x)
     for p, L in zip(paths, libs):  # correctness: identical bytes
         assert L.sml_quantize_pack(x.data_ptr(), N, P, 1, None, payload.data_ptr(), exps.data_ptr(), 0, st.cuda_stream) == 0
@@ -44,6 +46,25 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=9, reps=10):
             b.record(st)
             torch.cuda.synchronize()
             res[p].append(a.elapsed_time(b) / reps * 1e3)
+            L.sml_dequantize.restype = ctypes.c_int
+            L.sml_dequantize.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                         ctypes.c_uint16, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+            a.record(st)
+            for _ in range(reps):
+                L.sml_dequantize(payload.data_ptr(), exps.data_ptr(), N, P, 1, out.data_ptr(), 0, st.cuda_stream)
+            b.record(st)
+            torch.cuda.synchronize()
+            dres[p].append(a.elapsed_time(b) / reps * 1e3)
+            L.sml_roundtrip_loopback.restype = ctypes.c_int
+            L.sml_roundtrip_loopback.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                                 ctypes.c_uint16, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                                 ctypes.c_void_p]
+            a.record(st)
+            for _ in range(reps):
+                L.sml_roundtrip_loopback(x.data_ptr(), out.data_ptr(), N, P, 1, None, None, 0, st.cuda_stream)
+            b.record(st)
+            torch.cuda.synchronize()
+            rres[p].append(a.elapsed_time(b) / reps * 1e3)
             if hasattr(L, "sml_stream_copy"):
                 L.sml_stream_copy.restype = ctypes.c_int
                 L.sml_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
@@ -58,6 +79,8 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=9, reps=10):
     for p, v in res.items():
         rep[p] = {"median_us": round(statistics.median(v), 2), "min_us": round(min(v), 2),
                   "GBps": round(alg / statistics.median(v) / 1e3, 1)}
+        rep[p]["dequant_GBps"] = round(alg / statistics.median(dres[p]) / 1e3, 1)
+        rep[p]["roundtrip_GBps"] = round(8 * N / statistics.median(rres[p]) / 1e3, 1)
         if cres[p]:
             rep[p]["copy_probe_GBps"] = round(8 * N / statistics.median(cres[p]) / 1e3, 1)
     print(json.dumps(rep, indent=1))
