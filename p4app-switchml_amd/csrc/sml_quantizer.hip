@@ -255,23 +255,6 @@ __device__ __forceinline__ void build_lut(float* lut, uint32_t W) {
     __syncthreads();
 }
 
-// Dequantize table: for power-of-two W every scale is 2^x, +inf or 0, so
-// q / s == q * (1 / s) exactly (1/s is exact: 2^-x, 0 or +inf, and both sides
-// are the correctly rounded value of the same real; inf/0 specials agree) —
-// the table then holds 1/s and the kernel multiplies; other W keep the
-// division.  Returns true when the table holds reciprocals.
-__device__ __forceinline__ bool build_dequant_lut(float* lut, uint32_t W) {
-    const bool pow2 = (W & (W - 1)) == 0;
-    const float s = scale_for(W, (int)(int8_t)(uint8_t)threadIdx.x);
-    lut[threadIdx.x] = pow2 ? 1.0f / s : s;
-    __syncthreads();
-    return pow2;
-}
-
-__device__ __forceinline__ float dequantize_lut(uint32_t q_host_order, float t, bool rcp) {
-    return rcp ? (float)(int32_t)q_host_order * t : (float)(int32_t)q_host_order / t;
-}
-
 // -------------------------------------------------------------- kernels
 
 struct QuantArgs {
@@ -481,7 +464,7 @@ struct DequantArgs {
 template <int P, bool ALIGNED, bool BE>
 __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
     __shared__ float lut[256];
-    const bool rcp = build_dequant_lut(lut, a.W);
+    build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
@@ -489,12 +472,22 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
         const bool full = base + kTileElems <= a.numel;
         u4 w[kU];
         float s[kU];
+        if (P == 256 && full && ((uintptr_t)a.exps & 3u) == 0) {
+            // the tile's 4 exponents in one (wave-uniform) dword load
+            const uint32_t e4 = *reinterpret_cast<const uint32_t*>(a.exps + base / P);
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-            if (full || idx < a.numel) {
-                w[u] = __builtin_nontemporal_load(a.payload + idx / 4);
-                s[u] = lut[(uint8_t)a.exps[idx / P]];
+            for (int u = 0; u < kU; u++) {
+                w[u] = __builtin_nontemporal_load(a.payload + (base + (uint64_t)(u * kWave + lane) * 4) / 4);
+                s[u] = lut[(e4 >> (8 * u)) & 0xffu];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+                if (full || idx < a.numel) {
+                    w[u] = __builtin_nontemporal_load(a.payload + idx / 4);
+                    s[u] = lut[(uint8_t)a.exps[idx / P]];
+                }
             }
         }
 #pragma unroll
@@ -503,8 +496,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
             if (!full && idx >= a.numel) continue;
             uint32_t q0 = (uint32_t)w[u].x, q1 = (uint32_t)w[u].y, q2 = (uint32_t)w[u].z, q3 = (uint32_t)w[u].w;
             if constexpr (BE) { q0 = bswap(q0); q1 = bswap(q1); q2 = bswap(q2); q3 = bswap(q3); }
-            f4 o = mkf4(dequantize_lut(q0, s[u], rcp), dequantize_lut(q1, s[u], rcp),
-                        dequantize_lut(q2, s[u], rcp), dequantize_lut(q3, s[u], rcp));
+            f4 o = mkf4(dequantize1(q0, s[u]), dequantize1(q1, s[u]),
+                                   dequantize1(q2, s[u]), dequantize1(q3, s[u]));
             if (full) store4<ALIGNED>(a.out + idx, o);
             else store4_guarded(a.out + idx, o, idx, a.numel);
         }
@@ -527,9 +520,7 @@ struct RoundTripArgs {
 template <int P, bool ALIGNED, bool BE, bool RNE>
 __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
     __shared__ float lut[256];
-    __shared__ float dlut[256];
     build_lut(lut, a.W);
-    const bool rcp = build_dequant_lut(dlut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t padded = a.nblocks * P;
@@ -555,7 +546,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
             const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
             if (idx >= padded) continue;
             const float s = lut[(uint8_t)e[u]];
-            const float ds = dlut[(uint8_t)e[u]];
             uint64_t body = 0;
             if constexpr (RNE) {
                 const uint64_t blk0 = idx / P * P;
@@ -570,8 +560,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
                 store_payload(a.payload + idx / 4, wq);
             }
             // DummyBackend::ProcessPacket: int32 wrap multiply by W.
-            f4 o = mkf4(dequantize_lut(q[0] * a.W, ds, rcp), dequantize_lut(q[1] * a.W, ds, rcp),
-                        dequantize_lut(q[2] * a.W, ds, rcp), dequantize_lut(q[3] * a.W, ds, rcp));
+            f4 o = mkf4(dequantize1(q[0] * a.W, s), dequantize1(q[1] * a.W, s),
+                                   dequantize1(q[2] * a.W, s), dequantize1(q[3] * a.W, s));
             if (full) store4<ALIGNED>(a.out + idx, o);
             else if (idx < a.numel) store4_guarded(a.out + idx, o, idx, a.numel);
         }
