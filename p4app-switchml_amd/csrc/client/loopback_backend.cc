@@ -139,6 +139,10 @@ void LoopbackBackend::SetupWorker() {
 }
 
 void LoopbackBackend::CleanupWorker() {
+    {
+        std::lock_guard<std::mutex> lk(wire_mutex_);
+    }
+    wire_cv_.notify_all();
     for (auto& t : threads_)
         if (t.joinable()) t.join();
     threads_.clear();
@@ -178,8 +182,10 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
             const float bw = config_.backend_.dummy.bandwidth;
             if (ok && bw > 0) {  // the dummy backend's simulated wire time (dummy_backend.cc:124-133)
                 const double ns = 1000.0 * (double)packets * g.packet_numel * 4 * 8 * g.num_worker_threads / bw;
-                struct timespec req = {(time_t)(ns / 1e9), (long)((uint64_t)ns % 1000000000ull)};
-                nanosleep(&req, nullptr);
+                // interruptible: Stop() must not wait out a simulated wire
+                std::unique_lock<std::mutex> lk(wire_mutex_);
+                wire_cv_.wait_for(lk, std::chrono::nanoseconds((int64_t)std::min(ns, 9.0e18)),
+                                  [this] { return context_.GetContextState() != Context::RUNNING; });
             }
             context_.GetStats().AddSlice(tid, packets, js.slice.numel * DataTypeSize(js.slice.data_type));
         }

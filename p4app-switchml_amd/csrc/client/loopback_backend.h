@@ -13,6 +13,8 @@
 #ifndef SWITCHML_AMD_LOOPBACK_BACKEND_H_
 #define SWITCHML_AMD_LOOPBACK_BACKEND_H_
 
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -37,6 +39,8 @@ class LoopbackBackend {
     Context& context_;
     Config& config_;
     std::vector<std::thread> threads_;
+    std::mutex wire_mutex_;              // simulated wire time, cut short by Stop()
+    std::condition_variable wire_cv_;
 };
 
 // True if p is HIP device (or managed) memory; false for host memory.

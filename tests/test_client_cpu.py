@@ -115,3 +115,15 @@ def test_job_wait_after_stop_fails_queued(ctx):
     states = [j.status() for j in jobs]
     assert all(s in (C.JOB_FINISHED, C.JOB_FAILED) for s in states)
     assert C.JOB_FAILED in states
+
+
+def test_empty_job_finishes(ctx):
+    """numel = 0: every slice is empty and the job completes without the PPP
+    (dummy_worker_thread.cc:87)."""
+    C = ctx
+    C.start(C.make_config(prepostprocessor="hip_exponent_quantizer", num_worker_threads=3, bandwidth=0, device=0))
+    x = np.zeros(0, dtype=np.float32)
+    j = C.allreduce_async(x)
+    j.wait()
+    assert j.status() == C.JOB_FINISHED
+    C.stop()

@@ -307,3 +307,30 @@ def test_cfg3_256mib_roundtrip(cuda):
         assert np.all(err <= bound * 1.0000001)
         del out
         torch.cuda.empty_cache()
+
+
+def test_beyond_2_31_elements_sampled_blocks(cuda):
+    """Maximum sizes: a 2^31 + 300-element slice (8 GiB fp32; element and byte
+    offsets past 32 bits).  Blocks are independent once their exponent is
+    known, so sampled blocks (first, around 2^31, the partial last) are
+    checked against the oracle run on those blocks alone."""
+    import torch
+    N, P, W = (1 << 31) + 300, 256, 2
+    g = torch.Generator(device=cuda)
+    g.manual_seed(3)
+    x = torch.randn(N, device=cuda, generator=g)
+    payload, exps = sw().quantize_pack(x, P, W)
+    B = O.num_blocks(N, P)
+    assert payload.numel() == B * P
+    for k in (0, 1, (1 << 23) - 1, 1 << 23, (1 << 23) + 1, B - 2, B - 1):
+        blk = host(x[k * P:min((k + 1) * P, N)])
+        assert int(host(exps[k:k + 1])[0]) == int(O.exponents(blk, P)[0]), k
+        assert bits_equal(host(payload[k * P:(k + 1) * P]), O.quantize(blk, P, W)), k
+    out = sw().dequantize(payload, exps, N, P, W)
+    for k in (0, 1 << 23, B - 1):
+        blk_q = host(payload[k * P:(k + 1) * P]).view(np.uint32)
+        n = min(P, N - k * P)
+        ref = O.dequantize(blk_q, host(exps[k:k + 1]), n, P, W)
+        assert float_bits_equal_nan_ok(host(out[k * P:k * P + n]), ref), k
+    del x, payload, exps, out
+    torch.cuda.empty_cache()
