@@ -33,12 +33,17 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "switchml_hip.h"
 
 namespace sml {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+// 16-byte vector with 4-byte alignment: gfx950 runs in unaligned-access mode,
+// so this is still one global_store_dwordx4 (used at the 52-byte frame offset).
+typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
 
 __device__ __forceinline__ f4 mkf4(float a, float b, float c, float d) { return f4{a, b, c, d}; }
 __device__ __forceinline__ u4 mku4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return u4{a, b, c, d}; }
@@ -431,7 +436,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) 
             if (pk + a.b >= a.nblocks) write_frame_header(a, pk + a.b, lane, 0u);
             if (pk < a.b) {
                 uint32_t* pl = reinterpret_cast<uint32_t*>(a.frames + pk * a.stride + 52);
-                for (int i = lane; i < P; i += kWave) pl[i] = 0u;
+                for (int i = lane; i < P / 4; i += kWave) *reinterpret_cast<u4a*>(pl + 4 * i) = u4a{0u, 0u, 0u, 0u};
             }
         }
 #pragma unroll
@@ -443,10 +448,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) 
             if constexpr (GLOBAL) e = a.gexp[k];
             const u4 q = quantize4<false>(v[u], lut[(uint8_t)e], idx, 0);
             uint32_t* dst = reinterpret_cast<uint32_t*>(a.frames + (k + a.b) * a.stride + 52) + (idx - k * P);
-            dst[0] = bswap(q.x);
-            dst[1] = bswap(q.y);
-            dst[2] = bswap(q.z);
-            dst[3] = bswap(q.w);
+            *reinterpret_cast<u4a*>(dst) = u4a{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)};
         }
     }
 }
@@ -629,7 +631,7 @@ __global__ void k_scale_lut(float* lut, uint32_t W) {
 // ------------------------------------------------------------ host side
 
 static thread_local char g_last_error[256] = "";
-static uint32_t g_grid_limit = 0;
+static std::atomic<uint32_t> g_grid_limit{0};
 
 static sml_status_t hip_check(hipError_t err) {
     if (err == hipSuccess) return SML_OK;
@@ -649,14 +651,16 @@ static inline bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }
 static inline uint32_t grid_for_tiles(uint64_t ntiles) {
     uint64_t g = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
     if (g == 0) g = 1;
-    if (g_grid_limit && g > g_grid_limit) g = g_grid_limit;
+    const uint32_t lim = g_grid_limit.load(std::memory_order_relaxed);
+    if (lim && g > lim) g = lim;
     if (g > 0x7fffffffull) g = 0x7fffffffull;
     return (uint32_t)g;
 }
 
 static inline uint32_t grid_for_vec(uint64_t nvec) {
     uint64_t g = (nvec + kBlockThreads - 1) / kBlockThreads;
-    uint64_t cap = g_grid_limit ? g_grid_limit : 8192;
+    const uint32_t lim = g_grid_limit.load(std::memory_order_relaxed);
+    uint64_t cap = lim ? lim : 8192;
     if (g > cap) g = cap;
     if (g == 0) g = 1;
     return (uint32_t)g;
@@ -674,7 +678,7 @@ static void launch_quant_t(uint32_t P, dim3 grid, hipStream_t st, const QuantArg
     }
 }
 
-static uint32_t g_tiles_per_wave = 1;
+static std::atomic<uint32_t> g_tiles_per_wave{1};
 
 template <bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
 static void launch_quant_p(uint32_t P, dim3 grid, hipStream_t st, const QuantArgs& a) {
@@ -759,15 +763,11 @@ const char* sml_status_string(sml_status_t s) {
 const char* sml_last_error(void) { return g_last_error; }
 
 uint32_t sml_set_grid_limit(uint32_t max_workgroups) {
-    uint32_t prev = g_grid_limit;
-    g_grid_limit = max_workgroups;
-    return prev;
+    return g_grid_limit.exchange(max_workgroups);
 }
 
 uint32_t sml_set_tiles_per_wave(uint32_t tpw) {
-    uint32_t prev = g_tiles_per_wave;
-    g_tiles_per_wave = tpw == 2 ? 2 : 1;
-    return prev;
+    return g_tiles_per_wave.exchange(tpw == 2 ? 2u : 1u);
 }
 
 uint64_t sml_num_blocks(uint64_t numel, uint32_t packet_numel) {

@@ -147,10 +147,13 @@ def _torch():
     return torch
 
 
-def _stream(stream):
+def _stream(stream, like=None):
+    """The HIP stream to launch on: the given one, else torch's current
+    stream of `like`'s device (else of the current device)."""
     torch = _torch()
     if stream is None:
-        stream = torch.cuda.current_stream()
+        dev = like.device if like is not None and getattr(like, "is_cuda", False) else None
+        stream = torch.cuda.current_stream(dev)
     return ctypes.c_void_p(stream.cuda_stream)
 
 
@@ -176,7 +179,7 @@ def scale_lut(num_workers: int):
 def scale_lut_device(num_workers: int, device="cuda", stream=None):
     torch = _torch()
     out = torch.empty(256, dtype=torch.float32, device=device)
-    _check("sml_scale_lut_device", lib().sml_scale_lut_device(num_workers, _dev(out, torch.float32, "lut"), _stream(stream)))
+    _check("sml_scale_lut_device", lib().sml_scale_lut_device(num_workers, _dev(out, torch.float32, "lut"), _stream(stream, out)))
     return out
 
 
@@ -186,7 +189,7 @@ def exponents(x, packet_numel: int = 256, out=None, stream=None):
     if out is None:
         out = torch.empty(B, dtype=torch.int8, device=x.device)
     _check("sml_exponents", lib().sml_exponents(_dev(x, torch.float32, "x"), x.numel(), packet_numel,
-                                                _dev(out, torch.int8, "exps"), _stream(stream)))
+                                                _dev(out, torch.int8, "exps"), _stream(stream, x)))
     return out
 
 
@@ -203,7 +206,7 @@ def quantize_pack(x, packet_numel: int = 256, num_workers: int = 1, global_exps=
     e = None if exps_out is None else _dev(exps_out, torch.int8, "exps_out")
     _check("sml_quantize_pack", lib().sml_quantize_pack(
         _dev(x, torch.float32, "x"), x.numel(), packet_numel, num_workers, g,
-        _dev(payload, torch.int32, "payload"), e, flags, _stream(stream)))
+        _dev(payload, torch.int32, "payload"), e, flags, _stream(stream, x)))
     return payload, (global_exps if global_exps is not None else exps_out)
 
 
@@ -214,7 +217,7 @@ def dequantize(payload, exps, numel: int, packet_numel: int = 256, num_workers: 
         out = torch.empty(numel, dtype=torch.float32, device=payload.device)
     _check("sml_dequantize", lib().sml_dequantize(
         _dev(payload, torch.int32, "payload"), _dev(exps, torch.int8, "exps"), numel, packet_numel,
-        num_workers, _dev(out, torch.float32, "out"), flags, _stream(stream)))
+        num_workers, _dev(out, torch.float32, "out"), flags, _stream(stream, payload)))
     return out
 
 
@@ -223,14 +226,14 @@ def bswap_i32(x, out=None, stream=None):
     if out is None:
         out = torch.empty_like(x)
     _check("sml_bswap_i32", lib().sml_bswap_i32(_dev(x, torch.int32, "x"), _dev(out, torch.int32, "out"),
-                                                x.numel(), _stream(stream)))
+                                                x.numel(), _stream(stream, x)))
     return out
 
 
 def loopback_aggregate(payload, num_workers: int, flags: int = 0, stream=None):
     torch = _torch()
     _check("sml_loopback_aggregate", lib().sml_loopback_aggregate(
-        _dev(payload, torch.int32, "payload"), payload.numel(), num_workers, flags, _stream(stream)))
+        _dev(payload, torch.int32, "payload"), payload.numel(), num_workers, flags, _stream(stream, payload)))
     return payload
 
 
@@ -243,7 +246,7 @@ def roundtrip_loopback(x, packet_numel: int = 256, num_workers: int = 1, out=Non
     e = None if exps_out is None else _dev(exps_out, torch.int8, "exps_out")
     _check("sml_roundtrip_loopback", lib().sml_roundtrip_loopback(
         _dev(x, torch.float32, "x"), _dev(out, torch.float32, "out"), x.numel(), packet_numel,
-        num_workers, p, e, flags, _stream(stream)))
+        num_workers, p, e, flags, _stream(stream, x)))
     return out
 
 
@@ -251,7 +254,7 @@ def stream_copy(src, dst, stream=None):
     """Measurement probe: non-temporal tile copy (src/dst same byte size)."""
     nbytes = src.numel() * src.element_size()
     _check("sml_stream_copy", lib().sml_stream_copy(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
-                                                    nbytes, _stream(stream)))
+                                                    nbytes, _stream(stream, src)))
     return dst
 
 
@@ -274,7 +277,7 @@ def quantize_pack_frames(x, params: FrameParams, packet_numel: int = 256, num_wo
     g = None if global_exps is None else _dev(global_exps, torch.int8, "global_exps")
     _check("sml_quantize_pack_frames", lib().sml_quantize_pack_frames(
         _dev(x, torch.float32, "x"), x.numel(), packet_numel, num_workers, g, batch_max,
-        ctypes.byref(params), _dev(frames, torch.uint8, "frames"), stride, _stream(stream)))
+        ctypes.byref(params), _dev(frames, torch.uint8, "frames"), stride, _stream(stream, x)))
     return frames
 
 
@@ -285,5 +288,5 @@ def rdma_imm(exps, batch_max: int = 64, stream=None):
     B = exps.numel()
     out = torch.empty(B + min(B, batch_max), dtype=torch.int32, device=exps.device)
     _check("sml_rdma_imm", lib().sml_rdma_imm(_dev(exps, torch.int8, "exps"), B, batch_max,
-                                             _dev(out, torch.int32, "imm"), _stream(stream)))
+                                             _dev(out, torch.int32, "imm"), _stream(stream, exps)))
     return out
