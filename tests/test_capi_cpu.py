@@ -76,3 +76,34 @@ def test_python_wrapper_rejects_cpu_tensors(sw):
     torch = pytest.importorskip("torch")
     with pytest.raises(TypeError, match="no CPU fallback"):
         sw.quantize_pack(torch.zeros(16))
+
+
+def test_frames_and_rdma_validation_without_gpu(sw):
+    L = sw.lib()
+    fp = sw.frame_params()
+    buf = (ctypes.c_float * 16)()
+    frames = (ctypes.c_uint8 * 8192)()
+    assert sw.frame_bytes(256) == 52 + 1024 and sw.frame_bytes(64) == 52 + 256
+    # unsupported packet size / stride too small / stride not a multiple of 4
+    assert L.sml_quantize_pack_frames(buf, 16, 100, 1, None, 64, ctypes.byref(fp), frames, 4096, None) == sw.SML_ERR_UNSUPPORTED
+    assert L.sml_quantize_pack_frames(buf, 16, 256, 1, None, 64, ctypes.byref(fp), frames, 1000, None) == sw.SML_ERR_ALIGNMENT
+    assert L.sml_quantize_pack_frames(buf, 16, 256, 1, None, 64, ctypes.byref(fp), frames, 1078, None) == sw.SML_ERR_ALIGNMENT
+    # no params / batch 0 / W 0
+    assert L.sml_quantize_pack_frames(buf, 16, 256, 1, None, 64, None, frames, 1076, None) == sw.SML_ERR_INVALID_ARG
+    assert L.sml_quantize_pack_frames(buf, 16, 256, 1, None, 0, ctypes.byref(fp), frames, 1076, None) == sw.SML_ERR_INVALID_ARG
+    assert L.sml_quantize_pack_frames(buf, 16, 256, 0, None, 64, ctypes.byref(fp), frames, 1076, None) == sw.SML_ERR_INVALID_ARG
+    # empty slice: nothing to do
+    assert L.sml_quantize_pack_frames(None, 0, 256, 1, None, 64, ctypes.byref(fp), None, 1076, None) == sw.SML_OK
+    assert L.sml_rdma_imm(None, 0, 64, None, None) == sw.SML_OK
+    assert L.sml_rdma_imm(None, 10, 64, None, None) == sw.SML_ERR_INVALID_ARG
+
+
+def test_frame_params_layout_matches_header(sw):
+    """The ctypes mirror of sml_frame_params has the C layout (offsets per the
+    natural alignment of include/switchml_hip.h's struct)."""
+    F = sw.FrameParams
+    assert F.dst_mac.offset == 0 and F.src_mac.offset == 6
+    assert F.src_ip_be.offset == 12 and F.dst_ip_be.offset == 16
+    assert F.src_port_be.offset == 20 and F.dst_port_be.offset == 22
+    assert F.job_id.offset == 24 and F.pool_index_start.offset == 32
+    assert ctypes.sizeof(F) == 48
