@@ -88,8 +88,15 @@ def cpu_baseline(numel, P, budget_s):
             reps += 1
         return float(np.median(rates)), reps
 
-    single, reps1 = run(1, budget_s * 0.35, 2)
-    multi, repsT = run(cores, budget_s * 0.65, 3)
+    single, reps1 = run(1, budget_s * 0.3, 2)
+    four, reps4 = run(4, budget_s * 0.2, 3) if cores > 4 else (None, 0)
+    multi, repsT = run(cores, budget_s * 0.5, 3)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), model)
+    except OSError:
+        pass
     return {
         "value": round(multi, 3),
         "unit": "GB/s (8N+B algorithmic bytes, same as value)",
@@ -99,8 +106,10 @@ def cpu_baseline(numel, P, budget_s):
                    f"DummyWorkerThread order, PreprocessSingle only (exponent + quantize + BE pack into "
                    f"the b-packet ring), the full {numel * 4 >> 20} MiB bucket, packet_numel {P}, "
                    f"max_outstanding_packets 256; {cores} worker threads x {repsT} reps (median); "
-                   f"1 thread: {single:.3f} GB/s over {reps1} reps"),
+                   f"1 thread: {single:.3f} GB/s over {reps1} reps; host CPU {model}"),
         "single_thread_value": round(single, 3),
+        "ref_default_4_threads_value": None if four is None else round(four, 3),
+        "cpu_model": model,
         "input_GBps": round(multi * 4 * numel / alg, 3),
     }
 
