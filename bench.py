@@ -311,7 +311,17 @@ def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
     frames = torch.empty(fbytes, dtype=torch.uint8, device=x.device)
     t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=frames, stream=stream))
     res["frames_device_GBps"] = round((4 * N + fbytes) / t / 1e9, 1)
-    del frames
+    # receive side: the same frames (W = 1 loopback) back to fp32; the rx
+    # bitmap reset (rte_bitmap_reset per slice) is inside the timed call
+    rx = sw.RxSlice(N, P, 64, device=x.device, out=out)
+
+    def rx_once():
+        rx.state.zero_()
+        sw.dequantize_frames(frames, fbytes // sw.frame_bytes(P), rx, num_workers=1, stream=stream)
+    with torch.cuda.stream(stream):
+        t = timeit(rx_once)
+    res["frames_rx_device_GBps"] = round((4 * N + fbytes) / t / 1e9, 1)
+    del frames, rx
     hframes = torch.empty(fbytes, dtype=torch.uint8).pin_memory()
     t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=hframes, stream=stream))
     res["frames_to_pinned_host_input_GBps"] = round(4 * N / t / 1e9, 2)

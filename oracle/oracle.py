@@ -65,6 +65,7 @@ def lib():
         L.orc_dummy_packet_stream.argtypes = [vp, u64, u64, u32, u16, vp, vp, vp]
         L.orc_build_frames.restype = i32
         L.orc_build_frames.argtypes = [vp, u64, u64, u16, vp, u32, vp, vp, u64]
+        L.orc_dequantize_frames.argtypes = [vp, u64, u64, u64, u64, u16, u32, u64, vp, vp, vp, vp]
         L.orc_pkt_id_to_pool_index.restype = ctypes.c_uint16
         L.orc_pkt_id_to_pool_index.argtypes = [u64, u32, u32, u32]
         L.orc_glibc_rand.argtypes = [u32, u64, vp]
@@ -192,6 +193,32 @@ def build_frames(x: np.ndarray, params, P: int = 256, num_workers: int = 1, batc
     if rc != 0:
         raise RuntimeError("orc_build_frames failed")
     return out
+
+
+class RxState:
+    """Receive-side state of one slice for dequantize_frames (the PPP's
+    scaling factors as exponents, the worker's rx bitmap, the output)."""
+
+    def __init__(self, numel: int, P: int = 256, batch_max: int = 64):
+        B = num_blocks(numel, P)
+        self.numel, self.P, self.batch_max = numel, P, batch_max
+        self.exps = np.zeros(B, dtype=np.int8)
+        self.seen = np.zeros(max(1, B + min(B, batch_max)), dtype=np.uint8)
+        self.out = np.zeros(numel, dtype=np.float32)
+        self.counts = [0, 0]
+
+
+def dequantize_frames(frames: np.ndarray, num_frames: int, stride: int, rx: RxState,
+                      num_workers: int = 1, job_id: int = 0) -> RxState:
+    """DpdkWorkerThread's receive loop over `num_frames` received frames in
+    order; accumulates into `rx` (call repeatedly for successive rx bursts)."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    assert frames.size >= num_frames * stride
+    counts = np.zeros(2, dtype=np.uint64)
+    lib().orc_dequantize_frames(_p(frames), num_frames, stride, rx.numel, rx.P, num_workers, rx.batch_max,
+                                job_id, _p(rx.exps), _p(rx.seen), _p(rx.out), _p(counts))
+    rx.counts = [rx.counts[0] + int(counts[0]), rx.counts[1] + int(counts[1])]
+    return rx
 
 
 def pool_index(pkt_id, start, shift, mop) -> int:

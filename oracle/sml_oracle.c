@@ -471,3 +471,46 @@ int orc_build_frames(const float* in, uint64_t numel, uint64_t P, uint16_t W, co
     }
     return 0;
 }
+
+/* Receive loop of DpdkWorkerThread (dpdk_worker_thread.cc:300-345), one frame
+ * at a time in the given order: discard a pkt_id already received (the rx
+ * bitmap, :316-322) or a frame of another job (short_job_id, :325-331);
+ * otherwise PostprocessSingle(pkt_id, frame + 52, frame + 50) (ppp.cc:197-260):
+ * dequantize block pkt_id - b with scaling_factors_[pkt_id - b] when pkt_id >= b,
+ * then, if pkt_id < B, scaling_factors_[pkt_id] from the exponent byte.
+ * pkt_id >= B + b is counted as discarded (the reference would index its
+ * bitmap out of range).  `exps` (int8[B]) and `seen` (the rx bitmap, one
+ * byte per pkt_id, B + b, zeroed by the caller per slice) carry over between
+ * calls; the scale is recomputed from exps (scaling_factors_[k] is exactly
+ * orc_scale(W, exps[k])). */
+void orc_dequantize_frames(const uint8_t* frames, uint64_t num_frames, uint64_t stride, uint64_t numel,
+                           uint64_t P, uint16_t W, uint32_t batch_max, uint64_t job_id, int8_t* exps,
+                           uint8_t* seen, float* out, uint64_t counts[2]) {
+    const uint64_t B = orc_num_blocks(numel, P);
+    const uint64_t b = B < batch_max ? B : batch_max;
+    const uint64_t total = B + b;
+    float lut[256];
+    orc_scale_lut(W, lut);
+    for (uint64_t f = 0; f < num_frames; f++) {
+        const uint8_t* fr = frames + f * stride;
+        uint32_t pid;
+        memcpy(&pid, fr + 44, 4);
+        if (pid >= total || seen[pid] || fr[43] != (uint8_t)job_id) {
+            counts[1]++;
+            continue;
+        }
+        seen[pid] = 1;
+        counts[0]++;
+        if (pid >= b) {
+            const uint64_t k = pid - b, off = k * P, n = numel - off < P ? numel - off : P;
+            const float s = lut[(uint8_t)exps[k]];
+            for (uint64_t i = 0; i < n; i++) {
+                uint32_t w;
+                memcpy(&w, fr + 52 + 4 * i, 4);
+                out[off + i] = orc_dequantize_value(w, s);
+            }
+        }
+        if (pid < B) exps[pid] = (int8_t)fr[50];
+    }
+}
+

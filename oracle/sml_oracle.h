@@ -122,6 +122,13 @@ uint16_t orc_pkt_id_to_pool_index(uint64_t pkt_id, uint32_t start, uint32_t shif
 int orc_build_frames(const float* in, uint64_t numel, uint64_t P, uint16_t num_workers,
                      const int8_t* global_exps, uint32_t batch_max, const orc_frame_params* prm,
                      uint8_t* frames, uint64_t stride);
+/* Receive loop of DpdkWorkerThread + PostprocessSingle over received frames
+ * (dpdk_worker_thread.cc:300-345, ppp.cc:197-260).  counts[0] += accepted,
+ * counts[1] += discarded; exps (int8[B]) and seen (uint8[B + b], the rx
+ * bitmap) in/out across the calls of one slice. */
+void orc_dequantize_frames(const uint8_t* frames, uint64_t num_frames, uint64_t stride, uint64_t numel,
+                           uint64_t P, uint16_t num_workers, uint32_t batch_max, uint64_t job_id,
+                           int8_t* exps, uint8_t* seen, float* out, uint64_t counts[2]);
 
 /* glibc random()/rand() TYPE_3 generator restated (srand(seed) then n calls),
  * and the reference's random-float generator built on it:

@@ -453,6 +453,128 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) 
     }
 }
 
+// ------------------------------------------------- DPDK frames, receive side
+//
+// The rx bitmap of DpdkWorkerThread (dpdk_worker_thread.cc:316-342) becomes a
+// per-slice state word per packet id: 0 = not received, kRxDone = received
+// in an earlier call, otherwise the claim tag of the frame that won it in the
+// current call (larger tag = earlier frame, so atomicMax picks the first).
+constexpr uint32_t kRxDone = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t rx_tag(uint64_t f) { return 0xFFFFFFFEu - (uint32_t)f; }
+
+struct RxArgs {
+    const uint8_t* frames;
+    uint64_t nframes;
+    uint64_t stride;
+    uint64_t numel;
+    uint64_t nblocks;           // B
+    uint64_t b;                 // extra batch
+    uint32_t* state;            // [B + b]
+    int8_t* exps;               // [B]
+    float* out;
+    unsigned long long* counts; // {accepted, discarded} or nullptr
+    uint32_t W;
+    uint32_t job;               // (uint8_t)job_id
+};
+
+__device__ __forceinline__ uint32_t rx_pkt_id(const RxArgs& a, uint64_t f, bool* job_ok) {
+    const uint8_t* fr = a.frames + f * a.stride;
+    *job_ok = fr[43] == a.job;
+    return *reinterpret_cast<const uint32_t*>(fr + 44);
+}
+
+// Pass 1: every frame of another job, of an out-of-range or already received
+// pkt_id is discarded; the others claim their pkt_id (first frame wins).
+__global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
+    __shared__ uint32_t acc[2];
+    if (threadIdx.x < 2) acc[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t mine_acc = 0, mine_seen = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
+        bool job_ok;
+        const uint32_t pid = rx_pkt_id(a, f, &job_ok);
+        mine_seen++;
+        if (!job_ok || pid >= a.nblocks + a.b) continue;
+        if (atomicMax(a.state + pid, rx_tag(f)) == 0u) mine_acc++;   // first claim of a new pkt_id
+    }
+    if (a.counts) {
+        atomicAdd(&acc[0], mine_acc);
+        atomicAdd(&acc[1], mine_seen);
+        __syncthreads();
+        if (threadIdx.x == 0 && acc[1]) {
+            atomicAdd(a.counts + 0, (unsigned long long)acc[0]);
+            atomicAdd(a.counts + 1, (unsigned long long)(acc[1] - acc[0]));
+        }
+    }
+}
+
+// Pass 2: PostprocessSingle for every winning frame, 1024 payload elements per
+// wave (1024 / P frames; lane-chunk c = u*64 + lane is 16 bytes of frame c / (P/4)).
+// The exponent of block k comes from the frame that won pkt_id k in this call
+// (state[k] is its tag) or, if k arrived in an earlier call, from exps[k] —
+// never from an exps[] entry this launch writes.
+template <int P>
+__global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
+    __shared__ float lut[256];
+    build_lut(lut, a.W);
+    constexpr int kChunksPerFrame = P / 4;     // 16-B chunks per payload
+    constexpr int kFramesPerTile = kTileElems / P;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t ntiles = (a.nframes + kFramesPerTile - 1) / kFramesPerTile;
+    for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        u4a w[kU];
+        float s[kU];
+        int64_t dst[kU];                       // output element index of the chunk, -1 = none
+        uint32_t n[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            dst[u] = -1;
+            const int c = u * kWave + lane;
+            const uint64_t f = t * kFramesPerTile + c / kChunksPerFrame;
+            const uint32_t i = (uint32_t)(c % kChunksPerFrame);
+            if (f >= a.nframes) continue;
+            bool job_ok;
+            const uint32_t pid = rx_pkt_id(a, f, &job_ok);
+            if (!job_ok || pid >= a.nblocks + a.b || a.state[pid] != rx_tag(f)) continue;
+            const uint8_t* fr = a.frames + f * a.stride;
+            if (i == 0 && pid < a.nblocks) a.exps[pid] = (int8_t)fr[50];
+            if (pid < a.b) continue;
+            const uint64_t k = pid - a.b;
+            const uint32_t sk = a.state[k];
+            int8_t e;
+            if (sk != 0u && sk != kRxDone) e = (int8_t)a.frames[(uint64_t)(0xFFFFFFFEu - sk) * a.stride + 50];
+            else e = a.exps[k];
+            s[u] = lut[(uint8_t)e];
+            const uint64_t off = k * P + 4ull * i;
+            if (off >= a.numel) continue;
+            n[u] = a.numel - off < 4 ? (uint32_t)(a.numel - off) : 4u;
+            dst[u] = (int64_t)off;
+            w[u] = *reinterpret_cast<const u4a*>(fr + 52 + 16ull * i);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            if (dst[u] < 0) continue;
+            const f4 o = mkf4(dequantize1(bswap(w[u].x), s[u]), dequantize1(bswap(w[u].y), s[u]),
+                              dequantize1(bswap(w[u].z), s[u]), dequantize1(bswap(w[u].w), s[u]));
+            float* p = a.out + dst[u];
+            if (n[u] == 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o;
+            else store4_guarded(p, o, 0, n[u]);
+        }
+    }
+}
+
+// Pass 3: the winners' pkt_ids become "received" for later calls.
+__global__ __launch_bounds__(kBlockThreads) void k_rx_commit(RxArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
+        bool job_ok;
+        const uint32_t pid = rx_pkt_id(a, f, &job_ok);
+        if (job_ok && pid < a.nblocks + a.b && a.state[pid] == rx_tag(f)) a.state[pid] = kRxDone;
+    }
+}
+
 struct DequantArgs {
     const u4* payload;
     const int8_t* exps;
@@ -741,6 +863,16 @@ static void launch_frames_p(uint32_t P, dim3 grid, hipStream_t st, const FrameAr
     }
 }
 
+static void launch_rx_apply(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
+    switch (P) {
+        case 64:   k_rx_apply<64><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_rx_apply<128><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_rx_apply<256><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_rx_apply<512><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_rx_apply<1024><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
 }  // namespace sml
 
 using namespace sml;
@@ -952,6 +1084,39 @@ sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_
     const bool al = aligned16(d_in);
     if (d_global_exps) { if (al) launch_frames_p<true, true>(P, grid, st, a); else launch_frames_p<false, true>(P, grid, st, a); }
     else               { if (al) launch_frames_p<true, false>(P, grid, st, a); else launch_frames_p<false, false>(P, grid, st, a); }
+    return launch_check();
+}
+
+sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint64_t stride,
+                                   uint64_t numel, uint32_t P, uint16_t W, uint32_t batch_max,
+                                   uint64_t job_id, int8_t* d_exps, uint32_t* d_state, float* d_out,
+                                   uint64_t* d_counts, void* stream) {
+    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
+    if (W == 0 || batch_max == 0) return SML_ERR_INVALID_ARG;
+    if (num_frames == 0) return SML_OK;
+    if (num_frames >= 0xFFFFFFFEull) return SML_ERR_UNSUPPORTED;
+    if (!frames || !d_state || (numel && (!d_exps || !d_out))) return SML_ERR_INVALID_ARG;
+    if (!aligned4(frames) || !aligned4(d_out) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
+    if (d_counts && ((uintptr_t)d_counts & 7u)) return SML_ERR_ALIGNMENT;
+    RxArgs a;
+    a.frames = static_cast<const uint8_t*>(frames);
+    a.nframes = num_frames;
+    a.stride = stride;
+    a.numel = numel;
+    a.nblocks = sml_num_blocks(numel, P);
+    a.b = a.nblocks < batch_max ? a.nblocks : batch_max;
+    a.state = d_state;
+    a.exps = d_exps;
+    a.out = d_out;
+    a.counts = reinterpret_cast<unsigned long long*>(d_counts);
+    a.W = W;
+    a.job = (uint8_t)job_id;
+    hipStream_t st = (hipStream_t)stream;
+    uint64_t g1 = (num_frames + 4ull * kBlockThreads - 1) / (4ull * kBlockThreads);   // 4 frames per thread
+    k_rx_claim<<<(uint32_t)(g1 ? g1 : 1), kBlockThreads, 0, st>>>(a);
+    const uint64_t ntiles = (num_frames * P + kTileElems - 1) / kTileElems;
+    launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
+    k_rx_commit<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
     return launch_check();
 }
 

@@ -112,6 +112,8 @@ def lib():
     L.sml_quantize_pack_frames.argtypes = [vp, u64, u32, u16, vp, u32, ctypes.POINTER(FrameParams), vp, u64, vp]
     L.sml_set_tiles_per_wave.restype = u32
     L.sml_set_tiles_per_wave.argtypes = [u32]
+    L.sml_dequantize_frames.restype = i32
+    L.sml_dequantize_frames.argtypes = [vp, u64, u64, u64, u32, u16, u32, u64, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -279,6 +281,35 @@ def quantize_pack_frames(x, params: FrameParams, packet_numel: int = 256, num_wo
         _dev(x, torch.float32, "x"), x.numel(), packet_numel, num_workers, g, batch_max,
         ctypes.byref(params), _dev(frames, torch.uint8, "frames"), stride, _stream(stream, x)))
     return frames
+
+
+class RxSlice:
+    """Receive-side state of one job slice for dequantize_frames: the
+    received exponents, the rx bitmap (DpdkWorkerThread's rte_bitmap,
+    dpdk_worker_thread.cc:316-342) and {accepted, discarded} counters."""
+
+    def __init__(self, numel: int, packet_numel: int = 256, batch_max: int = 64, device="cuda",
+                 out=None):
+        torch = _torch()
+        self.numel, self.packet_numel, self.batch_max = numel, packet_numel, batch_max
+        B = num_blocks(numel, packet_numel)
+        self.exps = torch.zeros(B, dtype=torch.int8, device=device)
+        self.state = torch.zeros(max(1, B + min(B, batch_max)), dtype=torch.int32, device=device)
+        self.counts = torch.zeros(2, dtype=torch.int64, device=device)
+        self.out = out if out is not None else torch.zeros(numel, dtype=torch.float32, device=device)
+
+
+def dequantize_frames(frames, num_frames: int, rx: RxSlice, num_workers: int = 1, job_id: int = 0,
+                      stride: int | None = None, stream=None):
+    """PostprocessSingle over received DPDK frames (any order; duplicates and
+    other jobs' frames discarded), writing rx.out / rx.exps / rx.counts."""
+    torch = _torch()
+    stride = stride or frame_bytes(rx.packet_numel)
+    _check("sml_dequantize_frames", lib().sml_dequantize_frames(
+        _dev(frames, torch.uint8, "frames"), num_frames, stride, rx.numel, rx.packet_numel, num_workers,
+        rx.batch_max, job_id, _dev(rx.exps, torch.int8, "exps"), _dev(rx.state, torch.int32, "state"),
+        _dev(rx.out, torch.float32, "out"), _dev(rx.counts, torch.int64, "counts"), _stream(stream, rx.out)))
+    return rx.out
 
 
 def rdma_imm(exps, batch_max: int = 64, stream=None):

@@ -107,3 +107,22 @@ def test_frame_params_layout_matches_header(sw):
     assert F.src_port_be.offset == 20 and F.dst_port_be.offset == 22
     assert F.job_id.offset == 24 and F.pool_index_start.offset == 32
     assert ctypes.sizeof(F) == 48
+
+
+def test_rx_frames_validation_without_gpu(sw):
+    L = sw.lib()
+    frames = (ctypes.c_uint8 * 4096)()
+    st = (ctypes.c_uint32 * 16)()
+    ex = (ctypes.c_int8 * 16)()
+    out = (ctypes.c_float * 16)()
+    f = L.sml_dequantize_frames
+    assert f(frames, 1, 1076, 16, 100, 1, 64, 0, ex, st, out, None, None) == sw.SML_ERR_UNSUPPORTED
+    assert f(frames, 1, 1076, 16, 256, 0, 64, 0, ex, st, out, None, None) == sw.SML_ERR_INVALID_ARG
+    assert f(frames, 1, 1076, 16, 256, 1, 0, 0, ex, st, out, None, None) == sw.SML_ERR_INVALID_ARG
+    assert f(frames, 0, 1076, 16, 256, 1, 64, 0, None, None, None, None, None) == sw.SML_OK
+    assert f(frames, 1, 1076, 16, 256, 1, 64, 0, ex, None, out, None, None) == sw.SML_ERR_INVALID_ARG
+    assert f(frames, 1, 1000, 16, 256, 1, 64, 0, ex, st, out, None, None) == sw.SML_ERR_ALIGNMENT
+    assert f(frames, 1, 1078, 16, 256, 1, 64, 0, ex, st, out, None, None) == sw.SML_ERR_ALIGNMENT
+    assert f(frames, 2 ** 32, 1076, 16, 256, 1, 64, 0, ex, st, out, None, None) == sw.SML_ERR_UNSUPPORTED
+    cnt = (ctypes.c_uint64 * 3)()
+    assert f(frames, 1, 1076, 16, 256, 1, 64, 0, ex, st, out, ctypes.addressof(cnt) + 4, None) == sw.SML_ERR_ALIGNMENT

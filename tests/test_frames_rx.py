@@ -1,0 +1,189 @@
+"""Receive side of the DPDK backend (the inverse direction):
+DpdkWorkerThread's receive loop + PostprocessSingle over the frames the
+switch returns (client_lib/src/backends/dpdk/dpdk_worker_thread.cc:300-345,
+ppp.cc:197-260).
+
+The "switch" here is the dummy backend's (dummy_backend.cc:72-84): every BE
+payload word x W, the exponent byte unchanged.  Streams are built the way a
+real rx ring sees them: frames reordered within windows of b packets (the
+switch returns a window's packets in any order, but packet p + b is only sent
+after packet p came back — so exponent k always precedes payload k),
+duplicates of already received packets (a retransmission answered twice; the
+later copy carries garbage and must be discarded), frames of another job
+and an out-of-range pkt_id.
+
+CPU tests pin the oracle's receive loop (oracle/sml_oracle.c:
+orc_dequantize_frames) to the plane-level oracle; GPU tests compare
+sml_dequantize_frames with it bit for bit.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+
+def _params(job_id):
+    import switchml_amd as sw
+    return sw.frame_params(job_id=job_id, pool_index_start=0, pool_index_shift=0, max_outstanding_pkts=64)
+
+
+def switch_return(sent, stride, P, W):
+    """DummyBackend::ProcessPacket on every frame: BE payload words x W (wrap)."""
+    f = sent.reshape(-1, stride).copy()
+    pl = f[:, 52:52 + 4 * P].copy().view(">u4").astype(np.uint64)
+    f[:, 52:52 + 4 * P] = ((pl * W) & 0xFFFFFFFF).astype(">u4").view(np.uint8)
+    return f
+
+
+def rx_stream(x, P, W, batch_max, job_id, seed, n_dups=3, n_wrong=2, bad_pid=True):
+    """(frames [F, stride] uint8 in rx order, number of frames that must be discarded)."""
+    stride = 52 + 4 * P
+    sent = O.build_frames(x, _params(job_id), P=P, num_workers=W, batch_max=batch_max)
+    ret = switch_return(sent, stride, P, W)
+    B = O.num_blocks(x.size, P)
+    b = min(B, batch_max)
+    rng = np.random.default_rng(seed)
+    order = []
+    for w0 in range(0, B + b, b):
+        win = list(range(w0, min(w0 + b, B + b)))
+        rng.shuffle(win)
+        order += win
+    rows = [ret[i] for i in order]
+    discard = 0
+    for _ in range(n_dups):                        # a later garbage copy of a received packet
+        pos = int(rng.integers(0, len(rows)))
+        dup = rows[pos].copy()
+        dup[50] ^= 0x5A
+        dup[52:] = rng.integers(0, 256, dup.size - 52, dtype=np.uint8)
+        rows.insert(int(rng.integers(pos + 1, len(rows) + 1)), dup)
+        discard += 1
+    for _ in range(n_wrong):                       # another job's frame, anywhere
+        src = rows[int(rng.integers(0, len(rows)))].copy()
+        src[43] = (job_id + 1) & 0xFF
+        src[52:] = 0xEE
+        rows.insert(int(rng.integers(0, len(rows) + 1)), src)
+        discard += 1
+    if bad_pid:
+        bad = rows[0].copy()
+        bad[44:48] = np.frombuffer(np.uint32(B + b + 5).tobytes(), dtype=np.uint8)
+        rows.insert(int(rng.integers(0, len(rows) + 1)), bad)
+        discard += 1
+    return np.stack(rows), discard
+
+
+def expected_planes(x, P, W):
+    """Plane-level oracle: quantize -> loopback x W -> dequantize."""
+    q = O.quantize(x, P, W)
+    e = O.exponents(x, P)
+    return O.dequantize(O.loopback_aggregate(q, W), e, x.size, P, W), e
+
+
+# ---------------------------------------------------------------- CPU --
+
+@pytest.mark.parametrize("P,n,W,bm", [(256, 1, 1, 64), (256, 5000, 3, 4), (64, 777, 2, 8),
+                                      (1024, 9000, 8, 2), (256, 256 * 20, 1, 64)])
+def test_oracle_rx_loop_matches_planes(P, n, W, bm):
+    x = O.splitmix_normal(100 + n, n)
+    frames, disc = rx_stream(x, P, W, bm, job_id=7, seed=n)
+    B = O.num_blocks(n, P)
+    b = min(B, bm)
+    rx = O.dequantize_frames(frames, frames.shape[0], frames.shape[1], O.RxState(n, P, bm), W, job_id=7)
+    want, e = expected_planes(x, P, W)
+    assert np.array_equal(rx.out.view(np.uint32), want.view(np.uint32))
+    assert np.array_equal(rx.exps, e)
+    assert rx.counts == [B + b, disc]
+
+
+def test_oracle_rx_loop_across_calls():
+    """The rx bitmap and exponents persist across rx bursts of one slice."""
+    P, n, W, bm = 256, 256 * 40 + 3, 2, 8
+    x = O.splitmix_normal(5, n)
+    frames, disc = rx_stream(x, P, W, bm, job_id=1, seed=9, n_dups=0, n_wrong=0, bad_pid=False)
+    # a late duplicate of the very first frame, in the last burst
+    frames = np.concatenate([frames, frames[:1]])
+    cuts = [0, 13, 31, frames.shape[0]]
+    rx = O.RxState(n, P, bm)
+    for a, c in zip(cuts[:-1], cuts[1:]):
+        O.dequantize_frames(frames[a:c], c - a, frames.shape[1], rx, W, job_id=1)
+    want, _ = expected_planes(x, P, W)
+    assert np.array_equal(rx.out.view(np.uint32), want.view(np.uint32))
+    B = O.num_blocks(n, P)
+    assert rx.counts == [B + min(B, bm), 1]
+
+
+# ---------------------------------------------------------------- GPU --
+
+def _run_gpu(torch, sw, frames, P, W, bm, job, n, where, calls=1):
+    dev = torch.device("cuda:0")
+    F, stride = frames.shape
+    t = torch.from_numpy(frames.reshape(-1).copy())
+    t = t.to(dev) if where == "device" else t.pin_memory()
+    rx = sw.RxSlice(n, P, bm, device=dev)
+    cuts = np.linspace(0, F, calls + 1).astype(int)
+    for a, c in zip(cuts[:-1], cuts[1:]):
+        sw.dequantize_frames(t[a * stride:c * stride], int(c - a), rx, num_workers=W, job_id=job, stride=stride)
+    torch.cuda.synchronize()
+    return rx.out.cpu().numpy(), rx.exps.cpu().numpy(), [int(v) for v in rx.counts.cpu()]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,n,W,bm", [(256, 1, 1, 64), (256, 5000, 3, 4), (64, 777, 2, 8), (128, 4099, 5, 16),
+                                      (512, 3000, 4, 3), (1024, 9000, 8, 2), (256, 300_001, 7, 64)])
+@pytest.mark.parametrize("where", ["device", "pinned"])
+def test_rx_frames_match_oracle(cuda, P, n, W, bm, where):
+    torch = cuda
+    import switchml_amd as sw
+    x = O.splitmix_normal(200 + n, n)
+    frames, _ = rx_stream(x, P, W, bm, job_id=0x3C, seed=n + P)
+    ref = O.dequantize_frames(frames, frames.shape[0], frames.shape[1], O.RxState(n, P, bm), W, job_id=0x3C)
+    out, exps, cnt = _run_gpu(torch, sw, frames, P, W, bm, 0x3C, n, where)
+    assert np.array_equal(out.view(np.uint32), ref.out.view(np.uint32))
+    assert np.array_equal(exps, ref.exps)
+    assert cnt == ref.counts
+
+
+@pytest.mark.gpu
+def test_rx_frames_across_calls(cuda):
+    torch = cuda
+    import switchml_amd as sw
+    P, n, W, bm = 256, 256 * 300 + 17, 3, 16
+    x = O.splitmix_normal(77, n)
+    frames, _ = rx_stream(x, P, W, bm, job_id=9, seed=3)
+    frames = np.concatenate([frames, frames[5:9]])           # late duplicates in the last burst
+    ref = O.RxState(n, P, bm)
+    cuts = np.linspace(0, frames.shape[0], 5).astype(int)
+    for a, c in zip(cuts[:-1], cuts[1:]):
+        O.dequantize_frames(frames[a:c], int(c - a), frames.shape[1], ref, W, job_id=9)
+    out, exps, gcnt = _run_gpu(torch, sw, frames, P, W, bm, 9, n, "device", calls=4)
+    assert np.array_equal(out.view(np.uint32), ref.out.view(np.uint32))
+    assert np.array_equal(exps, ref.exps)
+    assert gcnt == ref.counts and ref.counts[1] >= 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [1, 6])
+def test_frames_tx_rx_round_trip_equals_fused_loopback(cuda, W):
+    """Size-independent property at a large size: quantize into frames ->
+    switch (x W on the wire words) -> dequantize from frames gives exactly the
+    fused loopback round trip (sml_roundtrip_loopback)."""
+    torch = cuda
+    import switchml_amd as sw
+    P, bm = 256, 64
+    n = 16 * 2 ** 20 + 333
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(W)
+    x = torch.randn(n, device=dev, generator=g)
+    stride = sw.frame_bytes(P)
+    fr = sw.quantize_pack_frames(x, sw.frame_params(job_id=4), packet_numel=P, num_workers=W, batch_max=bm)
+    F = fr.numel() // stride
+    v = fr.view(F, stride)[:, 52:52 + 4 * P].contiguous().view(torch.int32)
+    v = (v.view(torch.uint8).view(F, P, 4).flip(-1).contiguous().view(torch.int32) * W)   # ntohl, x W (wraps)
+    v = v.view(torch.uint8).view(F, P, 4).flip(-1).contiguous().view(F, 4 * P)           # htonl
+    fr.view(F, stride)[:, 52:52 + 4 * P] = v
+    rx = sw.RxSlice(n, P, bm, device=dev)
+    sw.dequantize_frames(fr, F, rx, num_workers=W, job_id=4)
+    ref = sw.roundtrip_loopback(x, P, W)
+    torch.cuda.synchronize()
+    assert torch.equal(rx.out.view(torch.int32), ref.view(torch.int32))
+    assert rx.counts.tolist() == [F, 0]
