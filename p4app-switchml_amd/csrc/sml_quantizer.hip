@@ -509,11 +509,26 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
     }
 }
 
-// Pass 2: PostprocessSingle for every winning frame, 1024 payload elements per
-// wave (1024 / P frames; lane-chunk c = u*64 + lane is 16 bytes of frame c / (P/4)).
-// The exponent of block k comes from the frame that won pkt_id k in this call
-// (state[k] is its tag) or, if k arrived in an earlier call, from exps[k] —
-// never from an exps[] entry this launch writes.
+// Pass 2: the winning frames with pkt_id < B store their exponent byte
+// (PostprocessSingle's scaling_factors_[pkt_id], ppp.cc:254-260), so pass 3
+// reads every block's exponent without a dependent frame lookup.
+__global__ __launch_bounds__(kBlockThreads) void k_rx_exps(RxArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
+        bool job_ok;
+        const uint32_t pid = rx_pkt_id(a, f, &job_ok);
+        if (job_ok && pid < a.nblocks && a.state[pid] == rx_tag(f)) a.exps[pid] = (int8_t)a.frames[f * a.stride + 50];
+    }
+}
+
+// Pass 3: dequantize the payload of every winning frame with pkt_id >= b,
+// 1024 payload elements per wave (1024 / P frames; lane-chunk c = u*64 + lane
+// is 16 bytes of frame c / (P/4)), then mark the winners received.  The
+// payload loads are issued first, independent of the header, so they overlap
+// the header -> state / exponent lookups.  Every chunk of a frame belongs to
+// this wave and all its state reads precede the commit stores, so a winner
+// can retire its pkt_id (kRxDone) here: a duplicate that reads kRxDone
+// instead of the winner's tag loses just the same.
 template <int P>
 __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     __shared__ float lut[256];
@@ -525,53 +540,42 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     const uint64_t ntiles = (a.nframes + kFramesPerTile - 1) / kFramesPerTile;
     for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
         u4a w[kU];
-        float s[kU];
-        int64_t dst[kU];                       // output element index of the chunk, -1 = none
-        uint32_t n[kU];
+        uint32_t pid[kU];
+        bool ok[kU];
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-            dst[u] = -1;
             const int c = u * kWave + lane;
             const uint64_t f = t * kFramesPerTile + c / kChunksPerFrame;
-            const uint32_t i = (uint32_t)(c % kChunksPerFrame);
-            if (f >= a.nframes) continue;
-            bool job_ok;
-            const uint32_t pid = rx_pkt_id(a, f, &job_ok);
-            if (!job_ok || pid >= a.nblocks + a.b || a.state[pid] != rx_tag(f)) continue;
+            ok[u] = f < a.nframes;
+            if (!ok[u]) continue;
             const uint8_t* fr = a.frames + f * a.stride;
-            if (i == 0 && pid < a.nblocks) a.exps[pid] = (int8_t)fr[50];
-            if (pid < a.b) continue;
-            const uint64_t k = pid - a.b;
-            const uint32_t sk = a.state[k];
-            int8_t e;
-            if (sk != 0u && sk != kRxDone) e = (int8_t)a.frames[(uint64_t)(0xFFFFFFFEu - sk) * a.stride + 50];
-            else e = a.exps[k];
-            s[u] = lut[(uint8_t)e];
-            const uint64_t off = k * P + 4ull * i;
-            if (off >= a.numel) continue;
-            n[u] = a.numel - off < 4 ? (uint32_t)(a.numel - off) : 4u;
-            dst[u] = (int64_t)off;
-            w[u] = *reinterpret_cast<const u4a*>(fr + 52 + 16ull * i);
+            w[u] = *reinterpret_cast<const u4a*>(fr + 52 + 16ull * (c % kChunksPerFrame));
+            bool job_ok;
+            pid[u] = rx_pkt_id(a, f, &job_ok);
+            ok[u] = job_ok && pid[u] < a.nblocks + a.b;
+        }
+        float s[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            if (!ok[u]) continue;
+            const uint64_t f = t * kFramesPerTile + (u * kWave + lane) / kChunksPerFrame;
+            ok[u] = a.state[pid[u]] == rx_tag(f);
+            s[u] = pid[u] >= a.b ? lut[(uint8_t)a.exps[pid[u] - a.b]] : 0.0f;
         }
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-            if (dst[u] < 0) continue;
+            if (!ok[u] || pid[u] < a.b) continue;
+            const uint64_t off = (uint64_t)(pid[u] - a.b) * P + 4ull * ((u * kWave + lane) % kChunksPerFrame);
+            if (off >= a.numel) continue;
             const f4 o = mkf4(dequantize1(bswap(w[u].x), s[u]), dequantize1(bswap(w[u].y), s[u]),
                               dequantize1(bswap(w[u].z), s[u]), dequantize1(bswap(w[u].w), s[u]));
-            float* p = a.out + dst[u];
-            if (n[u] == 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o;
-            else store4_guarded(p, o, 0, n[u]);
+            float* p = a.out + off;
+            if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o;
+            else store4_guarded(p, o, 0, a.numel - off);
         }
-    }
-}
-
-// Pass 3: the winners' pkt_ids become "received" for later calls.
-__global__ __launch_bounds__(kBlockThreads) void k_rx_commit(RxArgs a) {
-    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
-    for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
-        bool job_ok;
-        const uint32_t pid = rx_pkt_id(a, f, &job_ok);
-        if (job_ok && pid < a.nblocks + a.b && a.state[pid] == rx_tag(f)) a.state[pid] = kRxDone;
+#pragma unroll
+        for (int u = 0; u < kU; u++)
+            if (ok[u] && (u * kWave + lane) % kChunksPerFrame == 0) a.state[pid[u]] = kRxDone;
     }
 }
 
@@ -1114,9 +1118,9 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     hipStream_t st = (hipStream_t)stream;
     uint64_t g1 = (num_frames + 4ull * kBlockThreads - 1) / (4ull * kBlockThreads);   // 4 frames per thread
     k_rx_claim<<<(uint32_t)(g1 ? g1 : 1), kBlockThreads, 0, st>>>(a);
+    k_rx_exps<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
     const uint64_t ntiles = (num_frames * P + kTileElems - 1) / kTileElems;
     launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
-    k_rx_commit<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
     return launch_check();
 }
 

@@ -131,7 +131,7 @@ def _run_gpu(torch, sw, frames, P, W, bm, job, n, where, calls=1):
                                       (512, 3000, 4, 3), (1024, 9000, 8, 2), (256, 300_001, 7, 64)])
 @pytest.mark.parametrize("where", ["device", "pinned"])
 def test_rx_frames_match_oracle(cuda, P, n, W, bm, where):
-    torch = cuda
+    import torch
     import switchml_amd as sw
     x = O.splitmix_normal(200 + n, n)
     frames, _ = rx_stream(x, P, W, bm, job_id=0x3C, seed=n + P)
@@ -144,7 +144,7 @@ def test_rx_frames_match_oracle(cuda, P, n, W, bm, where):
 
 @pytest.mark.gpu
 def test_rx_frames_across_calls(cuda):
-    torch = cuda
+    import torch
     import switchml_amd as sw
     P, n, W, bm = 256, 256 * 300 + 17, 3, 16
     x = O.splitmix_normal(77, n)
@@ -166,7 +166,7 @@ def test_frames_tx_rx_round_trip_equals_fused_loopback(cuda, W):
     """Size-independent property at a large size: quantize into frames ->
     switch (x W on the wire words) -> dequantize from frames gives exactly the
     fused loopback round trip (sml_roundtrip_loopback)."""
-    torch = cuda
+    import torch
     import switchml_amd as sw
     P, bm = 256, 64
     n = 16 * 2 ** 20 + 333

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Frames tx + rx on the 256 MiB bucket, for rocprofv3 --kernel-trace --stats:
+quantize into DPDK frames (device), then the receive side over the same
+frames (W = 1 loopback), `reps` times each.  Prints wall-clock rates."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "p4app-switchml_amd")]
+
+import torch  # noqa: E402
+import switchml_amd as sw  # noqa: E402
+
+
+def main(N=64 * 2 ** 20, P=256, bm=64, reps=20):
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(42)
+    x = torch.randn(N, device=dev, generator=g)
+    B = sw.num_blocks(N, P)
+    F = B + min(B, bm)
+    fb = F * sw.frame_bytes(P)
+    frames = torch.empty(fb, dtype=torch.uint8, device=dev)
+    fp = sw.frame_params(max_outstanding_pkts=bm)
+    rx = sw.RxSlice(N, P, bm, device=dev)
+    res = {}
+    for name, fn in (("tx", lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=bm, frames=frames)),
+                     ("rx", lambda: (rx.state.zero_(), sw.dequantize_frames(frames, F, rx)))):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        res[name] = {"us": round(t * 1e6, 1), "GBps": round((4 * N + fb) / t / 1e9, 1)}
+    ref = sw.roundtrip_loopback(x, P, 1)
+    torch.cuda.synchronize()
+    res["rx_equals_roundtrip"] = bool(torch.equal(ref.view(torch.int32), rx.out.view(torch.int32)))
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
