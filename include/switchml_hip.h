@@ -179,20 +179,22 @@ sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_
  * before — in an earlier call for the slice, or earlier in `frames` (the
  * first copy wins, :316-330); a pkt_id >= B + b is discarded too.  Every
  * accepted frame is PostprocessSingle'd (ppp.cc:197-260): frame pkt_id < B
- * gives the global exponent d_exps[pkt_id] = byte 50; frame pkt_id >= b
- * gives the aggregated payload of block k = pkt_id - b (BE words at byte 52),
- * dequantized with exponent k into d_out[k*P .. k*P + min(P, numel - k*P)).
- * As in the reference, the frame carrying exponent k must come in this call
- * or an earlier one for the slice (the switch returns it first).
- *   d_exps:   int8[B], in/out; persists across the calls of a slice
- *   d_state:  uint32[B + b], the rx bitmap: zero-filled by the caller before
- *             the slice's first call (rte_bitmap_reset), persists across calls
+ * gives the global exponent of block pkt_id (byte 50, also stored to
+ * d_exps[pkt_id]); frame pkt_id >= b gives the aggregated payload of block
+ * k = pkt_id - b (BE words at byte 52), dequantized with exponent k into
+ * d_out[k*P .. k*P + min(P, numel - k*P)).  As in the reference, the frame
+ * carrying exponent k must come in this call or an earlier one for the slice
+ * (the switch returns it first).
+ *   d_exps:   int8[B], out (the slice's received global exponents)
+ *   d_state:  uint64[B + b], 8-B aligned, the rx bitmap (+ received
+ *             exponents): zero-filled by the caller before the slice's first
+ *             call (rte_bitmap_reset), persists across its calls
  *   d_counts: uint64[2] {accepted, discarded}, added to; nullable, 8-B aligned
- * Three launches on `stream`: claim, exponents, dequantize + commit. */
+ * Two launches on `stream`: claim, dequantize + commit. */
 sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint64_t frame_stride,
                                    uint64_t numel, uint32_t packet_numel, uint16_t num_workers,
                                    uint32_t batch_max, uint64_t job_id, int8_t* d_exps,
-                                   uint32_t* d_state, float* d_out, uint64_t* d_counts,
+                                   uint64_t* d_state, float* d_out, uint64_t* d_counts,
                                    void* stream);
 
 /* ---- RDMA messages --------------------------------------

@@ -456,9 +456,12 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) 
 // ------------------------------------------------- DPDK frames, receive side
 //
 // The rx bitmap of DpdkWorkerThread (dpdk_worker_thread.cc:316-342) becomes a
-// per-slice state word per packet id: 0 = not received, kRxDone = received
-// in an earlier call, otherwise the claim tag of the frame that won it in the
-// current call (larger tag = earlier frame, so atomicMax picks the first).
+// per-slice 64-bit state word per packet id: high half 0 = not received,
+// kRxDone = received in an earlier call, otherwise the claim tag of the frame
+// that won it in the current call (larger tag = earlier frame, so a 64-bit
+// atomicMax picks the first copy); low byte = that frame's exponent byte, so
+// the winner's exponent travels with the claim (PostprocessSingle's
+// scaling_factors_[pkt_id], ppp.cc:254-260) and needs no separate pass.
 constexpr uint32_t kRxDone = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t rx_tag(uint64_t f) { return 0xFFFFFFFEu - (uint32_t)f; }
 
@@ -469,7 +472,7 @@ struct RxArgs {
     uint64_t numel;
     uint64_t nblocks;           // B
     uint64_t b;                 // extra batch
-    uint32_t* state;            // [B + b]
+    unsigned long long* state;  // [B + b]
     int8_t* exps;               // [B]
     float* out;
     unsigned long long* counts; // {accepted, discarded} or nullptr
@@ -477,14 +480,26 @@ struct RxArgs {
     uint32_t job;               // (uint8_t)job_id
 };
 
-__device__ __forceinline__ uint32_t rx_pkt_id(const RxArgs& a, uint64_t f, bool* job_ok) {
-    const uint8_t* fr = a.frames + f * a.stride;
-    *job_ok = fr[43] == a.job;
-    return *reinterpret_cast<const uint32_t*>(fr + 44);
+// Header dwords 10..12 of frame f: short_job_id = byte 43, pkt_id = bytes
+// 44-47 (host order), exponent = byte 50.
+struct RxHdr {
+    uint32_t pid;
+    uint32_t exp;
+    bool ok;                    // this job, pkt_id in range
+};
+
+__device__ __forceinline__ RxHdr rx_header(const RxArgs& a, uint64_t f) {
+    const uint32_t* h = reinterpret_cast<const uint32_t*>(a.frames + f * a.stride + 40);
+    const uint32_t d10 = h[0], d11 = h[1], d12 = h[2];
+    RxHdr r;
+    r.pid = d11;
+    r.exp = (d12 >> 16) & 0xffu;
+    r.ok = (d10 >> 24) == a.job && (uint64_t)d11 < a.nblocks + a.b;
+    return r;
 }
 
-// Pass 1: every frame of another job, of an out-of-range or already received
-// pkt_id is discarded; the others claim their pkt_id (first frame wins).
+// Pass 1, thread per frame: frames of another job, out-of-range or already
+// received pkt_ids are discarded; the others claim their pkt_id.
 __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
     __shared__ uint32_t acc[2];
     if (threadIdx.x < 2) acc[threadIdx.x] = 0;
@@ -492,11 +507,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
     uint32_t mine_acc = 0, mine_seen = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
     for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
-        bool job_ok;
-        const uint32_t pid = rx_pkt_id(a, f, &job_ok);
+        const RxHdr h = rx_header(a, f);
         mine_seen++;
-        if (!job_ok || pid >= a.nblocks + a.b) continue;
-        if (atomicMax(a.state + pid, rx_tag(f)) == 0u) mine_acc++;   // first claim of a new pkt_id
+        if (!h.ok) continue;
+        const unsigned long long v = ((unsigned long long)rx_tag(f) << 32) | h.exp;
+        if (atomicMax(a.state + h.pid, v) == 0ull) mine_acc++;     // first claim of a new pkt_id
     }
     if (a.counts) {
         atomicAdd(&acc[0], mine_acc);
@@ -509,26 +524,14 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
     }
 }
 
-// Pass 2: the winning frames with pkt_id < B store their exponent byte
-// (PostprocessSingle's scaling_factors_[pkt_id], ppp.cc:254-260), so pass 3
-// reads every block's exponent without a dependent frame lookup.
-__global__ __launch_bounds__(kBlockThreads) void k_rx_exps(RxArgs a) {
-    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
-    for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
-        bool job_ok;
-        const uint32_t pid = rx_pkt_id(a, f, &job_ok);
-        if (job_ok && pid < a.nblocks && a.state[pid] == rx_tag(f)) a.exps[pid] = (int8_t)a.frames[f * a.stride + 50];
-    }
-}
-
-// Pass 3: dequantize the payload of every winning frame with pkt_id >= b,
-// 1024 payload elements per wave (1024 / P frames; lane-chunk c = u*64 + lane
-// is 16 bytes of frame c / (P/4)), then mark the winners received.  The
-// payload loads are issued first, independent of the header, so they overlap
-// the header -> state / exponent lookups.  Every chunk of a frame belongs to
-// this wave and all its state reads precede the commit stores, so a winner
-// can retire its pkt_id (kRxDone) here: a duplicate that reads kRxDone
-// instead of the winner's tag loses just the same.
+// Pass 2: PostprocessSingle for every winning frame, 1024 payload elements per
+// wave (1024 / P frames; lane-chunk c = u*64 + lane is 16 bytes of frame
+// c / (P/4)), then the winners retire their pkt_id.  The payload loads are
+// issued first, independent of the header; the exponent of block k is the low
+// byte of state[k], whoever holds it (a winner of this call or kRxDone).
+// Every chunk of a frame belongs to this wave and all its state reads precede
+// the commit stores, so a duplicate elsewhere that reads kRxDone instead of
+// the winner's tag loses just the same; the commit keeps the exponent byte.
 template <int P>
 __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     __shared__ float lut[256];
@@ -540,32 +543,28 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     const uint64_t ntiles = (a.nframes + kFramesPerTile - 1) / kFramesPerTile;
     for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
         u4a w[kU];
-        uint32_t pid[kU];
-        bool ok[kU];
+        RxHdr h[kU];
 #pragma unroll
         for (int u = 0; u < kU; u++) {
             const int c = u * kWave + lane;
             const uint64_t f = t * kFramesPerTile + c / kChunksPerFrame;
-            ok[u] = f < a.nframes;
-            if (!ok[u]) continue;
-            const uint8_t* fr = a.frames + f * a.stride;
-            w[u] = *reinterpret_cast<const u4a*>(fr + 52 + 16ull * (c % kChunksPerFrame));
-            bool job_ok;
-            pid[u] = rx_pkt_id(a, f, &job_ok);
-            ok[u] = job_ok && pid[u] < a.nblocks + a.b;
+            h[u].ok = false;
+            if (f >= a.nframes) continue;
+            w[u] = *reinterpret_cast<const u4a*>(a.frames + f * a.stride + 52 + 16ull * (c % kChunksPerFrame));
+            h[u] = rx_header(a, f);
         }
         float s[kU];
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-            if (!ok[u]) continue;
+            if (!h[u].ok) continue;
             const uint64_t f = t * kFramesPerTile + (u * kWave + lane) / kChunksPerFrame;
-            ok[u] = a.state[pid[u]] == rx_tag(f);
-            s[u] = pid[u] >= a.b ? lut[(uint8_t)a.exps[pid[u] - a.b]] : 0.0f;
+            h[u].ok = (uint32_t)(a.state[h[u].pid] >> 32) == rx_tag(f);
+            s[u] = h[u].pid >= a.b ? lut[(uint32_t)a.state[h[u].pid - a.b] & 0xffu] : 0.0f;
         }
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-            if (!ok[u] || pid[u] < a.b) continue;
-            const uint64_t off = (uint64_t)(pid[u] - a.b) * P + 4ull * ((u * kWave + lane) % kChunksPerFrame);
+            if (!h[u].ok || h[u].pid < a.b) continue;
+            const uint64_t off = (uint64_t)(h[u].pid - a.b) * P + 4ull * ((u * kWave + lane) % kChunksPerFrame);
             if (off >= a.numel) continue;
             const f4 o = mkf4(dequantize1(bswap(w[u].x), s[u]), dequantize1(bswap(w[u].y), s[u]),
                               dequantize1(bswap(w[u].z), s[u]), dequantize1(bswap(w[u].w), s[u]));
@@ -574,8 +573,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             else store4_guarded(p, o, 0, a.numel - off);
         }
 #pragma unroll
-        for (int u = 0; u < kU; u++)
-            if (ok[u] && (u * kWave + lane) % kChunksPerFrame == 0) a.state[pid[u]] = kRxDone;
+        for (int u = 0; u < kU; u++) {
+            if (!h[u].ok || (u * kWave + lane) % kChunksPerFrame != 0) continue;
+            a.state[h[u].pid] = ((unsigned long long)kRxDone << 32) | h[u].exp;
+            if (h[u].pid < a.nblocks) a.exps[h[u].pid] = (int8_t)h[u].exp;
+        }
     }
 }
 
@@ -1093,7 +1095,7 @@ sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_
 
 sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint64_t stride,
                                    uint64_t numel, uint32_t P, uint16_t W, uint32_t batch_max,
-                                   uint64_t job_id, int8_t* d_exps, uint32_t* d_state, float* d_out,
+                                   uint64_t job_id, int8_t* d_exps, uint64_t* d_state, float* d_out,
                                    uint64_t* d_counts, void* stream) {
     if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
     if (W == 0 || batch_max == 0) return SML_ERR_INVALID_ARG;
@@ -1101,7 +1103,7 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     if (num_frames >= 0xFFFFFFFEull) return SML_ERR_UNSUPPORTED;
     if (!frames || !d_state || (numel && (!d_exps || !d_out))) return SML_ERR_INVALID_ARG;
     if (!aligned4(frames) || !aligned4(d_out) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
-    if (d_counts && ((uintptr_t)d_counts & 7u)) return SML_ERR_ALIGNMENT;
+    if (((uintptr_t)d_state & 7u) || (d_counts && ((uintptr_t)d_counts & 7u))) return SML_ERR_ALIGNMENT;
     RxArgs a;
     a.frames = static_cast<const uint8_t*>(frames);
     a.nframes = num_frames;
@@ -1109,16 +1111,14 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     a.numel = numel;
     a.nblocks = sml_num_blocks(numel, P);
     a.b = a.nblocks < batch_max ? a.nblocks : batch_max;
-    a.state = d_state;
+    a.state = reinterpret_cast<unsigned long long*>(d_state);
     a.exps = d_exps;
     a.out = d_out;
     a.counts = reinterpret_cast<unsigned long long*>(d_counts);
     a.W = W;
     a.job = (uint8_t)job_id;
     hipStream_t st = (hipStream_t)stream;
-    uint64_t g1 = (num_frames + 4ull * kBlockThreads - 1) / (4ull * kBlockThreads);   // 4 frames per thread
-    k_rx_claim<<<(uint32_t)(g1 ? g1 : 1), kBlockThreads, 0, st>>>(a);
-    k_rx_exps<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
+    k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
     const uint64_t ntiles = (num_frames * P + kTileElems - 1) / kTileElems;
     launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
     return launch_check();

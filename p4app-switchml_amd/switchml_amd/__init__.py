@@ -294,7 +294,7 @@ class RxSlice:
         self.numel, self.packet_numel, self.batch_max = numel, packet_numel, batch_max
         B = num_blocks(numel, packet_numel)
         self.exps = torch.zeros(B, dtype=torch.int8, device=device)
-        self.state = torch.zeros(max(1, B + min(B, batch_max)), dtype=torch.int32, device=device)
+        self.state = torch.zeros(max(1, B + min(B, batch_max)), dtype=torch.int64, device=device)
         self.counts = torch.zeros(2, dtype=torch.int64, device=device)
         self.out = out if out is not None else torch.zeros(numel, dtype=torch.float32, device=device)
 
@@ -307,7 +307,7 @@ def dequantize_frames(frames, num_frames: int, rx: RxSlice, num_workers: int = 1
     stride = stride or frame_bytes(rx.packet_numel)
     _check("sml_dequantize_frames", lib().sml_dequantize_frames(
         _dev(frames, torch.uint8, "frames"), num_frames, stride, rx.numel, rx.packet_numel, num_workers,
-        rx.batch_max, job_id, _dev(rx.exps, torch.int8, "exps"), _dev(rx.state, torch.int32, "state"),
+        rx.batch_max, job_id, _dev(rx.exps, torch.int8, "exps"), _dev(rx.state, torch.int64, "state"),
         _dev(rx.out, torch.float32, "out"), _dev(rx.counts, torch.int64, "counts"), _stream(stream, rx.out)))
     return rx.out
 

@@ -112,7 +112,7 @@ def test_frame_params_layout_matches_header(sw):
 def test_rx_frames_validation_without_gpu(sw):
     L = sw.lib()
     frames = (ctypes.c_uint8 * 4096)()
-    st = (ctypes.c_uint32 * 16)()
+    st = (ctypes.c_uint64 * 16)()
     ex = (ctypes.c_int8 * 16)()
     out = (ctypes.c_float * 16)()
     f = L.sml_dequantize_frames
