@@ -367,3 +367,19 @@ def splitmix_normal(seed: int, n: int, sigma: float = 1.0) -> np.ndarray:
     z[0::2] = rad * np.cos(2 * np.pi * u2)
     z[1::2] = rad * np.sin(2 * np.pi * u2)
     return (z[:n] * sigma).astype(np.float32)
+
+
+def splitmix_grad(seed: int, n: int) -> np.ndarray:
+    """Gradient-like fp32 from integer arithmetic only (exact on every host,
+    unlike a libm-based Box-Muller): a signed 24-bit mantissa from splitmix64
+    scaled by 2^-(24 + k), k in 0..15, so magnitudes span ~2^-40..2^-1 and
+    blocks get different exponents.  Used for the full-size golden digests."""
+    i = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + i * np.uint64(0xBF58476D1CE4E5B9)) & np.uint64(0xFFFFFFFFFFFFFFFF)
+        z = ((z ^ (z >> np.uint64(31))) * np.uint64(0x94D049BB133111EB)) & np.uint64(0xFFFFFFFFFFFFFFFF)
+        z = z ^ (z >> np.uint64(29))
+    mant = (z >> np.uint64(40)).astype(np.int64) - (1 << 23)            # [-2^23, 2^23)
+    k = ((i >> np.uint64(8)) * np.uint64(7) + (z & np.uint64(1))) % np.uint64(16)   # varies per 256-block
+    return np.ldexp(mant.astype(np.float32), -(24 + k.astype(np.int32))).astype(np.float32)
+

@@ -1,0 +1,94 @@
+"""Generate tests/golden/digests.json — SHA-256 digests of the oracle's
+planes at the full BASELINE sizes ("SHA-256 of (BE payload
+plane, exponent plane, dequant output) for 64 MiB and 256 MiB").
+
+The GPU tests (tests/test_golden_digests.py) recompute the same planes with
+the HIP kernels and compare digests, so the full-size configurations are
+pinned bit for bit without the oracle on the GPU box; the CPU tests recompute
+them with the oracle to keep the fixture and the oracle in step.
+
+Inputs are integer-exact generators (identical bytes on every host):
+  randbits  the reference's own random-float recipe on glibc rand()
+            (allreduce_benchmark/main.cc:197-205), O.c_ref_random_floats
+  pattern   float(i) * (-1)^i (allreduce_benchmark/main.cc:207-212)
+  grad      O.splitmix_grad: 24-bit mantissas scaled by 2^-(24..39)
+
+Planes per slice (FIFO slices of fifo_scheduler.cc:93-109; blocks restart
+at every slice start): exps (int8[B]), payload (BE int32[B*P] = wire bytes),
+out = dequantize(loopback_xW(payload), exps) (float32[numel]).  Digests run
+over the slices in order.  NaN outputs — the 0/0 of a zero scale, when
+W * 2^e overflows float (e = 127, W >= 2) — are canonicalized to 0x7fc00000
+before hashing: x86 divides to the negative default NaN 0xffc00000, gfx950
+to the positive one; that sign is the one non-bit-exact case.
+
+Run: python tests/golden/make_digests.py   (rewrites digests.json, ~1 min)
+"""
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as O  # noqa: E402
+
+CASES = [
+    # name, generator, seed, numel, P, W, T
+    ("cfg2_randbits_T1", "randbits", 1, 16_777_216, 256, 1, 1),
+    ("cfg2_grad_T4", "grad", 42, 16_777_216, 256, 1, 4),
+    ("cfg2_pattern_W2", "pattern", 0, 16_777_216, 256, 2, 1),
+    ("cfg3_grad_W2", "grad", 43, 67_108_864, 256, 2, 1),
+    ("cfg3_randbits_W8_T4", "randbits", 7, 67_108_864, 256, 8, 4),
+    ("rdma_grad_P1024_W3", "grad", 44, 16_777_216 + 1000, 1024, 3, 1),
+]
+
+
+def make_input(gen, seed, n):
+    if gen == "randbits":
+        return O.c_ref_random_floats(seed, n)
+    if gen == "pattern":
+        return O.ref_pattern_floats(n)
+    if gen == "grad":
+        return O.splitmix_grad(seed, n)
+    raise ValueError(gen)
+
+
+def canonical_nan(out):
+    import numpy as np
+    b = out.view(np.uint32).copy()
+    b[np.isnan(out)] = 0x7FC00000
+    return b
+
+
+def oracle_digests(gen, seed, numel, P, W, T):
+    x = make_input(gen, seed, numel)
+    h = {k: hashlib.sha256() for k in ("input", "exps", "payload", "out")}
+    h["input"].update(x.tobytes())
+    for t in range(T):
+        off, n = O.slice_geometry(numel, T, t)
+        if n == 0:
+            continue
+        xs = x[off:off + n]
+        e = O.exponents(xs, P)
+        q = O.quantize(xs, P, W)
+        out = O.dequantize(O.loopback_aggregate(q, W), e, n, P, W)
+        h["exps"].update(e.tobytes())
+        h["payload"].update(q.tobytes())
+        h["out"].update(canonical_nan(out).tobytes())
+    return {k: v.hexdigest() for k, v in h.items()}
+
+
+def main():
+    res = {}
+    for name, gen, seed, numel, P, W, T in CASES:
+        res[name] = {"gen": gen, "seed": seed, "numel": numel, "packet_numel": P, "num_workers": W,
+                     "num_slices": T, "sha256": oracle_digests(gen, seed, numel, P, W, T)}
+        print(name, res[name]["sha256"]["out"][:16], flush=True)
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "digests.json"), "w") as f:
+        json.dump(res, f, indent=1)
+        f.write("\n")
+
+
+if __name__ == "__main__":
+    main()
