@@ -499,27 +499,30 @@ __device__ __forceinline__ RxHdr rx_header(const RxArgs& a, uint64_t f) {
 }
 
 // Pass 1, thread per frame: frames of another job, out-of-range or already
-// received pkt_ids are discarded; the others claim their pkt_id.
+// received pkt_ids are discarded; the others claim their pkt_id.  Counting:
+// accepted = frames - discarded, so block 0 adds the frame count once and only
+// workgroups that saw a discard touch the counters (same-address atomics from
+// every workgroup serialize in one L2 channel: ~40 us at 262 k frames).
 __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
-    __shared__ uint32_t acc[2];
-    if (threadIdx.x < 2) acc[threadIdx.x] = 0;
+    __shared__ uint32_t disc;
+    if (threadIdx.x == 0) disc = 0;
     __syncthreads();
-    uint32_t mine_acc = 0, mine_seen = 0;
+    uint32_t mine = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
     for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
         const RxHdr h = rx_header(a, f);
-        mine_seen++;
-        if (!h.ok) continue;
+        if (!h.ok) { mine++; continue; }
         const unsigned long long v = ((unsigned long long)rx_tag(f) << 32) | h.exp;
-        if (atomicMax(a.state + h.pid, v) == 0ull) mine_acc++;     // first claim of a new pkt_id
+        if (atomicMax(a.state + h.pid, v) != 0ull) mine++;          // duplicate or received earlier
     }
     if (a.counts) {
-        atomicAdd(&acc[0], mine_acc);
-        atomicAdd(&acc[1], mine_seen);
+        if (mine) atomicAdd(&disc, mine);
         __syncthreads();
-        if (threadIdx.x == 0 && acc[1]) {
-            atomicAdd(a.counts + 0, (unsigned long long)acc[0]);
-            atomicAdd(a.counts + 1, (unsigned long long)(acc[1] - acc[0]));
+        if (threadIdx.x == 0) {
+            unsigned long long acc = blockIdx.x == 0 ? (unsigned long long)a.nframes : 0ull;
+            acc -= disc;                                                 // mod 2^64
+            if (acc) atomicAdd(a.counts + 0, acc);
+            if (disc) atomicAdd(a.counts + 1, (unsigned long long)disc);
         }
     }
 }
@@ -532,20 +535,23 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
 // Every chunk of a frame belongs to this wave and all its state reads precede
 // the commit stores, so a duplicate elsewhere that reads kRxDone instead of
 // the winner's tag loses just the same; the commit keeps the exponent byte.
+constexpr int kRxU = 4;                        // 16-B chunks per lane per iteration
+constexpr int kRxTileElems = kRxU * kWave * 4;
+
 template <int P>
 __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     __shared__ float lut[256];
     build_lut(lut, a.W);
     constexpr int kChunksPerFrame = P / 4;     // 16-B chunks per payload
-    constexpr int kFramesPerTile = kTileElems / P;
+    constexpr int kFramesPerTile = kRxTileElems / P;
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t ntiles = (a.nframes + kFramesPerTile - 1) / kFramesPerTile;
     for (uint64_t t = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
-        u4a w[kU];
-        RxHdr h[kU];
+        u4a w[kRxU];
+        RxHdr h[kRxU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
+        for (int u = 0; u < kRxU; u++) {
             const int c = u * kWave + lane;
             const uint64_t f = t * kFramesPerTile + c / kChunksPerFrame;
             h[u].ok = false;
@@ -553,16 +559,16 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             w[u] = *reinterpret_cast<const u4a*>(a.frames + f * a.stride + 52 + 16ull * (c % kChunksPerFrame));
             h[u] = rx_header(a, f);
         }
-        float s[kU];
+        float s[kRxU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
+        for (int u = 0; u < kRxU; u++) {
             if (!h[u].ok) continue;
             const uint64_t f = t * kFramesPerTile + (u * kWave + lane) / kChunksPerFrame;
             h[u].ok = (uint32_t)(a.state[h[u].pid] >> 32) == rx_tag(f);
             s[u] = h[u].pid >= a.b ? lut[(uint32_t)a.state[h[u].pid - a.b] & 0xffu] : 0.0f;
         }
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
+        for (int u = 0; u < kRxU; u++) {
             if (!h[u].ok || h[u].pid < a.b) continue;
             const uint64_t off = (uint64_t)(h[u].pid - a.b) * P + 4ull * ((u * kWave + lane) % kChunksPerFrame);
             if (off >= a.numel) continue;
@@ -573,7 +579,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             else store4_guarded(p, o, 0, a.numel - off);
         }
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
+        for (int u = 0; u < kRxU; u++) {
             if (!h[u].ok || (u * kWave + lane) % kChunksPerFrame != 0) continue;
             a.state[h[u].pid] = ((unsigned long long)kRxDone << 32) | h[u].exp;
             if (h[u].pid < a.nblocks) a.exps[h[u].pid] = (int8_t)h[u].exp;
@@ -1119,7 +1125,7 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     a.job = (uint8_t)job_id;
     hipStream_t st = (hipStream_t)stream;
     k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
-    const uint64_t ntiles = (num_frames * P + kTileElems - 1) / kTileElems;
+    const uint64_t ntiles = (num_frames * P + kRxTileElems - 1) / kRxTileElems;
     launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
     return launch_check();
 }

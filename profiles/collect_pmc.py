@@ -79,6 +79,8 @@ def main(tag="r01", numel=64 * 1024 * 1024, packet_numel=256):
         "hbm_bytes_per_launch": fetch_b + write_b,
         "traffic_over_algorithmic": (fetch_b + write_b) / (alg_read + alg_write),
     }
+    if os.path.isdir(os.path.join(src, "fr_kt")):
+        summary["frames"] = frames_summary(src, dst, numel, packet_numel)
     with open(os.path.join(dst, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
@@ -86,6 +88,44 @@ def main(tag="r01", numel=64 * 1024 * 1024, packet_numel=256):
                    "quantize_pack": {"numel": numel, "packet_numel": packet_numel,
                                      "hbm_bytes_per_launch": round(fetch_b + write_b)}}, f, indent=1)
     print(json.dumps(summary, indent=1))
+
+
+def frames_summary(src, dst, numel, packet_numel, batch_max=64):
+    """F3 kernels from tools/prof_frames.py: per-kernel average duration and
+    PMC bytes per launch next to the algorithmic bytes (frames = B + b frames
+    of 52 + 4P bytes).  FETCH_SIZE doubling applies to the wide payload reads."""
+    stats = rows(os.path.join(src, "fr_kt", "kt_kernel_stats.csv"))
+    with open(os.path.join(dst, "frames_kernel_stats.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(stats[0].keys()))
+        w.writeheader()
+        for r in stats:
+            if "sml::" in r["Name"]:
+                w.writerow(r)
+    B = -(-numel // packet_numel)
+    fbytes = (B + min(B, batch_max)) * (52 + 4 * packet_numel)
+    alg = {"k_quantize_frames": (4 * numel, fbytes), "k_rx_apply": (fbytes, 4 * numel),
+           "k_rx_claim": (None, None)}
+
+    def pmc(sub, counter, key):
+        rr = rows(os.path.join(src, sub, "pmc_counter_collection.csv"))
+        v = [float(r["Counter_Value"]) * 1024 for r in rr if key in r["Kernel_Name"] and r["Counter_Name"] == counter]
+        return statistics.median(v) if v else None
+
+    out = {}
+    for key, (ar, aw) in alg.items():
+        st = [r for r in stats if key in r["Name"]]
+        if not st:
+            continue
+        avg_ns = float(st[0]["AverageNs"])
+        fetch, write = pmc("fr_fetch", "FETCH_SIZE", key), pmc("fr_write", "WRITE_SIZE", key)
+        e = {"avg_duration_ns": avg_ns, "launches": int(st[0]["Calls"]),
+             "hbm_read_bytes_per_launch (2 x FETCH_SIZE x 1024)": None if fetch is None else 2 * fetch,
+             "hbm_write_bytes_per_launch (WRITE_SIZE x 1024)": write}
+        if ar is not None:
+            e["algorithmic_bytes_per_launch"] = ar + aw
+            e["algorithmic_GBps_at_avg"] = (ar + aw) / avg_ns
+        out[key] = e
+    return out
 
 
 if __name__ == "__main__":

@@ -15,4 +15,9 @@ ARGS="$ROOT/bench.py --steps 20 --warmup 5 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 $ARGS > "$OUT/kt.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_write.log" 2>&1
+# F3 frames kernels (tx quantize-into-frames, rx claim/apply) on the same bucket
+FR="$ROOT/tools/prof_frames.py"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/fr_kt" -o kt --output-format csv -- python3 $FR > "$OUT/fr_kt.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fr_fetch" -o pmc --output-format csv -- python3 $FR > "$OUT/fr_fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/fr_write" -o pmc --output-format csv -- python3 $FR > "$OUT/fr_write.log" 2>&1
 echo "profiles done: $OUT"
