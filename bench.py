@@ -37,11 +37,16 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-leve
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=500)
+    ap.add_argument("--settle-ms", type=float, default=50.0,
+                    help="untimed launches of the same step for this long before the warmup steps "
+                         "(HBM/fabric clocks ramp under load: profiles/r01/bench_warmup_sweep.jsonl)")
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024, help="fp32 elements per GPU (256 MiB)")
     ap.add_argument("--packet-numel", type=int, default=256)
     ap.add_argument("--grid-limit", type=int, default=0, help="workgroups per launch (0 = one per 4 tiles)")
+    ap.add_argument("--xcd-chunk", type=int, default=64,
+                    help="workgroups per contiguous run on one XCD (0 = plain blockIdx order)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--extra", action="store_true", help="also time dequantize / fused round trip / copy")
@@ -138,6 +143,7 @@ def main():
     sw.lib()
     if args.grid_limit:
         sw.set_grid_limit(args.grid_limit)
+    sw.set_xcd_chunk(args.xcd_chunk)
 
     N, P = args.numel, args.packet_numel
     B = sw.num_blocks(N, P)
@@ -166,6 +172,15 @@ def main():
         step, per_call = graph.replay, args.graph_steps
         assert args.steps % per_call == 0 and args.warmup % per_call == 0, "steps/warmup must be multiples of --graph-steps"
 
+    # Clock settle: the first ~20-40 ms of streaming after idle run ~4 % slower
+    # (warmup 10 -> 78-79 us per launch, >= 500 -> 76 us); run the same step
+    # untimed for settle_ms first so the K timed steps see steady-state clocks
+    # whatever W the caller passes.
+    t_settle = time.perf_counter() + args.settle_ms * 1e-3
+    while time.perf_counter() < t_settle:
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize()
     for _ in range(args.warmup // per_call):
         step()
     torch.cuda.synchronize()
@@ -220,6 +235,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_ms": args.settle_ms,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
             "scaling": "weak",
@@ -234,6 +250,7 @@ def main():
                 "num_blocks_per_gpu": B,
                 "parallelism": f"shard{world} (FIFO slices, no data-path collective)",
                 "bytes_per_step_per_gpu": alg_bytes,
+                "xcd_chunk": args.xcd_chunk,
                 "launch": "eager" if args.graph_steps <= 1 else f"hipGraph replay, {args.graph_steps} steps per graph",
             },
             "input_GBps": round(world * 4 * N / (elapsed / args.steps) / 1e9, 2),

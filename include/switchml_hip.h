@@ -219,6 +219,11 @@ sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void
  * elements, i.e. no grid-stride).  Process-wide; returns the previous value. */
 uint32_t sml_set_grid_limit(uint32_t max_workgroups);
 
+/* Launch-order knob: the streaming kernels permute workgroups so that each
+ * of the 8 XCDs sweeps runs of `chunk` consecutive workgroups' data (default
+ * 64; 0 = plain blockIdx order).  Process-wide; returns the previous value. */
+uint32_t sml_set_xcd_chunk(uint32_t chunk);
+
 /* Experiment knob: tiles (1024 elements) per wave per loop iteration of the
  * quantize kernel, 1 (default) or 2.  Returns the previous value. */
 uint32_t sml_set_tiles_per_wave(uint32_t tiles);

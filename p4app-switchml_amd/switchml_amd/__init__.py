@@ -112,6 +112,8 @@ def lib():
     L.sml_quantize_pack_frames.argtypes = [vp, u64, u32, u16, vp, u32, ctypes.POINTER(FrameParams), vp, u64, vp]
     L.sml_set_tiles_per_wave.restype = u32
     L.sml_set_tiles_per_wave.argtypes = [u32]
+    L.sml_set_xcd_chunk.restype = u32
+    L.sml_set_xcd_chunk.argtypes = [u32]
     L.sml_dequantize_frames.restype = i32
     L.sml_dequantize_frames.argtypes = [vp, u64, u64, u64, u32, u16, u32, u64, vp, vp, vp, vp, vp]
     _lib = L
@@ -140,6 +142,11 @@ def set_grid_limit(max_workgroups: int) -> int:
 
 def set_tiles_per_wave(tiles: int) -> int:
     return int(lib().sml_set_tiles_per_wave(tiles))
+
+
+def set_xcd_chunk(chunk: int) -> int:
+    """Workgroups per contiguous run on one XCD (0 = plain order); returns the previous value."""
+    return int(lib().sml_set_xcd_chunk(chunk))
 
 
 # ------------------------------------------------------------- torch glue --

@@ -11,8 +11,13 @@ ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="$ROOT/bench.py --steps 20 --warmup 5 --no-cpu-baseline"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 $ARGS > "$OUT/kt.log" 2>&1
+# kernel-trace pass: the bench's own defaults (50 ms settle, 500 warmup steps)
+# and 2000 timed steps, so the average is dominated by steady-state launches;
+# collect_pmc.py also reports the average over the timed window alone.
+KT_ARGS="$ROOT/bench.py --steps 2000 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 $KT_ARGS > "$OUT/kt.log" 2>&1
+# PMC passes: bytes per launch do not depend on clocks; few launches suffice
+ARGS="$ROOT/bench.py --steps 20 --warmup 5 --settle-ms 0 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_write.log" 2>&1
 # F3 frames kernels (tx quantize-into-frames, rx claim/apply) on the same bucket

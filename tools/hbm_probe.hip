@@ -1,0 +1,159 @@
+// hbm_probe.hip — standalone HBM ceiling probe for the K1 access shape on
+// gfx950 (tools only; not part of the product library).
+//
+// Question it answers: is K1's 6.8 TB/s (read 4N fp32 + write 4N int32) the
+// ceiling for a 1:1 read:write stream on MI355X, or does another shape
+// (workgroup size, f4 per lane, cache policy, XCD-contiguous block order,
+// read-only / write-only) move more bytes?  Every variant is timed in every
+// round (interleaved), medians reported as JSON on stdout.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -o bin/hbm_probe tools/hbm_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <functional>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+
+// LOADNT / STORENT: 0 default policy, 1 nontemporal.
+// XCD: remap blockIdx so that each XCD (blockIdx % 8 under round-robin
+// dispatch) sweeps contiguous runs of XCD blocks (-1: one contiguous eighth
+// of the buffer per XCD; 0: no remap).
+template <int WG, int U, int LOADNT, int STORENT, int XCD>
+__global__ __launch_bounds__(WG) void k_copy(const u4* __restrict__ in, u4* __restrict__ out, unsigned long long nvec) {
+    unsigned long long b = blockIdx.x;
+    if (XCD < 0) {
+        const unsigned long long nb = gridDim.x, per = nb / 8;
+        b = (b % 8) * per + b / 8;   // nb is a multiple of 8
+    } else if (XCD > 0) {
+        const unsigned long long r = b / 8;   // this XCD's r-th block
+        b = (r / XCD) * 8 * XCD + (b % 8) * XCD + r % XCD;
+    }
+    const unsigned long long base = b * (unsigned long long)(WG * U) + (threadIdx.x / 64) * (64ull * U) + (threadIdx.x % 64);
+    u4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const u4* p = in + base + 64ull * u;
+        v[u] = LOADNT ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        v[u].x ^= 0x80000000u;       // touch the data (like a quantizer would)
+        u4* p = out + base + 64ull * u;
+        if (STORENT) __builtin_nontemporal_store(v[u], p); else *p = v[u];
+    }
+    (void)nvec;
+}
+
+template <int WG, int U, int LOADNT>
+__global__ __launch_bounds__(WG) void k_read(const u4* __restrict__ in, unsigned int* __restrict__ sink) {
+    const unsigned long long base = blockIdx.x * (unsigned long long)(WG * U) + (threadIdx.x / 64) * (64ull * U) + (threadIdx.x % 64);
+    unsigned int acc = 0;
+    u4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const u4* p = in + base + 64ull * u;
+        v[u] = LOADNT ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    if (acc == 0x12345678u) sink[threadIdx.x] = acc;   // practically never: keeps the loads
+}
+
+template <int WG, int U, int STORENT>
+__global__ __launch_bounds__(WG) void k_write(u4* __restrict__ out) {
+    const unsigned long long base = blockIdx.x * (unsigned long long)(WG * U) + (threadIdx.x / 64) * (64ull * U) + (threadIdx.x % 64);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        u4 v = {(unsigned)base, (unsigned)u, 1u, 2u};
+        u4* p = out + base + 64ull * u;
+        if (STORENT) __builtin_nontemporal_store(v, p); else *p = v;
+    }
+}
+
+struct Variant {
+    std::string name;
+    double bytes_per_vec;   // bytes moved per 16-B vector of the buffer
+    std::function<void(hipStream_t)> launch;
+    std::vector<float> us;
+};
+
+int main(int argc, char** argv) {
+    const unsigned long long bytes = (argc > 1 ? strtoull(argv[1], 0, 10) : 256ull) << 20;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 7;
+    const int reps = 10;
+    const unsigned long long nvec = bytes / 16;
+    u4 *in, *out;
+    unsigned int* sink;
+    CK(hipMalloc(&in, bytes));
+    CK(hipMalloc(&out, bytes));
+    CK(hipMalloc(&sink, 4096));
+    CK(hipMemset(in, 1, bytes));
+    CK(hipMemset(out, 0, bytes));
+    hipStream_t st;
+    CK(hipStreamCreate(&st));
+
+    std::vector<Variant> vs;
+#define COPY(WG, U, LN, SN, X) vs.push_back({"copy wg" #WG " u" #U " ldnt" #LN " stnt" #SN " xcd" #X, 32.0, \
+    [=](hipStream_t s) { unsigned long long g = nvec / (WG * U); \
+        k_copy<WG, U, LN, SN, X><<<g, WG, 0, s>>>(in, out, nvec); }, {}})
+#define READ(WG, U, LN) vs.push_back({"read wg" #WG " u" #U " ldnt" #LN, 16.0, \
+    [=](hipStream_t s) { unsigned long long g = nvec / (WG * U); k_read<WG, U, LN><<<g, WG, 0, s>>>(in, sink); }, {}})
+#define WRITE(WG, U, SN) vs.push_back({"write wg" #WG " u" #U " stnt" #SN, 16.0, \
+    [=](hipStream_t s) { unsigned long long g = nvec / (WG * U); k_write<WG, U, SN><<<g, WG, 0, s>>>(out); }, {}})
+    COPY(256, 4, 1, 0, 0);   // == K1's shape and policy before the XCD order
+    COPY(256, 4, 1, 0, 64);  // == K1 now
+    COPY(256, 4, 1, 0, -1);
+    COPY(128, 4, 1, 0, 64);
+    COPY(128, 4, 1, 0, 128);
+    COPY(64, 4, 1, 0, 64);
+    COPY(64, 4, 1, 0, 256);
+    COPY(64, 2, 1, 0, 64);
+    COPY(64, 2, 1, 0, 256);
+    COPY(64, 2, 1, 0, 512);
+    COPY(64, 2, 1, 0, -1);
+    COPY(128, 2, 1, 0, 128);
+    COPY(256, 2, 1, 0, 64);
+    COPY(256, 2, 1, 0, 128);
+    COPY(512, 4, 1, 0, 32);
+    COPY(256, 8, 1, 0, 32);
+    READ(256, 4, 1);
+    WRITE(256, 4, 0);
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (auto& v : vs) { v.launch(st); }
+    CK(hipStreamSynchronize(st));
+    for (int r = 0; r < rounds; r++) {
+        for (auto& v : vs) {
+            v.launch(st);
+            CK(hipEventRecord(a, st));
+            for (int i = 0; i < reps; i++) v.launch(st);
+            CK(hipEventRecord(b, st));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            v.us.push_back(ms * 1000.f / reps);
+        }
+        fprintf(stderr, "round %d done\n", r);
+    }
+    CK(hipGetLastError());
+    printf("{\"bytes\": %llu, \"rounds\": %d, \"reps\": %d, \"variants\": [", bytes, rounds, reps);
+    for (size_t i = 0; i < vs.size(); i++) {
+        auto& v = vs[i];
+        std::sort(v.us.begin(), v.us.end());
+        const double med = v.us[v.us.size() / 2];
+        const double moved = v.bytes_per_vec * nvec;   // copy: 2x buffer, read/write: 1x
+        printf("%s{\"name\": \"%s\", \"median_us\": %.2f, \"min_us\": %.2f, \"GBps\": %.1f}", i ? ", " : "",
+               v.name.c_str(), med, v.us[0], moved / med * 1e-3);
+    }
+    printf("]}\n");
+    return 0;
+}
