@@ -406,7 +406,8 @@ __device__ __forceinline__ uint32_t pool_index(uint64_t p, const FrameArgs& a) {
 
 // Lanes 0..12 write the 52 header bytes of frame p (one dword each):
 // dwords 0-10 constant, 11 = pkt_id (host order), 12 = pool index (BE16),
-// exponent byte, zero byte.
+// exponent byte, zero byte.  (Extra-batch frames; the bulk of the headers is
+// written lane-parallel by k_quantize_frames.)
 __device__ __forceinline__ void write_frame_header(const FrameArgs& a, uint64_t p, int lane, uint32_t exp_byte) {
     if (lane > 12) return;
     uint32_t dw = a.hdr[0];
@@ -422,6 +423,24 @@ __device__ __forceinline__ void write_frame_header(const FrameArgs& a, uint64_t 
 
 // Fused quantize + pack into DPDK frames (BuildPacket + PreprocessSingle for
 // every packet of the slice, dpdk_worker_thread_utils.inc:67-135 + ppp.cc:69-156).
+//
+// Frame f carries the exponent of block f (f < B) in header dword 12 (pool
+// index BE16, exponent byte, zero byte) and the payload of block f - b.  The
+// wave of block k therefore writes:
+//  * frame k + b: header dwords 0-11 and the payload — one wave writes all
+//    of the frame but dword 12 (and dword 12 too once k + b >= B: those
+//    frames carry exponent 0);
+//  * dword 12 of frame k (k >= b), or the whole of extra-batch frame k
+//    (k < b: header with this exponent, zero payload).
+// One dword store instruction covers 4 frames: lane l < 48 writes dword
+// l % 12 of payload frame l / 12, lanes 48-51 write dword 12 of the 4
+// exponent frames.  Constant dwords are picked once per wave; the pool index
+// (PktId2PoolIndex) costs one 64-bit modulo per tile.
+__device__ __forceinline__ uint32_t pool_dword(const FrameArgs& a, uint32_t i, uint32_t exp_byte) {
+    const uint32_t pool = i < a.mop ? ((a.pool_start + i) & 0xffffu) : (((a.pool_start + (i - a.mop)) | 0x8000u) & 0xffffu);
+    return (pool >> 8) | ((pool & 0xffu) << 8) | ((exp_byte & 0xffu) << 16);
+}
+
 template <int P, bool ALIGNED, bool GLOBAL>
 __global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) {
     __shared__ float lut[256];
@@ -429,35 +448,78 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) 
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t padded = a.nblocks * P;
-    constexpr int kPk = kTileElems / P;        // packets per tile
+    constexpr int kPk = kTileElems / P;                   // packets per tile
+    constexpr int kLanesPerPk = P / 4 < kWave ? P / 4 : kWave;
+    const int hd = lane % 12;                              // header dword of lanes 0..47
+    const int hj = lane < 48 ? lane / 12 : lane - 48;      // frame (of 4) of lanes 0..51
+    uint32_t hconst = a.hdr[0];
+#pragma unroll
+    for (int i = 1; i < 11; i++) hconst = hd == i ? a.hdr[i] : hconst;
+    const uint32_t m2 = 2u * a.mop;
     for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
         const uint64_t base = t * kTileElems;
-        QuantArgs qa;                           // reuse the K1 tile loader
+        const uint64_t pk0 = base / P;                     // first block of the tile
+        QuantArgs qa;                                      // reuse the K1 tile loader
         qa.in = a.in;
         qa.numel = a.numel;
         f4 v[kU];
         load_tile<ALIGNED>(qa, base, lane, v);
         int eloc[kU];
         tile_exponents<P>(v, eloc);
-        // headers (and the zero payload of extra-batch frames) of this tile's packets
+        // exponent of packet j of the tile: slice j*P/256, lane (j*P/4) % 64
+        uint32_t ej[kPk];
 #pragma unroll
         for (int j = 0; j < kPk; j++) {
-            const uint64_t pk = base / P + j;
-            if (pk >= a.nblocks) break;
-            // the exponent of packet pk: slice u = j*P/256, lane (j*P/4) % 64
-            constexpr int kLanesPerPk = P / 4 < kWave ? P / 4 : kWave;
             const int u = (j * P) / 256;
-            uint32_t e = 0;
+            ej[j] = 0;
 #pragma unroll
             for (int uu = 0; uu < kU; uu++)
-                if (uu == u) e = (uint32_t)__builtin_amdgcn_readlane(eloc[uu], (j * kLanesPerPk) % kWave);
-            write_frame_header(a, pk, lane, e);
-            if (pk + a.b >= a.nblocks) write_frame_header(a, pk + a.b, lane, 0u);
-            if (pk < a.b) {
-                uint32_t* pl = reinterpret_cast<uint32_t*>(a.frames + pk * a.stride + 52);
-                for (int i = lane; i < P / 4; i += kWave) *reinterpret_cast<u4a*>(pl + 4 * i) = u4a{0u, 0u, 0u, 0u};
+                if (uu == u) ej[j] = (uint32_t)__builtin_amdgcn_readlane(eloc[uu], (j * kLanesPerPk) % kWave);
+        }
+        const uint32_t r = (uint32_t)((pk0 + a.pool_shift) % m2);   // pool slot of frame pk0
+        const bool extra = pk0 < a.b;                               // wave-uniform, first b / kPk tiles
+#pragma unroll
+        for (int j0 = 0; j0 < kPk; j0 += 4) {
+            const int j = j0 + hj;
+            if (lane < 48) {
+                if (j < kPk && pk0 + j < a.nblocks) {
+                    const uint64_t f = pk0 + j + a.b;
+                    *reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 4 * hd) = hd == 11 ? (uint32_t)f : hconst;
+                }
+            } else if (lane < 52 && !extra) {
+                if (j < kPk && pk0 + j < a.nblocks) {
+                    uint32_t e = 0;
+#pragma unroll
+                    for (int jj = 0; jj < kPk; jj++) e = j == jj ? ej[jj] : e;
+                    *reinterpret_cast<uint32_t*>(a.frames + (pk0 + j) * a.stride + 48) = pool_dword(a, (r + (uint32_t)j) % m2, e);
+                }
             }
         }
+        if (__builtin_expect(pk0 + kPk + a.b > a.nblocks, 0)) {
+            // tail: payload frames at or past B carry exponent 0; their dword 12 is ours
+            if (lane < kPk && pk0 + lane < a.nblocks && pk0 + lane + a.b >= a.nblocks) {
+                const uint64_t f = pk0 + lane + a.b;
+                *reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 48) =
+                    pool_dword(a, (uint32_t)((f + a.pool_shift) % m2), 0u);
+            }
+        }
+        if (__builtin_expect(extra, 0)) {
+            // extra-batch frames: header with this tile's exponent, zero payload; all ours
+#pragma unroll
+            for (int j = 0; j < kPk; j++) {
+                const uint64_t pk = pk0 + j;
+                if (pk >= a.nblocks) break;
+                if (pk < a.b) {
+                    write_frame_header(a, pk, lane, ej[j]);
+                    uint32_t* pl = reinterpret_cast<uint32_t*>(a.frames + pk * a.stride + 52);
+                    for (int i = lane; i < P / 4; i += kWave) *reinterpret_cast<u4a*>(pl + 4 * i) = u4a{0u, 0u, 0u, 0u};
+                } else if (lane == 0) {
+                    *reinterpret_cast<uint32_t*>(a.frames + pk * a.stride + 48) =
+                        pool_dword(a, (uint32_t)((pk + a.pool_shift) % m2), ej[j]);
+                }
+            }
+        }
+        // payloads
 #pragma unroll
         for (int u = 0; u < kU; u++) {
             const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;

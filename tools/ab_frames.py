@@ -29,7 +29,8 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=7, reps=10):
         cur = frames.clone()
         if ref is None:
             ref = cur
-        assert torch.equal(ref, cur), p
+        if not os.environ.get("AB_NOCHECK"):
+            assert torch.equal(ref, cur), p
     res = {p: [] for p in paths}
     for _ in range(rounds):
         for p, L in zip(paths, libs):

@@ -52,6 +52,25 @@ __global__ __launch_bounds__(WG) void k_copy(const u4* __restrict__ in, u4* __re
     (void)nvec;
 }
 
+// Copy with the destination shifted by OFF bytes (unaligned 16-B stores, as
+// at the 52-byte payload offset of a DPDK frame).
+typedef unsigned int u4a __attribute__((ext_vector_type(4), aligned(4)));
+template <int OFF>
+__global__ __launch_bounds__(256) void k_copy_off(const u4* __restrict__ in, unsigned char* __restrict__ out) {
+    const unsigned long long r = blockIdx.x / 8, C = 64, span = 8 * C;
+    unsigned long long b = blockIdx.x;
+    if (b < gridDim.x / span * span) b = (r / C) * span + (b % 8) * C + r % C;
+    const unsigned long long base = b * 1024ull + (threadIdx.x / 64) * 256ull + (threadIdx.x % 64);
+    u4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = __builtin_nontemporal_load(in + base + 64ull * u);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        u4a w = {v[u].x ^ 1u, v[u].y, v[u].z, v[u].w};
+        *reinterpret_cast<u4a*>(out + OFF + 16ull * (base + 64ull * u)) = w;
+    }
+}
+
 template <int WG, int U, int LOADNT>
 __global__ __launch_bounds__(WG) void k_read(const u4* __restrict__ in, unsigned int* __restrict__ sink) {
     const unsigned long long base = blockIdx.x * (unsigned long long)(WG * U) + (threadIdx.x / 64) * (64ull * U) + (threadIdx.x % 64);
@@ -94,6 +113,8 @@ int main(int argc, char** argv) {
     unsigned int* sink;
     CK(hipMalloc(&in, bytes));
     CK(hipMalloc(&out, bytes));
+    u4* out2;
+    CK(hipMalloc(&out2, bytes + 4096));
     CK(hipMalloc(&sink, 4096));
     CK(hipMemset(in, 1, bytes));
     CK(hipMemset(out, 0, bytes));
@@ -108,24 +129,14 @@ int main(int argc, char** argv) {
     [=](hipStream_t s) { unsigned long long g = nvec / (WG * U); k_read<WG, U, LN><<<g, WG, 0, s>>>(in, sink); }, {}})
 #define WRITE(WG, U, SN) vs.push_back({"write wg" #WG " u" #U " stnt" #SN, 16.0, \
     [=](hipStream_t s) { unsigned long long g = nvec / (WG * U); k_write<WG, U, SN><<<g, WG, 0, s>>>(out); }, {}})
-    COPY(256, 4, 1, 0, 0);   // == K1's shape and policy before the XCD order
     COPY(256, 4, 1, 0, 64);  // == K1 now
-    COPY(256, 4, 1, 0, -1);
-    COPY(128, 4, 1, 0, 64);
-    COPY(128, 4, 1, 0, 128);
-    COPY(64, 4, 1, 0, 64);
-    COPY(64, 4, 1, 0, 256);
-    COPY(64, 2, 1, 0, 64);
-    COPY(64, 2, 1, 0, 256);
-    COPY(64, 2, 1, 0, 512);
-    COPY(64, 2, 1, 0, -1);
-    COPY(128, 2, 1, 0, 128);
-    COPY(256, 2, 1, 0, 64);
-    COPY(256, 2, 1, 0, 128);
-    COPY(512, 4, 1, 0, 32);
-    COPY(256, 8, 1, 0, 32);
-    READ(256, 4, 1);
-    WRITE(256, 4, 0);
+#define COPYOFF(O) vs.push_back({"copy dst+" #O " bytes (unaligned x4 stores)", 32.0, \
+    [=](hipStream_t s) { k_copy_off<O><<<nvec / 1024, 256, 0, s>>>(in, reinterpret_cast<unsigned char*>(out2)); }, {}})
+    COPYOFF(0);
+    COPYOFF(4);
+    COPYOFF(8);
+    COPYOFF(12);
+    COPYOFF(16);
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
