@@ -71,6 +71,27 @@ __global__ __launch_bounds__(256) void k_copy_off(const u4* __restrict__ in, uns
     }
 }
 
+// Copy with the SOURCE shifted by OFF bytes (unaligned 16-B loads, as when
+// reading payloads at the 52-byte offset of returned frames).
+template <int OFF, int NT>
+__global__ __launch_bounds__(256) void k_copy_srcoff(const unsigned char* __restrict__ in, u4* __restrict__ out) {
+    const unsigned long long r = blockIdx.x / 8, C = 64, span = 8 * C;
+    unsigned long long b = blockIdx.x;
+    if (b < gridDim.x / span * span) b = (r / C) * span + (b % 8) * C + r % C;
+    const unsigned long long base = b * 1024ull + (threadIdx.x / 64) * 256ull + (threadIdx.x % 64);
+    u4a v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const u4a* p = reinterpret_cast<const u4a*>(in + OFF + 16ull * (base + 64ull * u));
+        v[u] = NT ? __builtin_nontemporal_load(p) : *p;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        u4 w = {v[u].x ^ 1u, v[u].y, v[u].z, v[u].w};
+        out[base + 64ull * u] = w;
+    }
+}
+
 template <int WG, int U, int LOADNT>
 __global__ __launch_bounds__(WG) void k_read(const u4* __restrict__ in, unsigned int* __restrict__ sink) {
     const unsigned long long base = blockIdx.x * (unsigned long long)(WG * U) + (threadIdx.x / 64) * (64ull * U) + (threadIdx.x % 64);
@@ -137,6 +158,13 @@ int main(int argc, char** argv) {
     COPYOFF(8);
     COPYOFF(12);
     COPYOFF(16);
+#define COPYSRC(O, NT) vs.push_back({"copy src+" #O " bytes nt" #NT " (unaligned x4 loads)", 32.0, \
+    [=](hipStream_t s) { k_copy_srcoff<O, NT><<<nvec / 1024, 256, 0, s>>>(reinterpret_cast<const unsigned char*>(out2), out); }, {}})
+    COPYSRC(0, 1);
+    COPYSRC(4, 1);
+    COPYSRC(8, 1);
+    COPYSRC(0, 0);
+    COPYSRC(4, 0);
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
