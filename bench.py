@@ -321,6 +321,17 @@ def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
     res["roundtrip_fused_GBps"] = round(8 * N / t / 1e9, 1)
     t = timeit(lambda: out.copy_(x))
     res["torch_copy_GBps"] = round(8 * N / t / 1e9, 1)
+    # a FIFO slice that starts 4 bytes past a 16-B boundary (unaligned path)
+    xm = x[1:]
+    pm = torch.empty(sw.num_blocks(N - 1, P) * P, dtype=torch.int32, device=x.device)
+    em = torch.empty(sw.num_blocks(N - 1, P), dtype=torch.int8, device=x.device)
+    t = timeit(lambda: sw.quantize_pack(xm, P, 1, payload=pm, exps_out=em, stream=stream))
+    res["quantize_pack_unaligned_slice_GBps"] = round((8 * (N - 1) + em.numel()) / t / 1e9, 1)
+    del xm, pm, em
+    t = timeit(lambda: sw.loopback_aggregate(payload, 2, stream=stream))
+    res["loopback_x2_GBps"] = round(8 * N / t / 1e9, 1)
+    t = timeit(lambda: sw.bswap_i32(payload, out=payload, stream=stream))
+    res["bswap_int32_GBps"] = round(8 * N / t / 1e9, 1)
     res.update(host_inclusive(sw, torch, x, N, P))
     # DPDK frames (F3): fused quantize straight into Eth/IP/UDP/SwitchML frames
     fp = sw.frame_params(max_outstanding_pkts=64)

@@ -44,6 +44,7 @@ typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 // 16-byte vector with 4-byte alignment: gfx950 runs in unaligned-access mode,
 // so this is still one global_store_dwordx4 (used at the 52-byte frame offset).
 typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f4a __attribute__((ext_vector_type(4), aligned(4)));
 
 __device__ __forceinline__ f4 mkf4(float a, float b, float c, float d) { return f4{a, b, c, d}; }
 __device__ __forceinline__ u4 mku4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return u4{a, b, c, d}; }
@@ -127,12 +128,18 @@ __device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32
 
 // ------------------------------------------------------------- memory ops
 
+// ALIGNED = false: slices that start at any 4-byte offset (FIFO slices,
+// fifo_scheduler.cc:93-109).  gfx950 runs in unaligned mode and moves 4-byte
+// aligned 16-B accesses at the full stream rate (hbm_probe: +4 B offset
+// loads 7.15 TB/s, stores 7.20 TB/s vs 7.23 aligned), so both forms are one
+// dwordx4 per lane.
 template <bool ALIGNED>
 __device__ __forceinline__ f4 load4(const float* p) {
     if constexpr (ALIGNED) {
         return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
     } else {
-        return mkf4(p[0], p[1], p[2], p[3]);
+        const f4a v = __builtin_nontemporal_load(reinterpret_cast<const f4a*>(p));
+        return mkf4(v.x, v.y, v.z, v.w);
     }
 }
 
@@ -150,7 +157,7 @@ __device__ __forceinline__ void store4(float* p, f4 v) {
     if constexpr (ALIGNED) {
         *reinterpret_cast<f4*>(p) = v;   // default policy: faster than nt stores here
     } else {
-        p[0] = v.x; p[1] = v.y; p[2] = v.z; p[3] = v.w;
+        *reinterpret_cast<f4a*>(p) = f4a{v.x, v.y, v.z, v.w};
     }
 }
 
@@ -790,32 +797,49 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
     }
 }
 
-// K5: DummyBackend::ProcessPacket over the payload plane (in place).
-template <bool BE>
-__global__ __launch_bounds__(kBlockThreads) void k_loopback(u4* p, uint64_t nvec, uint32_t W) {
-    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; i < nvec; i += stride) {
-        u4 v = __builtin_nontemporal_load(p + i);
-        uint32_t q[4] = {(uint32_t)v.x, (uint32_t)v.y, (uint32_t)v.z, (uint32_t)v.w};
+// Word streams in the quantizer's tile shape (1024 words per wave, 16-B
+// non-temporal loads, default-policy stores, XCD order, one-shot grid; any
+// 4-byte alignment; in may alias out):
+//  * K5 DummyBackend::ProcessPacket over the payload plane: per word bswap,
+//    int32 wrap multiply by W, bswap (dummy_backend.cc:72-84); LE words skip
+//    the swaps;
+//  * INT32 path: byteswap (ppp.cc:158-190, 262-298).
+struct LoopbackOp {
+    uint32_t W;
+    bool be;
+    __device__ __forceinline__ uint32_t operator()(uint32_t q) const { return be ? bswap(bswap(q) * W) : q * W; }
+};
+struct BswapOp {
+    __device__ __forceinline__ uint32_t operator()(uint32_t q) const { return bswap(q); }
+};
+
+template <class Op>
+__global__ __launch_bounds__(kBlockThreads) void k_words(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t xcd,
+                                                         Op op) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t ntiles = (n + kTileElems - 1) / kTileElems;
+    for (uint64_t t = xcd_block(xcd) * kWavesPerBlock + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+        const uint64_t base = t * kTileElems;
+        if (base + kTileElems <= n) {
+            u4a v[kU];
 #pragma unroll
-        for (int j = 0; j < 4; j++) q[j] = BE ? bswap(bswap(q[j]) * W) : q[j] * W;
-        p[i] = mku4(q[0], q[1], q[2], q[3]);
+            for (int u = 0; u < kU; u++)
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(in + base + (u * kWave + lane) * 4));
+#pragma unroll
+            for (int u = 0; u < kU; u++)
+                *reinterpret_cast<u4a*>(out + base + (u * kWave + lane) * 4) =
+                    u4a{op(v[u].x), op(v[u].y), op(v[u].z), op(v[u].w)};
+        } else {
+#pragma unroll
+            for (int u = 0; u < kU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4 + j;
+                    if (idx < n) out[idx] = op(in[idx]);
+                }
+        }
     }
-}
-
-// INT32 path: byteswap (in may alias out).  Vector form when both are 16-B aligned.
-__global__ __launch_bounds__(kBlockThreads) void k_bswap_vec(const u4* in, u4* out, uint64_t nvec) {
-    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; i < nvec; i += stride) {
-        u4 v = in[i];
-        out[i] = mku4(bswap(v.x), bswap(v.y), bswap(v.z), bswap(v.w));
-    }
-}
-
-__global__ __launch_bounds__(kBlockThreads) void k_bswap_scalar(const int32_t* in, int32_t* out, uint64_t n) {
-    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; i < n; i += stride)
-        out[i] = (int32_t)bswap((uint32_t)in[i]);
 }
 
 // Measurement probe (not on the hot path): the same 1024-element tiles and
@@ -1240,17 +1264,10 @@ sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void
 sml_status_t sml_bswap_i32(const int32_t* d_in, int32_t* d_out, uint64_t numel, void* stream) {
     if (numel == 0) return SML_OK;
     if (!d_in || !d_out || !aligned4(d_in) || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
-    hipStream_t st = (hipStream_t)stream;
-    if (aligned16(d_in) && aligned16(d_out)) {
-        uint64_t nvec = numel / 4;
-        if (nvec) k_bswap_vec<<<grid_for_vec(nvec), kBlockThreads, 0, st>>>(
-            reinterpret_cast<const u4*>(d_in), reinterpret_cast<u4*>(d_out), nvec);
-        uint64_t done = nvec * 4;
-        if (done < numel)
-            k_bswap_scalar<<<1, kBlockThreads, 0, st>>>(d_in + done, d_out + done, numel - done);
-    } else {
-        k_bswap_scalar<<<grid_for_vec((numel + 3) / 4), kBlockThreads, 0, st>>>(d_in, d_out, numel);
-    }
+    const uint64_t ntiles = (numel + kTileElems - 1) / kTileElems;
+    k_words<<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(
+        reinterpret_cast<const uint32_t*>(d_in), reinterpret_cast<uint32_t*>(d_out), numel,
+        g_xcd_chunk.load(std::memory_order_relaxed), BswapOp{});
     return launch_check();
 }
 
@@ -1260,12 +1277,11 @@ sml_status_t sml_loopback_aggregate(int32_t* d_payload, uint64_t count, uint16_t
     if (count == 0) return SML_OK;
     if (!d_payload) return SML_ERR_INVALID_ARG;
     if (!aligned16(d_payload) || (count & 3u)) return SML_ERR_ALIGNMENT;
-    hipStream_t st = (hipStream_t)stream;
-    uint64_t nvec = count / 4;
-    if (flags & SML_FLAG_PAYLOAD_LE)
-        k_loopback<false><<<grid_for_vec(nvec), kBlockThreads, 0, st>>>(reinterpret_cast<u4*>(d_payload), nvec, num_workers);
-    else
-        k_loopback<true><<<grid_for_vec(nvec), kBlockThreads, 0, st>>>(reinterpret_cast<u4*>(d_payload), nvec, num_workers);
+    const uint64_t ntiles = (count + kTileElems - 1) / kTileElems;
+    uint32_t* p = reinterpret_cast<uint32_t*>(d_payload);
+    k_words<<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(
+        p, p, count, g_xcd_chunk.load(std::memory_order_relaxed),
+        LoopbackOp{num_workers, !(flags & SML_FLAG_PAYLOAD_LE)});
     return launch_check();
 }
 

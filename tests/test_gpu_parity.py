@@ -213,9 +213,10 @@ def test_dequantize_arbitrary_words(cuda, P):
 
 
 @pytest.mark.parametrize("W", [1, 2, 3, 8, 65535])
-def test_loopback_aggregate(cuda, W):
+@pytest.mark.parametrize("count", [4096 * 4, 4100, 100_004])
+def test_loopback_aggregate(cuda, W, count):
     rng = np.random.default_rng(W)
-    words = rng.integers(0, 2 ** 32, 4096 * 4, dtype=np.uint64).astype(np.uint32)
+    words = rng.integers(0, 2 ** 32, count, dtype=np.uint64).astype(np.uint32)
     d = to_dev(words.view(np.int32), cuda)
     sw().loopback_aggregate(d, W)
     assert bits_equal(host(d), O.loopback_aggregate(words, W))
@@ -232,6 +233,10 @@ def test_bswap_int32(cuda, n, offset):
     d = to_dev(words, cuda)
     out = sw().bswap_i32(d[offset:offset + n])
     assert bits_equal(host(out), O.bswap32(words[offset:offset + n]))
+    # in place (the reference swaps the packet buffer in place, ppp.cc:158-190)
+    v = d[offset:offset + n]
+    sw().bswap_i32(v, out=v)
+    assert bits_equal(host(v), O.bswap32(words[offset:offset + n]))
 
 
 # -------------------------------------------------------- round trips ----
