@@ -97,3 +97,35 @@ def test_allreduce_benchmark_cfg1(cuda, device):
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Data verified successfully." in r.stdout
     assert "Median" in r.stdout and "Gbps" in r.stdout
+
+
+def test_dnn_benchmark_example_model_device(C):
+    """dnn_benchmark's flow on its example model (models/example.csv, via
+    tests/golden/dnn_example_model.json): one device buffer, each layer a
+    slice of it (ragged numels: most slices start 4-12 bytes off a 16-B
+    boundary), AllReduceAsync of every layer in place in backward order
+    (dnn_benchmark/main.cc:312-318), all jobs in flight, then WaitForAllJobs;
+    bit-exact against the oracle's per-layer packet loop (T = 4 FIFO slices)."""
+    import json
+    import torch
+    with open(os.path.join(ROOT, "tests", "golden", "dnn_example_model.json")) as f:
+        layers = [l[1] for l in json.load(f)["layers"]]
+    T, W, P, iters = 4, 2, 256, 2
+    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, max_outstanding_packets=256,
+                          mode="bulk", bandwidth=0))
+    x = O.ref_pattern_floats(sum(layers))
+    offs = np.concatenate([[0], np.cumsum(layers)]).astype(np.int64)
+    xd = torch.from_numpy(x).cuda()
+    ref = x.copy()
+    for _ in range(iters):
+        jobs = []
+        for li in reversed(range(len(layers))):
+            v = xd[offs[li]:offs[li + 1]]
+            jobs.append(C.allreduce_async(v))
+            r = ref[offs[li]:offs[li + 1]]
+            O.dummy_allreduce(r, P=P, max_outstanding_packets=256, num_worker_threads=T, num_workers=W,
+                              threaded=True, out=r)
+        C.wait_for_all_jobs()
+        del jobs
+    torch.cuda.synchronize()
+    assert bits_equal(xd.cpu().numpy(), ref)

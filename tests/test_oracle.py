@@ -1,9 +1,11 @@
 """CPU tests: pin the oracle before trusting it.
 
 1. The reference's own known-answer checks (the only ones it has):
-   examples/hello_world/main.cc:58-74 and
-   benchmarks/allreduce_benchmark/main.cc:331-399 (1 %, signed), run through
-   the oracle's restatement of the dummy-backend packet loop.
+   examples/hello_world/main.cc:58-74,
+   benchmarks/allreduce_benchmark/main.cc:331-399 and
+   benchmarks/dnn_benchmark/main.cc:334-358 on its models/example.csv
+   (1 %, signed), run through the oracle's restatement of the dummy-backend
+   packet loop.
 2. The hand-derived known-answer vectors in tests/golden/kat_vectors.json
    (tests/golden/make_kat.py: exact rational arithmetic from a reading of ppp.cc).
 3. The C restatement against the independent numpy restatement.
@@ -101,6 +103,34 @@ def test_allreduce_benchmark_verify_random_not_inplace():
     assert resolved.sum() > n // 20
     assert not np.any(err[resolved] > 1)
     assert np.any(err[~resolved] > 1)  # the flushed small elements
+
+
+def dnn_example_layers():
+    with open(os.path.join(os.path.dirname(GOLDEN), "dnn_example_model.json")) as f:
+        return [l[1] for l in json.load(f)["layers"]]
+
+
+def test_dnn_benchmark_verify_example_model():
+    """dnn_benchmark/main.cc:253-270, 284-318, 334-358 on the reference's own
+    example model (models/example.csv, tests/golden/dnn_example_model.json):
+    one buffer of float(i)*sign, each layer a slice of it (ragged numels, so
+    most layers start off a 16-B boundary), every iteration all-reduces the
+    layers in place in backward order; expected = ctrl * W^(iters + warmup),
+    signed error <= 1 %.  general.cfg geometry: T = 4, 256 outstanding."""
+    layers = dnn_example_layers()
+    W, iters = 2, 2
+    x = O.ref_pattern_floats(sum(layers))
+    ctrl = x.copy()
+    offs = np.concatenate([[0], np.cumsum(layers)])
+    for _ in range(iters):
+        for li in reversed(range(len(layers))):
+            v = x[offs[li]:offs[li + 1]]
+            O.dummy_allreduce(v, P=256, max_outstanding_packets=256, num_worker_threads=4, num_workers=W,
+                              threaded=True, out=v)
+    expected = ctrl * np.float32(W ** iters)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        err = (expected - x) / expected * 100
+    assert not np.any(err > 1)
 
 
 # ------------------------------------------------- hand-derived vectors --
