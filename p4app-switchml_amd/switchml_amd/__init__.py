@@ -136,6 +136,32 @@ def num_blocks(numel: int, packet_numel: int = 256) -> int:
     return int(lib().sml_num_blocks(numel, packet_numel))
 
 
+def fifo_slice(numel: int, num_slices: int, t: int) -> tuple[int, int]:
+    """(offset, numel) of slice t of a job split num_slices ways — the FIFO
+    scheduler's rule (client_lib/src/schedulers/fifo_scheduler.cc:93-109):
+    the first numel % num_slices slices get one extra element.  Used for the
+    multi-GPU sharding mode (slice g -> GPU g, as worker thread g would get it)."""
+    if num_slices <= 0 or not 0 <= t < num_slices:
+        raise ValueError("need 0 <= t < num_slices")
+    n = numel // num_slices
+    rem = numel % num_slices
+    if t < rem:
+        n += 1
+        return t * n, n
+    return t * n + rem, n
+
+
+def shard_quantize_pack(job, rank: int, world: int, packet_numel: int = 256, num_workers: int = 1,
+                        flags: int = 0, stream=None):
+    """Sharding mode: K1 over this rank's FIFO slice of `job` (a 1-D fp32
+    device tensor holding the whole job).  Returns (offset, payload, exps);
+    blocks restart at the slice start, exactly as for worker thread `rank`
+    of `world` (ppp.cc:54-62 per slice)."""
+    off, n = fifo_slice(job.numel(), world, rank)
+    payload, exps = quantize_pack(job[off:off + n], packet_numel, num_workers, flags=flags, stream=stream)
+    return off, payload, exps
+
+
 def set_grid_limit(max_workgroups: int) -> int:
     return int(lib().sml_set_grid_limit(max_workgroups))
 

@@ -122,3 +122,62 @@ def test_switchsim_allreduce_two_workers_one_gpu(cuda, P):
         p.join(timeout=60)
     for rank, ok, err in res:
         assert ok, (rank, err)
+
+
+# ---------------------------------------------------- sharding mode (e) --
+
+@pytest.mark.parametrize("numel,T", [(0, 2), (1, 2), (1023, 2), (100_003, 3), (67_108_864, 8), (268_435_457, 8)])
+def test_fifo_slice_matches_oracle(numel, T):
+    """switchml_amd.fifo_slice (the multi-GPU shard rule) == the oracle's
+    restatement of fifo_scheduler.cc:93-109."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
+    import switchml_amd as sw
+    for t in range(T):
+        assert sw.fifo_slice(numel, T, t) == O.slice_geometry(numel, T, t)
+
+
+def _gpu_shard(rank, world, port, n, P, q):
+    try:
+        dist = _init(rank, world, port)
+        import switchml_amd as sw
+        x = O.splitmix_normal(77, n)                     # the same job on every rank
+        job = torch.from_numpy(x).to("cuda:0")
+        off, payload, exps = sw.shard_quantize_pack(job, rank, world, P)
+        torch.cuda.synchronize()
+        # gather every rank's planes (gloo, CPU tensors) to check them together
+        got = [None] * world
+        dist.all_gather_object(got, (off, payload.cpu().numpy(), exps.cpu().numpy()))
+        ok = True
+        for t, (o, pl, ex) in enumerate(got):
+            ro, rn = O.slice_geometry(n, world, t)
+            sl = x[ro:ro + rn]
+            ok &= o == ro
+            ok &= np.array_equal(pl.view(np.uint32), O.quantize(sl, P))
+            ok &= np.array_equal(ex, O.exponents(sl, P))
+        q.put((rank, bool(ok), ""))
+        dist.destroy_process_group()
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, False, repr(ex)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharding_mode_ranks_one_gpu(cuda, world):
+    """Sharding mode (SURVEY E1): rank g quantizes FIFO slice g of one job;
+    together the ranks produce, bit for bit, the planes of the reference run
+    with num_worker_threads = world (blocks restart at every slice start).
+    Ranks share one MI355X here (gloo); the driver's multi-GPU bench runs the
+    same per-rank work on one GPU per rank."""
+    n, P = 100_003, 256
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_shard, args=(r, world, port, n, P, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, err in res:
+        assert ok, (rank, err)
