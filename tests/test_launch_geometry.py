@@ -1,0 +1,93 @@
+"""GPU: the streaming kernels give the same bytes under every launch geometry.
+
+The workgroup -> data mapping is a permutation (XCD-aware order,
+`sml_set_xcd_chunk`) and the grid may be capped
+(`sml_set_grid_limit`, grid-stride loops), so a bug in either would move or
+drop tiles.  Every kernel of the path runs under several (grid cap, XCD chunk)
+pairs — grid sizes that are and are not multiples of 8 x chunk, so the
+permuted head and the identity tail both occur — and must reproduce the
+oracle (or, for kernels without a direct oracle call, the default geometry's
+output) bit for bit.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+# (grid cap, xcd chunk): default, plain order, odd chunks, small caps (grid-stride), cap not a multiple of 8
+GEOMETRIES = [(0, 64), (0, 0), (0, 1), (0, 3), (40, 64), (40, 1), (1000, 7), (13, 2), (8, 1)]
+
+
+@pytest.fixture
+def sw(cuda):
+    import switchml_amd
+    yield switchml_amd
+    switchml_amd.set_grid_limit(0)
+    switchml_amd.set_xcd_chunk(64)
+
+
+def _run_all(sw, torch, x, P, W):
+    dev = x.device
+    n = x.numel()
+    payload, exps = sw.quantize_pack(x, P, W)
+    le, _ = sw.quantize_pack(x, P, W, global_exps=exps, flags=sw.FLAG_PAYLOAD_LE)
+    e_only = sw.exponents(x, P)
+    agg = payload.clone()
+    sw.loopback_aggregate(agg, W)
+    deq = sw.dequantize(agg, exps, n, P, W)
+    rt = sw.roundtrip_loopback(x, P, W)
+    sw_ = sw.bswap_i32(payload)
+    fp = sw.frame_params(max_outstanding_pkts=64)
+    frames = sw.quantize_pack_frames(x, fp, P, W, batch_max=64)
+    rx = sw.RxSlice(n, P, 64, device=dev)
+    nframes = frames.numel() // sw.frame_bytes(P)
+    sw.dequantize_frames(frames, nframes, rx, num_workers=W)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy().copy() for k, v in dict(payload=payload, exps=exps, le=le, e_only=e_only,
+                                                      agg=agg, deq=deq, rt=rt, bswap=sw_, frames=frames,
+                                                      rx_out=rx.out, rx_exps=rx.exps).items()}
+
+
+@pytest.mark.parametrize("P,n", [(256, 1_000_003), (64, 300_001), (1024, 777_777)])
+def test_every_kernel_geometry_invariant(sw, P, n):
+    import torch
+    W = 3
+    x_np = O.splitmix_normal(P + n, n)
+    x = torch.from_numpy(x_np).cuda()
+    ref = None
+    for cap, chunk in GEOMETRIES:
+        sw.set_grid_limit(cap)
+        sw.set_xcd_chunk(chunk)
+        got = _run_all(sw, torch, x, P, W)
+        if ref is None:
+            # the default geometry against the oracle first
+            assert np.array_equal(got["payload"].view(np.uint32), O.quantize(x_np, P, W))
+            assert np.array_equal(got["exps"], O.exponents(x_np, P))
+            dq = O.dequantize(O.loopback_aggregate(O.quantize(x_np, P, W), W), O.exponents(x_np, P), n, P, W)
+            assert np.array_equal(got["deq"].view(np.uint32), dq.view(np.uint32))
+            assert np.array_equal(got["rt"].view(np.uint32), dq.view(np.uint32))
+            # frames go tx -> rx without a switch in between: the sent words come back
+            rx = O.dequantize(O.quantize(x_np, P, W), O.exponents(x_np, P), n, P, W)
+            assert np.array_equal(got["rx_out"].view(np.uint32), rx.view(np.uint32))
+            ref = got
+            continue
+        for k in ref:
+            assert np.array_equal(got[k], ref[k]), (k, cap, chunk)
+
+
+def test_misaligned_slice_geometry_invariant(sw):
+    """4-byte-offset slices (the unaligned vector path) under capped grids."""
+    import torch
+    P, W, n = 256, 2, 262_147
+    x_np = O.splitmix_normal(11, n + 3)
+    xd = torch.from_numpy(x_np).cuda()
+    for off in (1, 2, 3):
+        xs = xd[off:off + n]
+        want = O.quantize(x_np[off:off + n], P, W)
+        for cap, chunk in GEOMETRIES:
+            sw.set_grid_limit(cap)
+            sw.set_xcd_chunk(chunk)
+            payload, _ = sw.quantize_pack(xs, P, W)
+            assert np.array_equal(payload.cpu().numpy().view(np.uint32), want), (off, cap, chunk)
