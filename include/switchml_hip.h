@@ -190,7 +190,7 @@ sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_
  *             exponents): zero-filled by the caller before the slice's first
  *             call (rte_bitmap_reset), persists across its calls
  *   d_counts: uint64[2] {accepted, discarded}, added to; nullable, 8-B aligned
- * Two launches on `stream`: claim, dequantize + commit. */
+ * Three launches on `stream`: claim, dequantize, commit. */
 sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint64_t frame_stride,
                                    uint64_t numel, uint32_t packet_numel, uint16_t num_workers,
                                    uint32_t batch_max, uint64_t job_id, int8_t* d_exps,

@@ -618,12 +618,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
 
 // Pass 2: PostprocessSingle for every winning frame, 1024 payload elements per
 // wave (1024 / P frames; lane-chunk c = u*64 + lane is 16 bytes of frame
-// c / (P/4)), then the winners retire their pkt_id.  The payload loads are
-// issued first, independent of the header; the exponent of block k is the low
-// byte of state[k], whoever holds it (a winner of this call or kRxDone).
-// Every chunk of a frame belongs to this wave and all its state reads precede
-// the commit stores, so a duplicate elsewhere that reads kRxDone instead of
-// the winner's tag loses just the same; the commit keeps the exponent byte.
+// c / (P/4)).  The payload loads are issued first, independent of the header;
+// a frame is the winner of its pkt_id iff state[pkt_id] holds its claim tag;
+// the exponent of block k is the low byte of state[k], whoever holds it (a
+// winner of this call or kRxDone).  Pass 3 retires the winners.
 constexpr int kRxU = 4;                        // 16-B chunks per lane per iteration
 constexpr int kRxTileElems = kRxU * kWave * 4;
 
@@ -669,12 +667,22 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o;
             else store4_guarded(p, o, 0, a.numel - off);
         }
-#pragma unroll
-        for (int u = 0; u < kRxU; u++) {
-            if (!h[u].ok || (u * kWave + lane) % kChunksPerFrame != 0) continue;
-            a.state[h[u].pid] = ((unsigned long long)kRxDone << 32) | h[u].exp;
-            if (h[u].pid < a.nblocks) a.exps[h[u].pid] = (int8_t)h[u].exp;
-        }
+    }
+}
+
+// Pass 3, thread per pkt_id: the winners of this call retire their pkt_id
+// (state -> kRxDone, keeping the exponent byte) and publish the exponent to
+// exps[pkt_id] — one coalesced sweep instead of two scattered 1-8 byte
+// stores per frame inside pass 2 (partial-line stores from many waves).
+__global__ __launch_bounds__(kBlockThreads) void k_rx_commit(RxArgs a) {
+    const uint64_t n = a.nblocks + a.b;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; k < n; k += stride) {
+        const unsigned long long st = a.state[k];
+        const uint32_t hi = (uint32_t)(st >> 32);
+        if (hi == 0u || hi == kRxDone) continue;
+        a.state[k] = ((unsigned long long)kRxDone << 32) | (st & 0xffull);
+        if (k < a.nblocks) a.exps[k] = (int8_t)(st & 0xffull);
     }
 }
 
@@ -1248,6 +1256,7 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
     const uint64_t ntiles = (num_frames * P + kRxTileElems - 1) / kRxTileElems;
     launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
+    k_rx_commit<<<grid_for_vec(a.nblocks + a.b), kBlockThreads, 0, st>>>(a);
     return launch_check();
 }
 

@@ -39,7 +39,8 @@ def main(paths, N=64 * 1024 * 1024, P=256, bm=64, rounds=7, reps=10):
         out.zero_()
         run(L)
         torch.cuda.synchronize()
-        assert torch.equal(out.view(torch.int32), ref.view(torch.int32)), p
+        if not os.environ.get("AB_NOCHECK"):
+            assert torch.equal(out.view(torch.int32), ref.view(torch.int32)), p
     res = {p: [] for p in paths}
     for _ in range(rounds):
         for p, L in zip(paths, libs):
