@@ -623,6 +623,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
 // the exponent of block k is the low byte of state[k], whoever holds it (a
 // winner of this call or kRxDone).  Pass 3 retires the winners.
 constexpr int kRxU = 4;                        // 16-B chunks per lane per iteration
+// Read-only views through the scalar data cache (s_load) for wave-uniform
+// per-frame metadata; loads only — nothing here writes through it.
+typedef const uint32_t __attribute__((address_space(4))) ConstU32;
+typedef const unsigned long long __attribute__((address_space(4))) ConstU64;
 constexpr int kRxTileElems = kRxU * kWave * 4;
 
 template <int P>
@@ -634,27 +638,58 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t ntiles = (a.nframes + kFramesPerTile - 1) / kFramesPerTile;
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+    // the wave index is wave-uniform; say so, so that per-frame addresses are scalar
+    const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_in_block; t < ntiles; t += nwaves) {
         u4a w[kRxU];
         RxHdr h[kRxU];
-#pragma unroll
-        for (int u = 0; u < kRxU; u++) {
-            const int c = u * kWave + lane;
-            const uint64_t f = t * kFramesPerTile + c / kChunksPerFrame;
-            h[u].ok = false;
-            if (f >= a.nframes) continue;
-            // non-temporal: 25 % faster than default-policy loads for this stream (hbm_probe)
-            w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(a.frames + f * a.stride + 52 +
-                                                                           16ull * (c % kChunksPerFrame)));
-            h[u] = rx_header(a, f);
-        }
         float s[kRxU];
+        if constexpr (kChunksPerFrame >= kWave) {
+            // P >= 256: slice u of the tile lies in one frame, so its header and
+            // state words are wave-uniform: scalar loads (no vector-memory
+            // instructions for the per-frame metadata; pass 2 writes neither)
 #pragma unroll
-        for (int u = 0; u < kRxU; u++) {
-            if (!h[u].ok) continue;
-            const uint64_t f = t * kFramesPerTile + (u * kWave + lane) / kChunksPerFrame;
-            h[u].ok = (uint32_t)(a.state[h[u].pid] >> 32) == rx_tag(f);
-            s[u] = h[u].pid >= a.b ? lut[(uint32_t)a.state[h[u].pid - a.b] & 0xffu] : 0.0f;
+            for (int u = 0; u < kRxU; u++) {
+                const uint64_t f = t * kFramesPerTile + (u * kWave) / kChunksPerFrame;
+                if (f < a.nframes)
+                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
+                        a.frames + f * a.stride + 52 + 16ull * ((u * kWave + lane) % kChunksPerFrame)));
+            }
+            const ConstU32* hdr = reinterpret_cast<const ConstU32*>(reinterpret_cast<uintptr_t>(a.frames));
+            const ConstU64* state = reinterpret_cast<const ConstU64*>(reinterpret_cast<uintptr_t>(a.state));
+#pragma unroll
+            for (int u = 0; u < kRxU; u++) {
+                const uint64_t f = t * kFramesPerTile + (u * kWave) / kChunksPerFrame;
+                h[u] = RxHdr{0u, 0u, false};
+                s[u] = 0.0f;
+                if (f >= a.nframes) continue;
+                const uint64_t hw = (f * a.stride + 40) / 4;
+                const uint32_t d10 = hdr[hw], d11 = hdr[hw + 1], d12 = hdr[hw + 2];
+                h[u].pid = d11;
+                h[u].exp = (d12 >> 16) & 0xffu;
+                h[u].ok = (d10 >> 24) == a.job && (uint64_t)d11 < a.nblocks + a.b &&
+                          (uint32_t)(state[d11] >> 32) == rx_tag(f);
+                if (h[u].ok && d11 >= a.b) s[u] = lut[(uint32_t)state[d11 - a.b] & 0xffu];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kRxU; u++) {
+                const int c = u * kWave + lane;
+                const uint64_t f = t * kFramesPerTile + c / kChunksPerFrame;
+                h[u].ok = false;
+                if (f >= a.nframes) continue;
+                // non-temporal: 25 % faster than default-policy loads for this stream (hbm_probe)
+                w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(a.frames + f * a.stride + 52 +
+                                                                               16ull * (c % kChunksPerFrame)));
+                h[u] = rx_header(a, f);
+            }
+#pragma unroll
+            for (int u = 0; u < kRxU; u++) {
+                if (!h[u].ok) continue;
+                const uint64_t f = t * kFramesPerTile + (u * kWave + lane) / kChunksPerFrame;
+                h[u].ok = (uint32_t)(a.state[h[u].pid] >> 32) == rx_tag(f);
+                s[u] = h[u].pid >= a.b ? lut[(uint32_t)a.state[h[u].pid - a.b] & 0xffu] : 0.0f;
+            }
         }
 #pragma unroll
         for (int u = 0; u < kRxU; u++) {
