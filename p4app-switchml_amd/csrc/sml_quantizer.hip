@@ -41,10 +41,16 @@ namespace sml {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u2 __attribute__((ext_vector_type(2)));
 // 16-byte vector with 4-byte alignment: gfx950 runs in unaligned-access mode,
 // so this is still one global_store_dwordx4 (used at the 52-byte frame offset).
 typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
 typedef float f4a __attribute__((ext_vector_type(4), aligned(4)));
+// Read-only views through the scalar data cache (s_load) for wave-uniform
+// metadata (exponent bytes, frame headers, rx state); loads only — nothing in
+// this file writes through the scalar cache.
+typedef const uint32_t __attribute__((address_space(4))) ConstU32;
+typedef const unsigned long long __attribute__((address_space(4))) ConstU64;
 
 __device__ __forceinline__ f4 mkf4(float a, float b, float c, float d) { return f4{a, b, c, d}; }
 __device__ __forceinline__ u4 mku4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return u4{a, b, c, d}; }
@@ -245,6 +251,52 @@ __device__ __forceinline__ void store_exponents(int8_t* exps_out, uint64_t tile_
     }
 }
 
+// A full tile's kPk = 1024 / P exponent bytes are contiguous in exps_out:
+// lane 0 gathers them (v_readlane of each packet's first lane) and writes them
+// with one 1/2/4/8/16-byte store — per-packet byte stores cost ~10 % on the
+// 256 MiB bucket (partial-line writes).  dst must be kPk-byte aligned.
+template <int P>
+__device__ __forceinline__ void store_tile_exponents(int8_t* dst, int lane, const int (&e)[kU]) {
+    constexpr int kPk = kTileElems / P;
+    constexpr int kLanesPerPk = P / 4 < kWave ? P / 4 : kWave;
+    constexpr int kWords = (kPk + 3) / 4;
+    uint32_t w[kWords];
+#pragma unroll
+    for (int i = 0; i < kWords; i++) w[i] = 0;
+#pragma unroll
+    for (int j = 0; j < kPk; j++) {
+        const int u = (j * P) / 256;
+        uint32_t ej = 0;
+#pragma unroll
+        for (int uu = 0; uu < kU; uu++)
+            if (uu == u) ej = (uint32_t)__builtin_amdgcn_readlane(e[uu], (j * kLanesPerPk) % kWave);
+        w[j / 4] |= (ej & 0xffu) << (8 * (j % 4));
+    }
+    if (lane != 0) return;
+    if constexpr (kPk == 16) *reinterpret_cast<u4*>(dst) = mku4(w[0], w[1], w[2], w[3]);
+    else if constexpr (kPk == 8) *reinterpret_cast<u2*>(dst) = u2{w[0], w[1]};
+    else if constexpr (kPk == 4) *reinterpret_cast<uint32_t*>(dst) = w[0];
+    else if constexpr (kPk == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)w[0];
+    else *dst = (int8_t)w[0];
+}
+
+// Exponent byte of each lane's packet in slice u of a tile, with one
+// wave-uniform scalar load per slice (base must be wave-uniform).  A slice
+// holds 4, 2 or 1 packets (P = 64, 128, >= 256); their bytes lie in one
+// aligned dword whenever exps is 4-byte aligned, and always for P > 256.
+template <int P>
+__device__ __forceinline__ bool slice_exps_scalar_ok(const int8_t* exps) {
+    return P > 256 || (reinterpret_cast<uintptr_t>(exps) & 3u) == 0;
+}
+template <int P>
+__device__ __forceinline__ uint32_t slice_exponent_byte(const int8_t* exps, uint64_t base, int u, int lane) {
+    const uintptr_t e0 = reinterpret_cast<uintptr_t>(exps);
+    const uintptr_t first = e0 + base / P + (uint64_t)(u * 256) / P;
+    const uint32_t word = *reinterpret_cast<ConstU32*>(first & ~(uintptr_t)3);
+    const uintptr_t mine = e0 + (base + (uint64_t)(u * kWave + lane) * 4) / P;
+    return (word >> (8 * (mine & 3u))) & 0xffu;
+}
+
 // scale_of for W = 2^k without the double division: 2147483647 / 2^(e+k)
 // rounds to 2^(31-e-k) (normal range for every int8 e and k <= 16), +inf when
 // 31-e-k > 127, and 0 when W * 2^e overflows float (e + k >= 128).
@@ -276,6 +328,10 @@ __device__ __forceinline__ void build_lut(float* lut, uint32_t W) {
 // 8th one; the tail keeps its order (a bijection on [0, nb) either way).
 // Measured on the 256 MiB bucket: C = 64 moves a 1:1 read:write stream
 // 4 % faster than the plain order (profiles/r01/ab5_xcd_chunk.json, hbm_probe_*.json).
+// The wave's index in its workgroup, as a wave-uniform (SGPR) value, so that
+// tile bases and per-tile metadata addresses are scalar.
+__device__ __forceinline__ uint32_t wave_index() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __device__ __forceinline__ uint64_t xcd_block(uint32_t C) {
     const uint64_t b = blockIdx.x;
     if (C == 0) return b;
@@ -319,29 +375,22 @@ __device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, in
     const uint64_t padded = a.nblocks * P;
     int e[kU];
     if constexpr (GLOBAL) {
+        if (base + kTileElems <= padded && slice_exps_scalar_ok<P>(a.gexp)) {
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            uint64_t pkt = (base + (uint64_t)(u * kWave + lane) * 4) / P;
-            e[u] = pkt < a.nblocks ? (int)a.gexp[pkt] : 0;
+            for (int u = 0; u < kU; u++) e[u] = (int)(int8_t)slice_exponent_byte<P>(a.gexp, base, u, lane);
+        } else {
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                uint64_t pkt = (base + (uint64_t)(u * kWave + lane) * 4) / P;
+                e[u] = pkt < a.nblocks ? (int)a.gexp[pkt] : 0;
+            }
         }
     } else {
         tile_exponents<P>(v, e);
         if (a.exps_out) {
             constexpr int kPk = kTileElems / P;   // packets per tile
-            if (P >= 256 && ((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= padded) {
-                // e[] is wave-uniform: lane 0 stores the tile's kPk exponent bytes at once
-                // (per-packet byte stores cost ~10 %: partial-line writes).
-                if (lane == 0) {
-                    int8_t* dst = a.exps_out + base / P;
-                    if constexpr (kPk == 4) {
-                        *reinterpret_cast<uint32_t*>(dst) = (uint32_t)(uint8_t)e[0] | ((uint32_t)(uint8_t)e[1] << 8) |
-                                                            ((uint32_t)(uint8_t)e[2] << 16) | ((uint32_t)(uint8_t)e[3] << 24);
-                    } else if constexpr (kPk == 2) {
-                        *reinterpret_cast<uint16_t*>(dst) = (uint16_t)((uint8_t)e[0] | ((uint8_t)e[2] << 8));
-                    } else {
-                        *dst = (int8_t)e[0];
-                    }
-                }
+            if (((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= padded) {
+                store_tile_exponents<P>(a.exps_out + base / P, lane, e);
             } else {
                 store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
             }
@@ -376,7 +425,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
     if (a.payload) build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t wave = xcd_block(a.xcd) * kWavesPerBlock + (threadIdx.x >> 6);
+    const uint64_t wave = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
     for (uint64_t t = wave * TPW; t < a.ntiles; t += nwaves * TPW) {
         f4 v[TPW][kU];
 #pragma unroll
@@ -463,7 +512,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) 
 #pragma unroll
     for (int i = 1; i < 11; i++) hconst = hd == i ? a.hdr[i] : hconst;
     const uint32_t m2 = 2u * a.mop;
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
         const uint64_t base = t * kTileElems;
         const uint64_t pk0 = base / P;                     // first block of the tile
         QuantArgs qa;                                      // reuse the K1 tile loader
@@ -623,10 +672,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
 // the exponent of block k is the low byte of state[k], whoever holds it (a
 // winner of this call or kRxDone).  Pass 3 retires the winners.
 constexpr int kRxU = 4;                        // 16-B chunks per lane per iteration
-// Read-only views through the scalar data cache (s_load) for wave-uniform
-// per-frame metadata; loads only — nothing here writes through it.
-typedef const uint32_t __attribute__((address_space(4))) ConstU32;
-typedef const unsigned long long __attribute__((address_space(4))) ConstU64;
 constexpr int kRxTileElems = kRxU * kWave * 4;
 
 template <int P>
@@ -638,9 +683,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t ntiles = (a.nframes + kFramesPerTile - 1) / kFramesPerTile;
-    // the wave index is wave-uniform; say so, so that per-frame addresses are scalar
-    const uint32_t wave_in_block = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_in_block; t < ntiles; t += nwaves) {
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < ntiles; t += nwaves) {
         u4a w[kRxU];
         RxHdr h[kRxU];
         float s[kRxU];
@@ -738,18 +781,18 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
     build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
         const uint64_t base = t * kTileElems;
         const bool full = base + kTileElems <= a.numel;
         u4 w[kU];
         float s[kU];
-        if (P == 256 && full && ((uintptr_t)a.exps & 3u) == 0) {
-            // the tile's 4 exponents in one (wave-uniform) dword load
-            const uint32_t e4 = *reinterpret_cast<const uint32_t*>(a.exps + base / P);
+        if (full && slice_exps_scalar_ok<P>(a.exps)) {
+            // each slice's exponent bytes with one scalar load (measured: a
+            // per-lane byte load per slice costs ~8 % at P != 256)
 #pragma unroll
             for (int u = 0; u < kU; u++) {
                 w[u] = __builtin_nontemporal_load(a.payload + (base + (uint64_t)(u * kWave + lane) * 4) / 4);
-                s[u] = lut[(e4 >> (8 * u)) & 0xffu];
+                s[u] = lut[slice_exponent_byte<P>(a.exps, base, u, lane)];
             }
         } else {
 #pragma unroll
@@ -796,7 +839,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t padded = a.nblocks * P;
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + (threadIdx.x >> 6); t < a.ntiles; t += nwaves) {
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
         const uint64_t base = t * kTileElems;
         const bool full = base + kTileElems <= a.numel;
         f4 v[kU];
@@ -812,7 +855,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
         }
         int e[kU];
         tile_exponents<P>(v, e);
-        if (a.exps_out) store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
+        if (a.exps_out) {
+            constexpr int kPk = kTileElems / P;
+            if (((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= padded)
+                store_tile_exponents<P>(a.exps_out + base / P, lane, e);
+            else
+                store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
+        }
 #pragma unroll
         for (int u = 0; u < kU; u++) {
             const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
@@ -862,7 +911,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_words(const uint32_t* in, uin
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t ntiles = (n + kTileElems - 1) / kTileElems;
-    for (uint64_t t = xcd_block(xcd) * kWavesPerBlock + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+    for (uint64_t t = xcd_block(xcd) * kWavesPerBlock + wave_index(); t < ntiles; t += nwaves) {
         const uint64_t base = t * kTileElems;
         if (base + kTileElems <= n) {
             u4a v[kU];
@@ -893,7 +942,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_stream_copy(const u4* in, u4*
     struct { uint32_t xcd; } a{xcd};
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < ntiles; t += nwaves) {
         u4 v[kU];
 #pragma unroll
         for (int u = 0; u < kU; u++) v[u] = __builtin_nontemporal_load(in + t * (kTileElems / 4) + u * kWave + lane);

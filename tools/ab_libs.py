@@ -4,6 +4,7 @@
 §5.4 rule 24).  Usage: ab_libs.py lib1.so lib2.so ..."""
 import ctypes
 import json
+import os
 import statistics
 import sys
 
@@ -87,4 +88,4 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=9, reps=10):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    main(sys.argv[1:], P=int(os.environ.get("AB_P", 256)))
