@@ -328,6 +328,20 @@ def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
     t = timeit(lambda: sw.quantize_pack(xm, P, 1, payload=pm, exps_out=em, stream=stream))
     res["quantize_pack_unaligned_slice_GBps"] = round((8 * (N - 1) + em.numel()) / t / 1e9, 1)
     del xm, pm, em
+    # the other halves of the switch-sim pipeline: K2 (exponents only) and K3 (given global exponents)
+    t = timeit(lambda: sw.exponents(x, P, out=exps, stream=stream))
+    res["exponents_only_GBps"] = round((4 * N + B) / t / 1e9, 1)
+    t = timeit(lambda: sw.quantize_pack(x, P, 1, global_exps=exps, payload=payload, stream=stream))
+    res["quantize_global_exps_GBps"] = round((8 * N + B) / t / 1e9, 1)
+    # other packet sizes: 64 (DPDK's other LTU), 1024 (RDMA message LTU)
+    for Pq in (64, 1024):
+        Bq = sw.num_blocks(N, Pq)
+        eq = torch.empty(Bq, dtype=torch.int8, device=x.device)
+        t = timeit(lambda: sw.quantize_pack(x, Pq, 1, payload=payload, exps_out=eq, stream=stream))
+        res[f"quantize_pack_P{Pq}_GBps"] = round((8 * N + Bq) / t / 1e9, 1)
+        t = timeit(lambda: sw.dequantize(payload, eq, N, Pq, 1, out=out, stream=stream))
+        res[f"dequantize_P{Pq}_GBps"] = round((8 * N + Bq) / t / 1e9, 1)
+    sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=stream)
     t = timeit(lambda: sw.loopback_aggregate(payload, 2, stream=stream))
     res["loopback_x2_GBps"] = round(8 * N / t / 1e9, 1)
     t = timeit(lambda: sw.bswap_i32(payload, out=payload, stream=stream))
