@@ -72,6 +72,13 @@ def test_grid_limit_knob(sw):
     assert sw.set_grid_limit(prev) == 1024
 
 
+def test_xcd_chunk_knob_default_and_roundtrip(sw):
+    """Workgroup order knob: default 64, returns the previous value."""
+    prev = sw.set_xcd_chunk(7)
+    assert prev == 64
+    assert sw.set_xcd_chunk(prev) == 7
+
+
 def test_python_wrapper_rejects_cpu_tensors(sw):
     torch = pytest.importorskip("torch")
     with pytest.raises(TypeError, match="no CPU fallback"):
