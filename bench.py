@@ -73,7 +73,12 @@ def load_traffic(numel, P):
 def cpu_baseline(numel, P, budget_s):
     """The oracle's restatement of the reference CPU path (per-packet
     PreprocessSingle calls in DummyWorkerThread order, b = mop/T ring) on this
-    host's cores, over the same 256 MiB bucket, repeated for ~budget_s."""
+    host's cores, over the same 256 MiB bucket, repeated for ~budget_s.
+
+    `value` is the reference's DEFAULT build, VCL=1 (client_lib/Makefile:26,
+    113-120): its 16-element vector loops restated with SSE2 intrinsics — the
+    instruction set that build targets (no -m flags) — on all cores used.  The
+    scalar VCL=0 path (roundf per element) is reported beside it."""
     import numpy as np
     from oracle import oracle as O
 
@@ -83,19 +88,21 @@ def cpu_baseline(numel, P, budget_s):
     out = np.empty_like(x)
     alg = 8 * numel + O.num_blocks(numel, P)
 
-    def run(T, deadline_s, min_reps):
+    def run(T, deadline_s, min_reps, vcl):
         rates, t_end, reps = [], time.perf_counter() + deadline_s, 0
         while reps < min_reps or time.perf_counter() < t_end:
             t0 = time.perf_counter()
             O.dummy_allreduce(x, P=P, max_outstanding_packets=256, num_worker_threads=T,
-                              num_workers=1, threaded=T > 1, mode=O.MODE_PREPROCESS, out=out)
+                              num_workers=1, threaded=T > 1, mode=O.MODE_PREPROCESS, out=out, vcl=vcl)
             rates.append(alg / (time.perf_counter() - t0) / 1e9)
             reps += 1
         return float(np.median(rates)), reps
 
-    single, reps1 = run(1, budget_s * 0.3, 2)
-    four, reps4 = run(4, budget_s * 0.2, 3) if cores > 4 else (None, 0)
-    multi, repsT = run(cores, budget_s * 0.5, 3)
+    multi, repsT = run(cores, budget_s * 0.35, 3, True)
+    four, reps4 = run(4, budget_s * 0.1, 3, True) if cores > 4 else (None, 0)
+    single, reps1 = run(1, budget_s * 0.1, 2, True)
+    s_multi, s_repsT = run(cores, budget_s * 0.25, 3, False)
+    s_single, s_reps1 = run(1, budget_s * 0.2, 2, False)
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -107,13 +114,16 @@ def cpu_baseline(numel, P, budget_s):
         "unit": "GB/s (8N+B algorithmic bytes, same as value)",
         "cores": cores,
         "kind": "port",
-        "sample": (f"oracle/sml_oracle.c restatement of CpuExponentQuantizerPPP (VCL=0) driven in "
-                   f"DummyWorkerThread order, PreprocessSingle only (exponent + quantize + BE pack into "
-                   f"the b-packet ring), the full {numel * 4 >> 20} MiB bucket, packet_numel {P}, "
-                   f"max_outstanding_packets 256; {cores} worker threads x {repsT} reps (median); "
-                   f"1 thread: {single:.3f} GB/s over {reps1} reps; host CPU {model}"),
+        "sample": (f"oracle/sml_oracle.c restatement of CpuExponentQuantizerPPP as the reference builds it by "
+                   f"default (VCL=1, vector loops in SSE2), driven in DummyWorkerThread order, PreprocessSingle "
+                   f"only (exponent + quantize + BE pack into the b-packet ring), the full {numel * 4 >> 20} MiB "
+                   f"bucket, packet_numel {P}, max_outstanding_packets 256; {cores} worker threads x {repsT} reps "
+                   f"(median); 1 thread: {single:.3f} GB/s; scalar VCL=0 build: {s_multi:.3f} GB/s on {cores} "
+                   f"threads, {s_single:.3f} on 1; host CPU {model}"),
         "single_thread_value": round(single, 3),
         "ref_default_4_threads_value": None if four is None else round(four, 3),
+        "vcl0_scalar_value": round(s_multi, 3),
+        "vcl0_scalar_single_thread_value": round(s_single, 3),
         "cpu_model": model,
         "input_GBps": round(multi * 4 * numel / alg, 3),
     }

@@ -61,6 +61,9 @@ def lib():
         L.orc_slice.argtypes = [u64, i32, i32, ctypes.POINTER(u64), ctypes.POINTER(u64)]
         L.orc_dummy_allreduce.restype = i32
         L.orc_dummy_allreduce.argtypes = [vp, vp, u64, u64, u32, i32, u16, i32, i32]
+        L.orc_dummy_allreduce_ex.restype = i32
+        L.orc_dummy_allreduce_ex.argtypes = [vp, vp, u64, u64, u32, i32, u16, i32, i32, i32]
+        L.orc_quantize_vcl.argtypes = [vp, u64, u64, u16, vp, vp]
         L.orc_dummy_packet_stream.restype = i32
         L.orc_dummy_packet_stream.argtypes = [vp, u64, u64, u32, u16, vp, vp, vp]
         L.orc_build_frames.restype = i32
@@ -109,6 +112,16 @@ def quantize(x: np.ndarray, P: int, num_workers: int = 1, global_exps: np.ndarra
     return out
 
 
+def quantize_vcl(x: np.ndarray, P: int, num_workers: int = 1):
+    """(payload_be uint32[B*P], exps int8[B]) of the VCL=1 build's vector loops (SSE2)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    B = num_blocks(x.size, P)
+    out = np.empty(B * P, dtype=np.uint32)
+    exps = np.empty(B, dtype=np.int8)
+    lib().orc_quantize_vcl(_p(x), x.size, P, num_workers, _p(out), _p(exps))
+    return out, exps
+
+
 def dequantize(payload_be: np.ndarray, exps: np.ndarray, numel: int, P: int, num_workers: int = 1) -> np.ndarray:
     payload_be = np.ascontiguousarray(payload_be, dtype=np.uint32)
     exps = np.ascontiguousarray(exps, dtype=np.int8)
@@ -154,12 +167,14 @@ def slice_geometry(numel: int, num_slices: int, t: int):
 
 def dummy_allreduce(x: np.ndarray, P: int = 256, max_outstanding_packets: int = 256,
                     num_worker_threads: int = 4, num_workers: int = 1, threaded: bool = False,
-                    mode: int = MODE_ROUNDTRIP, out: np.ndarray | None = None) -> np.ndarray:
+                    mode: int = MODE_ROUNDTRIP, out: np.ndarray | None = None, vcl: bool = False) -> np.ndarray:
+    """The dummy-backend packet loop; vcl=True runs the VCL=1 build's vector
+    loops (SSE2 restatement, RNE body) instead of the scalar VCL=0 path."""
     x = np.ascontiguousarray(x, dtype=np.float32)
     if out is None:
         out = np.empty_like(x)
-    rc = lib().orc_dummy_allreduce(_p(x), _p(out), x.size, P, max_outstanding_packets,
-                                   num_worker_threads, num_workers, int(threaded), mode)
+    rc = lib().orc_dummy_allreduce_ex(_p(x), _p(out), x.size, P, max_outstanding_packets,
+                                      num_worker_threads, num_workers, int(threaded), mode, int(vcl))
     if rc != 0:
         raise RuntimeError(f"orc_dummy_allreduce failed rc={rc}")
     return out

@@ -12,6 +12,7 @@
  */
 #include "sml_oracle.h"
 
+#include <emmintrin.h> /* SSE2: the instruction set the reference's VCL=1 build targets */
 #include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
@@ -191,7 +192,70 @@ typedef struct {
     uint16_t W;
     float* scales;    /* scaling_factors_ (ppp.cc:60) */
     const float* lut;
+    int vcl;          /* 1: the VCL=1 build's vector loops (ppp.cc:88-99, 128-140) */
 } orc_ppp;
+
+/* ---- VCL=1 build, restated for the instruction set it is compiled for ----
+ * client_lib/Makefile:113-120 adds -DVCL and no -m flags, so VCL's
+ * instrset selection (un-vendored: github.com/vectorclass/version2) builds
+ * for the x86-64 baseline, SSE2: Vec16f is four __m128.  Per 16 elements:
+ *   quantize (ppp.cc:92-99): roundi(x * s) = cvtps2dq (RNE; out of range or
+ *     NaN -> 0x80000000), then permute64<ENDIANESS_CONVERSION> = bswap32 of
+ *     every word (SSE2 has no pshufb: shifts, masks, or);
+ *   exponent scan (ppp.cc:128-140): max(acc, abs(x)) = maxps, then
+ *     horizontal_max.
+ * The tails (n % 16 elements) run the scalar loops, as in the reference.
+ * Only the timing baseline and the RNE-mode cross-check use this; its bits
+ * equal orc_quantize(rounding = 1) (tested), and like that mode it is parity
+ * unpinned (VCL is not in /root/reference). */
+static inline __m128i bswap32_sse2(__m128i v) {
+    __m128i t = _mm_or_si128(_mm_slli_epi16(v, 8), _mm_srli_epi16(v, 8));   /* swap bytes in 16-bit halves */
+    return _mm_or_si128(_mm_slli_epi32(t, 16), _mm_srli_epi32(t, 16));       /* swap the halves */
+}
+
+static void vcl_quantize_block(const float* in, uint64_t n, float sc, uint32_t* out) {
+    const __m128 s = _mm_set1_ps(sc);
+    uint64_t i = 0, vec = n - n % 16;
+    for (; i < vec; i += 4) {
+        __m128i q = _mm_cvtps_epi32(_mm_mul_ps(_mm_loadu_ps(in + i), s));
+        _mm_storeu_si128((__m128i*)(out + i), bswap32_sse2(q));
+    }
+    for (; i < n; i++) out[i] = orc_quantize_value(in[i], sc);
+}
+
+static int8_t vcl_block_exponent(const float* x, uint64_t n) {
+    const __m128 absmask = _mm_castsi128_ps(_mm_set1_epi32(0x7fffffff));
+    __m128 acc = _mm_setzero_ps();
+    uint64_t i = 0, vec = n - n % 16;
+    for (; i < vec; i += 4) acc = _mm_max_ps(acc, _mm_and_ps(_mm_loadu_ps(x + i), absmask));
+    float current_max = 0.0f;
+    if (vec) { /* horizontal_max */
+        acc = _mm_max_ps(acc, _mm_movehl_ps(acc, acc));
+        acc = _mm_max_ss(acc, _mm_shuffle_ps(acc, acc, 1));
+        current_max = _mm_cvtss_f32(acc);
+    }
+    for (; i < n; i++) {
+        float v = fabsf(x[i]);
+        if (v > current_max) current_max = v;
+    }
+    int32_t bits = (int32_t)f2u(current_max);
+    int32_t e = ((bits & 0x7f800000) >> 23) - 126;
+    return (int8_t)(uint8_t)(e & 0xff);
+}
+
+void orc_quantize_vcl(const float* in, uint64_t numel, uint64_t P, uint16_t num_workers, uint32_t* payload_be,
+                      int8_t* exps) {
+    uint64_t B = orc_num_blocks(numel, P);
+    float lut[256];
+    orc_scale_lut(num_workers, lut);
+    for (uint64_t k = 0; k < B; k++) {
+        uint64_t off = k * P, n = numel - off < P ? numel - off : P;
+        int8_t e = vcl_block_exponent(in + off, n);
+        exps[k] = e;
+        vcl_quantize_block(in + off, n, lut[(uint8_t)e], payload_be + off);
+        for (uint64_t i = n; i < P; i++) payload_be[off + i] = 0u;
+    }
+}
 
 /* PreprocessSingle, FLOAT32 branch — ppp.cc:69-156 */
 static void ppp_preprocess(orc_ppp* s, uint64_t ltu_id, uint32_t* entries, uint8_t* extra) {
@@ -200,13 +264,14 @@ static void ppp_preprocess(orc_ppp* s, uint64_t ltu_id, uint32_t* entries, uint8
         uint64_t off = k * s->P;
         uint64_t n = s->numel - off < s->P ? s->numel - off : s->P;
         float sc = s->scales[k];
-        for (uint64_t i = 0; i < n; i++) entries[i] = orc_quantize_value(s->in[off + i], sc);
+        if (s->vcl) vcl_quantize_block(s->in + off, n, sc, entries);
+        else for (uint64_t i = 0; i < n; i++) entries[i] = orc_quantize_value(s->in[off + i], sc);
         ltu_id = k + s->b;
     }
     if (ltu_id < s->B) {
         uint64_t off = ltu_id * s->P;
         uint64_t n = s->numel - off < s->P ? s->numel - off : s->P;
-        extra[0] = (uint8_t)orc_block_exponent(s->in + off, n);
+        extra[0] = (uint8_t)(s->vcl ? vcl_block_exponent(s->in + off, n) : orc_block_exponent(s->in + off, n));
     }
 }
 
@@ -288,6 +353,12 @@ done:
 int orc_dummy_allreduce(const float* in, float* out, uint64_t numel, uint64_t P,
                         uint32_t max_outstanding_packets, int T, uint16_t W,
                         int threaded, int mode) {
+    return orc_dummy_allreduce_ex(in, out, numel, P, max_outstanding_packets, T, W, threaded, mode, 0);
+}
+
+int orc_dummy_allreduce_ex(const float* in, float* out, uint64_t numel, uint64_t P,
+                           uint32_t max_outstanding_packets, int T, uint16_t W,
+                           int threaded, int mode, int vcl) {
     if (T <= 0 || P == 0) return -1;
     float lut[256];
     orc_scale_lut(W, lut);
@@ -307,6 +378,7 @@ int orc_dummy_allreduce(const float* in, float* out, uint64_t numel, uint64_t P,
         s->b = s->B < batch_max ? s->B : batch_max;
         s->W = W;
         s->lut = lut;
+        s->vcl = vcl;
         ws[t].mode = mode;
         if (s->b == 0 && s->B > 0) { free(ws); free(th); return -1; }
     }

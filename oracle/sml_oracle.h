@@ -92,6 +92,16 @@ int orc_dummy_allreduce(const float* in, float* out, uint64_t numel, uint64_t P,
  * calls of that loop (exponent + quantize+pack into the ring; the scale of
  * block p is stored as the loopback would return it) — the quantize+pack
  * CPU baseline. */
+/* Same, with vcl = 1: the reference's VCL=1 build (its default), whose
+ * 16-element vector loops are restated with SSE2 intrinsics — the x86-64
+ * baseline it is compiled for (client_lib/Makefile:113-120, no -m flags).
+ * RNE body / scalar tail, like orc_quantize(rounding = 1). */
+int orc_dummy_allreduce_ex(const float* in, float* out, uint64_t numel, uint64_t P,
+                           uint32_t max_outstanding_packets, int num_worker_threads,
+                           uint16_t num_workers, int threaded, int mode, int vcl);
+/* Planes of the VCL=1 build (exponents and BE payload), for the cross-check. */
+void orc_quantize_vcl(const float* in, uint64_t numel, uint64_t P, uint16_t num_workers,
+                      uint32_t* payload_be, int8_t* exps);
 #define ORC_MODE_ROUNDTRIP 0
 #define ORC_MODE_PREPROCESS 1
 

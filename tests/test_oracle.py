@@ -263,3 +263,38 @@ def test_threaded_equals_sequential():
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     p = O.dummy_allreduce(x, num_worker_threads=4, num_workers=3, mode=O.MODE_PREPROCESS)
     assert p.shape == x.shape
+
+
+# ------------------------------------------- VCL=1 build (SSE2 restatement) --
+
+@pytest.mark.parametrize("P", [64, 256, 1024])
+@pytest.mark.parametrize("n", [15, 16, 17, 255, 257, 100_003])
+@pytest.mark.parametrize("W", [1, 3])
+def test_vcl_sse2_equals_rne_restatement(P, n, W):
+    """The SSE2 restatement of the VCL=1 loops (cvtps2dq + byte swap; maxps
+    scan) gives the same planes as the scalar RNE_VCL restatement: RNE on the
+    16-aligned body, half-away scalar tail.  Inputs include exact .5 ties,
+    where the two roundings differ."""
+    rng = np.random.default_rng(n + P + W)
+    x = O.splitmix_normal(n * 7 + P, n)
+    x[::5] = (rng.integers(-400, 400, x[::5].size) + 0.5).astype(np.float32) * np.float32(2.0 ** -20)
+    x[::7] = 0.0
+    pl, ex = O.quantize_vcl(x, P, W)
+    assert np.array_equal(ex, O.exponents(x, P))
+    assert np.array_equal(pl, O.quantize(x, P, W, rounding=O.RNE_VCL))
+
+
+def test_vcl_packet_loop_matches_planes():
+    """The CPU baseline's VCL=1 packet loop (DummyWorkerThread order, T slices)
+    reproduces the plane-level RNE_VCL pipeline slice by slice."""
+    n, P, W, T = 300_007, 256, 2, 4
+    x = O.splitmix_normal(99, n)
+    got = O.dummy_allreduce(x, P=P, num_worker_threads=T, num_workers=W, threaded=True, vcl=True)
+    want = np.empty_like(x)
+    for t in range(T):
+        off, m = O.slice_geometry(n, T, t)
+        sl = x[off:off + m]
+        e = O.exponents(sl, P)
+        agg = O.loopback_aggregate(O.quantize(sl, P, W, rounding=O.RNE_VCL), W)
+        want[off:off + m] = O.dequantize(agg, e, m, P, W)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
