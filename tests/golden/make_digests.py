@@ -21,7 +21,8 @@ W * 2^e overflows float (e = 127, W >= 2) — are canonicalized to 0x7fc00000
 before hashing: x86 divides to the negative default NaN 0xffc00000, gfx950
 to the positive one; that sign is the one non-bit-exact case.
 
-Run: python tests/golden/make_digests.py   (rewrites digests.json, ~1 min)
+Run: python tests/golden/make_digests.py   (rewrites digests.json and
+digests_ext.json, ~1 min; --ext-only rewrites only the latter)
 """
 import hashlib
 import json
@@ -79,7 +80,53 @@ def oracle_digests(gen, seed, numel, P, W, T):
     return {k: v.hexdigest() for k, v in h.items()}
 
 
+# Full-size cases for the (f) data formats and the VCL=1 rounding mode:
+#   frames  DPDK frames of the whole slice (BuildPacket + PreprocessSingle for
+#           every packet, dpdk_worker_thread_utils.inc:67-135), stride 1076,
+#           frame params = switchml_amd.frame_params(job_id, pool_start,
+#           pool_shift, max_outstanding_pkts)
+#   rne     payload plane of the VCL=1 build (RNE body, scalar tail;
+#           parity unpinned: VCL is not in the reference tree)
+EXT_CASES = [
+    # name, kind, generator, seed, numel, P, W, extra
+    ("cfg2_frames_grad", "frames", "grad", 45, 16_777_216, 256, 1,
+     {"batch_max": 64, "job_id": 5, "pool_index_start": 3, "pool_index_shift": 7, "max_outstanding_pkts": 64}),
+    ("frames_P64_W2_ragged", "frames", "randbits", 9, 4_000_037, 64, 2,
+     {"batch_max": 100, "job_id": 1, "pool_index_start": 0, "pool_index_shift": 0, "max_outstanding_pkts": 50}),
+    ("cfg2_rne_grad_W3", "rne", "grad", 46, 16_777_216 + 77, 256, 3, {}),
+]
+
+
+def frame_params(extra):
+    sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
+    import switchml_amd as sw  # the ctypes struct only; no GPU library call
+    return sw.frame_params(job_id=extra["job_id"], pool_index_start=extra["pool_index_start"],
+                           pool_index_shift=extra["pool_index_shift"],
+                           max_outstanding_pkts=extra["max_outstanding_pkts"])
+
+
+def oracle_ext_digest(kind, gen, seed, numel, P, W, extra):
+    x = make_input(gen, seed, numel)
+    if kind == "frames":
+        fr = O.build_frames(x, frame_params(extra), P, W, batch_max=extra["batch_max"])
+        return hashlib.sha256(fr.tobytes()).hexdigest()
+    if kind == "rne":
+        return hashlib.sha256(O.quantize(x, P, W, rounding=O.RNE_VCL).tobytes()).hexdigest()
+    raise ValueError(kind)
+
+
 def main():
+    ext = {}
+    for name, kind, gen, seed, numel, P, W, extra in EXT_CASES:
+        ext[name] = {"kind": kind, "gen": gen, "seed": seed, "numel": numel, "packet_numel": P,
+                     "num_workers": W, "extra": extra,
+                     "sha256": oracle_ext_digest(kind, gen, seed, numel, P, W, extra)}
+        print(name, ext[name]["sha256"][:16], flush=True)
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "digests_ext.json"), "w") as f:
+        json.dump(ext, f, indent=1)
+        f.write("\n")
+    if "--ext-only" in sys.argv:
+        return
     res = {}
     for name, gen, seed, numel, P, W, T in CASES:
         res[name] = {"gen": gen, "seed": seed, "numel": numel, "packet_numel": P, "num_workers": W,

@@ -20,6 +20,8 @@ from oracle import oracle as O
 HERE = os.path.dirname(os.path.abspath(__file__))
 with open(os.path.join(HERE, "golden", "digests.json")) as _f:
     DIGESTS = json.load(_f)
+with open(os.path.join(HERE, "golden", "digests_ext.json")) as _f:
+    DIGESTS_EXT = json.load(_f)
 
 
 def _gen():
@@ -72,3 +74,30 @@ def test_hip_path_reproduces_digests(cuda, name):
     assert h["payload"].hexdigest() == want["payload"]
     assert h["out"].hexdigest() == want["out"]
     assert h["fused"].hexdigest() == want["out"]
+
+
+@pytest.mark.parametrize("name", sorted(DIGESTS_EXT))
+def test_oracle_reproduces_ext_digests(name):
+    c = DIGESTS_EXT[name]
+    got = _gen().oracle_ext_digest(c["kind"], c["gen"], c["seed"], c["numel"], c["packet_numel"],
+                                   c["num_workers"], c["extra"])
+    assert got == c["sha256"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(DIGESTS_EXT))
+def test_hip_path_reproduces_ext_digests(cuda, name):
+    """Full-size DPDK frames (sml_quantize_pack_frames) and the VCL=1
+    rounding mode (SML_FLAG_ROUND_RNE) against the oracle's digests."""
+    import torch
+    import switchml_amd as sw
+    m = _gen()
+    c = DIGESTS_EXT[name]
+    n, P, W, ex = c["numel"], c["packet_numel"], c["num_workers"], c["extra"]
+    x = torch.from_numpy(m.make_input(c["gen"], c["seed"], n)).to(cuda)
+    if c["kind"] == "frames":
+        out = sw.quantize_pack_frames(x, m.frame_params(ex), P, W, batch_max=ex["batch_max"])
+    else:
+        out, _ = sw.quantize_pack(x, P, W, flags=sw.FLAG_ROUND_RNE)
+    torch.cuda.synchronize()
+    assert hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest() == c["sha256"]
