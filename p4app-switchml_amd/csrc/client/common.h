@@ -59,6 +59,11 @@ struct Tensor {
     }
 };
 
+// How long a waiter polls before it sleeps (job completion, a worker's
+// stream, an idle worker waiting for the next job), in microseconds.
+// SWITCHML_SPIN_US overrides the default; 0 = always sleep at once.
+int SpinMicros();
+
 }  // namespace switchml
 
 #endif  // SWITCHML_AMD_COMMON_H_

@@ -1,6 +1,9 @@
 // fifo_scheduler.cc — see fifo_scheduler.h.
 #include "fifo_scheduler.h"
 
+#include <chrono>
+#include <thread>
+
 namespace switchml {
 
 bool Barrier::Wait() {
@@ -48,6 +51,7 @@ bool FifoScheduler::EnqueueJob(std::shared_ptr<Job> job) {
     finished_job_slices_[job->id_] = 0;
     undispatched_job_slices_[job->id_] = config_.general_.num_worker_threads;
     queue_.push(job);
+    queue_size_.store(queue_.size(), std::memory_order_release);
     job_submitted_event_.notify_all();
     return true;
 }
@@ -60,6 +64,17 @@ bool FifoScheduler::GetJobSlice(WorkerTid tid, JobSlice& job_slice) {
     // All worker threads meet here so that they take slices of the same job.
     if (!barrier_.Wait()) return false;
     std::unique_lock<std::mutex> lock(access_mutex_);
+    if (!stopped_ && queue_.empty() && SpinMicros() > 0) {
+        // Jobs tend to come in bursts (a framework's gradient buckets): poll
+        // for a short while before sleeping, so the next job does not pay a
+        // futex wake-up.
+        lock.unlock();
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(SpinMicros());
+        while (!stopped_flag_.load(std::memory_order_acquire) && queue_size_.load(std::memory_order_acquire) == 0 &&
+               std::chrono::steady_clock::now() < until)
+            std::this_thread::yield();
+        lock.lock();
+    }
     job_submitted_event_.wait(lock, [this] { return stopped_ || !queue_.empty(); });
     if (stopped_) return false;
 
@@ -67,6 +82,7 @@ bool FifoScheduler::GetJobSlice(WorkerTid tid, JobSlice& job_slice) {
     int& left = undispatched_job_slices_.at(job->id_);
     if (--left == 0) {
         queue_.pop();
+        queue_size_.store(queue_.size(), std::memory_order_release);
         undispatched_job_slices_.erase(job->id_);
     }
     job_slice.job = job;
@@ -96,11 +112,13 @@ bool FifoScheduler::NotifyJobSliceCompletion(WorkerTid, const JobSlice& job_slic
 void FifoScheduler::Stop() {
     std::unique_lock<std::mutex> lock(access_mutex_);
     stopped_ = true;
+    stopped_flag_.store(true, std::memory_order_release);
     barrier_.Destroy();
     while (!queue_.empty()) {
         queue_.front()->SetJobStatus(FAILED);
         queue_.pop();
     }
+    queue_size_.store(0, std::memory_order_release);
     undispatched_job_slices_.clear();
     job_submitted_event_.notify_all();
 }

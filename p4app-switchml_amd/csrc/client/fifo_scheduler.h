@@ -8,6 +8,7 @@
 #include <condition_variable>
 #include <map>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <queue>
 
@@ -60,6 +61,10 @@ class FifoScheduler {
     std::map<JobId, int> finished_job_slices_;
     Barrier barrier_;
     bool stopped_ = false;
+    // lock-free mirrors of stopped_ / queue_.size() for the short poll before
+    // a worker sleeps on job_submitted_event_
+    std::atomic<bool> stopped_flag_{false};
+    std::atomic<size_t> queue_size_{0};
 };
 
 }  // namespace switchml

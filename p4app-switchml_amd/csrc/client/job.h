@@ -19,7 +19,7 @@ class Job {
     Job(const Job&) = delete;
     Job& operator=(const Job&) = delete;
 
-    // Block until the job is FINISHED or FAILED.
+    // Block until the job is FINISHED or FAILED (polls for SpinMicros() first).
     void WaitToComplete();
     JobStatus GetJobStatus() const { return job_status_.load(); }
     // Statuses only move forward; FINISHED/FAILED wake waiters (job.cc:49-57).

@@ -5,6 +5,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <memory>
 #include <string>
@@ -25,6 +26,18 @@ void hip_ok(hipError_t e, const char* what) {
 void sml_ok(int s, const char* what) {
     if (s != SML_OK)
         throw SwitchMLFatal(std::string(what) + ": " + sml_status_string((sml_status_t)s) + " " + sml_last_error());
+}
+
+// Wait for the worker's stream: poll for a short while (a slice's kernels
+// usually finish within it), then block in hipStreamSynchronize.
+void stream_wait(hipStream_t st) {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(SpinMicros());
+    do {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) hip_ok(q, "hipStreamQuery");
+    } while (std::chrono::steady_clock::now() < until);
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
 }
 
 // Grow-only device buffer owned by one worker thread.
@@ -115,7 +128,7 @@ uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, J
     }
     if (!out_dev)
         hip_ok(hipMemcpyAsync(t.out_ptr, staged.slice.out_ptr, bytes, hipMemcpyDeviceToHost, st), "hipMemcpyAsync D2H");
-    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    stream_wait(st);
     ppp->CleanupJobSlice();
     return packets;
 }
