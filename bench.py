@@ -44,6 +44,9 @@ def parse():
                          "(HBM/fabric clocks ramp under load: profiles/r01/bench_warmup_sweep.jsonl)")
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024, help="fp32 elements per GPU (256 MiB)")
     ap.add_argument("--packet-numel", type=int, default=256)
+    ap.add_argument("--job-numel", type=int, default=0,
+                    help="strong scaling: one job of this many fp32 elements split over the ranks by the FIFO "
+                         "rule (configs[3]: 268435456 = 1 GiB); 0 = --numel per GPU (weak scaling, default)")
     ap.add_argument("--grid-limit", type=int, default=0, help="workgroups per launch (0 = one per 4 tiles)")
     ap.add_argument("--xcd-chunk", type=int, default=64,
                     help="workgroups per contiguous run on one XCD (0 = plain blockIdx order)")
@@ -155,7 +158,15 @@ def main():
         sw.set_grid_limit(args.grid_limit)
     sw.set_xcd_chunk(args.xcd_chunk)
 
-    N, P = args.numel, args.packet_numel
+    P = args.packet_numel
+    if args.job_numel:
+        # configs[3]: one job sharded over the ranks, slice g -> GPU g (fifo_scheduler.cc:93-109)
+        N = sw.fifo_slice(args.job_numel, world, rank)[1]
+        total_alg = sum(8 * n + sw.num_blocks(n, P)
+                        for n in (sw.fifo_slice(args.job_numel, world, r)[1] for r in range(world)))
+    else:
+        N = args.numel
+        total_alg = world * (8 * N + sw.num_blocks(N, P))
     B = sw.num_blocks(N, P)
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
@@ -236,7 +247,7 @@ def main():
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
-        value = world * alg_bytes / (elapsed / args.steps) / 1e9
+        value = total_alg / (elapsed / args.steps) / 1e9
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
         line = {
             "metric": "fp32→int32 quantize+pack GB/s (device-resident), 256 MiB bucket, 1/2/4/8 GPU",
@@ -248,13 +259,16 @@ def main():
             "settle_ms": args.settle_ms,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.job_numel else "weak",
             "vs_baseline": None,
             "dtype": "f32->i32",
             "data": "synthetic N(0,1) fp32 (torch.randn on device, seed 42+rank)",
             "config": {
-                "workload": "configs[2]-sized bucket: 256 MiB fp32 per GPU, fused exponent+quantize+BE pack "
-                            "(sml_quantize_pack, K1), loopback exponents (W=1)",
+                "workload": (f"configs[3]-style job: {args.job_numel * 4 >> 20} MiB fp32 sharded over {world} GPU(s) "
+                             "by the FIFO rule, fused exponent+quantize+BE pack (sml_quantize_pack, K1), loopback "
+                             "exponents (W=1)") if args.job_numel else
+                            ("configs[2]-sized bucket: 256 MiB fp32 per GPU, fused exponent+quantize+BE pack "
+                             "(sml_quantize_pack, K1), loopback exponents (W=1)"),
                 "numel_per_gpu": N,
                 "packet_numel": P,
                 "num_blocks_per_gpu": B,
@@ -263,7 +277,7 @@ def main():
                 "xcd_chunk": args.xcd_chunk,
                 "launch": "eager" if args.graph_steps <= 1 else f"hipGraph replay, {args.graph_steps} steps per graph",
             },
-            "input_GBps": round(world * 4 * N / (elapsed / args.steps) / 1e9, 2),
+            "input_GBps": round(4 * (args.job_numel or world * N) / (elapsed / args.steps) / 1e9, 2),
             "kernel_ms": round(kern_ms_max, 5),
             "roofline": {
                 "bound": "hbm",
