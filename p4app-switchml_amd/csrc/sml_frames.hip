@@ -1,0 +1,458 @@
+// sml_frames.hip — DPDK wire frames on gfx950: the transmit
+// side (BuildPacket + PreprocessSingle for every packet of a slice,
+// client_lib/src/backends/dpdk/dpdk_worker_thread_utils.inc:42-135) and the
+// receive side (DpdkWorkerThread's rx loop, dpdk_worker_thread.cc:300-345,
+// with PostprocessSingle per accepted frame), and their C-ABI entry points.
+#include "sml_host.h"
+
+namespace sml {
+
+// ---------------------------------------------------------- DPDK frames
+
+struct FrameArgs {
+    const float* in;
+    uint64_t numel;
+    uint64_t nblocks;       // B
+    uint64_t ntiles;        // ceil(B*P / 1024)
+    uint64_t b;             // extra-batch size = min(batch_max, B)
+    const int8_t* gexp;     // global exponents or nullptr
+    uint8_t* frames;        // B + b frames, 4-byte aligned
+    uint64_t stride;        // bytes between frames, multiple of 4
+    uint32_t W;
+    uint32_t xcd;           // xcd_block chunk (0 = plain order)
+    uint32_t pool_start, pool_shift, mop;
+    uint32_t hdr[11];       // frame bytes 0..43: Eth, IPv4, UDP, job_type_size, short_job_id
+};
+
+// PktId2PoolIndex, dpdk_worker_thread_utils.inc:42-52.
+__device__ __forceinline__ uint32_t pool_index(uint64_t p, const FrameArgs& a) {
+    const uint32_t i = (uint32_t)((p + a.pool_shift) % (2ull * a.mop));
+    return i < a.mop ? ((a.pool_start + i) & 0xffffu) : (((a.pool_start + (i - a.mop)) | 0x8000u) & 0xffffu);
+}
+
+// Lanes 0..12 write the 52 header bytes of frame p (one dword each):
+// dwords 0-10 constant, 11 = pkt_id (host order), 12 = pool index (BE16),
+// exponent byte, zero byte.  (Extra-batch frames; the bulk of the headers is
+// written lane-parallel by k_quantize_frames.)
+__device__ __forceinline__ void write_frame_header(const FrameArgs& a, uint64_t p, int lane, uint32_t exp_byte) {
+    if (lane > 12) return;
+    uint32_t dw = a.hdr[0];
+#pragma unroll
+    for (int i = 1; i < 11; i++) dw = lane == i ? a.hdr[i] : dw;
+    if (lane == 11) dw = (uint32_t)p;
+    if (lane == 12) {
+        const uint32_t pool = pool_index(p, a);
+        dw = (pool >> 8) | ((pool & 0xffu) << 8) | ((exp_byte & 0xffu) << 16);
+    }
+    *reinterpret_cast<uint32_t*>(a.frames + p * a.stride + 4 * lane) = dw;
+}
+
+// Fused quantize + pack into DPDK frames (BuildPacket + PreprocessSingle for
+// every packet of the slice, dpdk_worker_thread_utils.inc:67-135 + ppp.cc:69-156).
+//
+// Frame f carries the exponent of block f (f < B) in header dword 12 (pool
+// index BE16, exponent byte, zero byte) and the payload of block f - b.  The
+// wave of block k therefore writes:
+//  * frame k + b: header dwords 0-11 and the payload — one wave writes all
+//    of the frame but dword 12 (and dword 12 too once k + b >= B: those
+//    frames carry exponent 0);
+//  * dword 12 of frame k (k >= b), or the whole of extra-batch frame k
+//    (k < b: header with this exponent, zero payload).
+// One dword store instruction covers 4 frames: lane l < 48 writes dword
+// l % 12 of payload frame l / 12, lanes 48-51 write dword 12 of the 4
+// exponent frames.  Constant dwords are picked once per wave; the pool index
+// (PktId2PoolIndex) costs one 64-bit modulo per tile.
+__device__ __forceinline__ uint32_t pool_dword(const FrameArgs& a, uint32_t i, uint32_t exp_byte) {
+    const uint32_t pool = i < a.mop ? ((a.pool_start + i) & 0xffffu) : (((a.pool_start + (i - a.mop)) | 0x8000u) & 0xffffu);
+    return (pool >> 8) | ((pool & 0xffu) << 8) | ((exp_byte & 0xffu) << 16);
+}
+
+template <int P, bool ALIGNED, bool GLOBAL>
+__global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) {
+    __shared__ float lut[256];
+    build_lut(lut, a.W);
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t padded = a.nblocks * P;
+    constexpr int kPk = kTileElems / P;                   // packets per tile
+    constexpr int kLanesPerPk = P / 4 < kWave ? P / 4 : kWave;
+    const int hd = lane % 12;                              // header dword of lanes 0..47
+    const int hj = lane < 48 ? lane / 12 : lane - 48;      // frame (of 4) of lanes 0..51
+    uint32_t hconst = a.hdr[0];
+#pragma unroll
+    for (int i = 1; i < 11; i++) hconst = hd == i ? a.hdr[i] : hconst;
+    const uint32_t m2 = 2u * a.mop;
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
+        const uint64_t base = t * kTileElems;
+        const uint64_t pk0 = base / P;                     // first block of the tile
+        QuantArgs qa;                                      // reuse the K1 tile loader
+        qa.in = a.in;
+        qa.numel = a.numel;
+        f4 v[kU];
+        load_tile<ALIGNED>(qa, base, lane, v);
+        int eloc[kU];
+        tile_exponents<P>(v, eloc);
+        // exponent of packet j of the tile: slice j*P/256, lane (j*P/4) % 64
+        uint32_t ej[kPk];
+#pragma unroll
+        for (int j = 0; j < kPk; j++) {
+            const int u = (j * P) / 256;
+            ej[j] = 0;
+#pragma unroll
+            for (int uu = 0; uu < kU; uu++)
+                if (uu == u) ej[j] = (uint32_t)__builtin_amdgcn_readlane(eloc[uu], (j * kLanesPerPk) % kWave);
+        }
+        const uint32_t r = (uint32_t)((pk0 + a.pool_shift) % m2);   // pool slot of frame pk0
+        const bool extra = pk0 < a.b;                               // wave-uniform, first b / kPk tiles
+#pragma unroll
+        for (int j0 = 0; j0 < kPk; j0 += 4) {
+            const int j = j0 + hj;
+            if (lane < 48) {
+                if (j < kPk && pk0 + j < a.nblocks) {
+                    const uint64_t f = pk0 + j + a.b;
+                    *reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 4 * hd) = hd == 11 ? (uint32_t)f : hconst;
+                }
+            } else if (lane < 52 && !extra) {
+                if (j < kPk && pk0 + j < a.nblocks) {
+                    uint32_t e = 0;
+#pragma unroll
+                    for (int jj = 0; jj < kPk; jj++) e = j == jj ? ej[jj] : e;
+                    *reinterpret_cast<uint32_t*>(a.frames + (pk0 + j) * a.stride + 48) = pool_dword(a, (r + (uint32_t)j) % m2, e);
+                }
+            }
+        }
+        if (__builtin_expect(pk0 + kPk + a.b > a.nblocks, 0)) {
+            // tail: payload frames at or past B carry exponent 0; their dword 12 is ours
+            if (lane < kPk && pk0 + lane < a.nblocks && pk0 + lane + a.b >= a.nblocks) {
+                const uint64_t f = pk0 + lane + a.b;
+                *reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 48) =
+                    pool_dword(a, (uint32_t)((f + a.pool_shift) % m2), 0u);
+            }
+        }
+        if (__builtin_expect(extra, 0)) {
+            // extra-batch frames: header with this tile's exponent, zero payload; all ours
+#pragma unroll
+            for (int j = 0; j < kPk; j++) {
+                const uint64_t pk = pk0 + j;
+                if (pk >= a.nblocks) break;
+                if (pk < a.b) {
+                    write_frame_header(a, pk, lane, ej[j]);
+                    uint32_t* pl = reinterpret_cast<uint32_t*>(a.frames + pk * a.stride + 52);
+                    for (int i = lane; i < P / 4; i += kWave) *reinterpret_cast<u4a*>(pl + 4 * i) = u4a{0u, 0u, 0u, 0u};
+                } else if (lane == 0) {
+                    *reinterpret_cast<uint32_t*>(a.frames + pk * a.stride + 48) =
+                        pool_dword(a, (uint32_t)((pk + a.pool_shift) % m2), ej[j]);
+                }
+            }
+        }
+        // payloads
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            if (idx >= padded) continue;
+            const uint64_t k = idx / P;
+            int e = eloc[u];
+            if constexpr (GLOBAL) e = a.gexp[k];
+            const u4 q = quantize4<false>(v[u], lut[(uint8_t)e], idx, 0);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(a.frames + (k + a.b) * a.stride + 52) + (idx - k * P);
+            *reinterpret_cast<u4a*>(dst) = u4a{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)};
+        }
+    }
+}
+
+// ------------------------------------------------- DPDK frames, receive side
+//
+// The rx bitmap of DpdkWorkerThread (dpdk_worker_thread.cc:316-342) becomes a
+// per-slice 64-bit state word per packet id: high half 0 = not received,
+// kRxDone = received in an earlier call, otherwise the claim tag of the frame
+// that won it in the current call (larger tag = earlier frame, so a 64-bit
+// atomicMax picks the first copy); low byte = that frame's exponent byte, so
+// the winner's exponent travels with the claim (PostprocessSingle's
+// scaling_factors_[pkt_id], ppp.cc:254-260) and needs no separate pass.
+constexpr uint32_t kRxDone = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t rx_tag(uint64_t f) { return 0xFFFFFFFEu - (uint32_t)f; }
+
+struct RxArgs {
+    const uint8_t* frames;
+    uint64_t nframes;
+    uint64_t stride;
+    uint64_t numel;
+    uint64_t nblocks;           // B
+    uint64_t b;                 // extra batch
+    unsigned long long* state;  // [B + b]
+    int8_t* exps;               // [B]
+    float* out;
+    unsigned long long* counts; // {accepted, discarded} or nullptr
+    uint32_t W;
+    uint32_t xcd;           // xcd_block chunk (0 = plain order)
+    uint32_t job;               // (uint8_t)job_id
+};
+
+// Header dwords 10..12 of frame f: short_job_id = byte 43, pkt_id = bytes
+// 44-47 (host order), exponent = byte 50.
+struct RxHdr {
+    uint32_t pid;
+    uint32_t exp;
+    bool ok;                    // this job, pkt_id in range
+};
+
+__device__ __forceinline__ RxHdr rx_header(const RxArgs& a, uint64_t f) {
+    const uint32_t* h = reinterpret_cast<const uint32_t*>(a.frames + f * a.stride + 40);
+    const uint32_t d10 = h[0], d11 = h[1], d12 = h[2];
+    RxHdr r;
+    r.pid = d11;
+    r.exp = (d12 >> 16) & 0xffu;
+    r.ok = (d10 >> 24) == a.job && (uint64_t)d11 < a.nblocks + a.b;
+    return r;
+}
+
+// Pass 1, thread per frame: frames of another job, out-of-range or already
+// received pkt_ids are discarded; the others claim their pkt_id.  Counting:
+// accepted = frames - discarded, so block 0 adds the frame count once and only
+// workgroups that saw a discard touch the counters (same-address atomics from
+// every workgroup serialize in one L2 channel: ~40 us at 262 k frames).
+__global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
+    __shared__ uint32_t disc;
+    if (threadIdx.x == 0) disc = 0;
+    __syncthreads();
+    uint32_t mine = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
+        const RxHdr h = rx_header(a, f);
+        if (!h.ok) { mine++; continue; }
+        const unsigned long long v = ((unsigned long long)rx_tag(f) << 32) | h.exp;
+        if (atomicMax(a.state + h.pid, v) != 0ull) mine++;          // duplicate or received earlier
+    }
+    if (a.counts) {
+        if (mine) atomicAdd(&disc, mine);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long acc = blockIdx.x == 0 ? (unsigned long long)a.nframes : 0ull;
+            acc -= disc;                                                 // mod 2^64
+            if (acc) atomicAdd(a.counts + 0, acc);
+            if (disc) atomicAdd(a.counts + 1, (unsigned long long)disc);
+        }
+    }
+}
+
+// Pass 2: PostprocessSingle for every winning frame, 1024 payload elements per
+// wave (1024 / P frames; lane-chunk c = u*64 + lane is 16 bytes of frame
+// c / (P/4)).  The payload loads are issued first, independent of the header;
+// a frame is the winner of its pkt_id iff state[pkt_id] holds its claim tag;
+// the exponent of block k is the low byte of state[k], whoever holds it (a
+// winner of this call or kRxDone).  Pass 3 retires the winners.
+constexpr int kRxU = 4;                        // 16-B chunks per lane per iteration
+constexpr int kRxTileElems = kRxU * kWave * 4;
+
+template <int P>
+__global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
+    __shared__ float lut[256];
+    build_lut(lut, a.W);
+    constexpr int kChunksPerFrame = P / 4;     // 16-B chunks per payload
+    constexpr int kFramesPerTile = kRxTileElems / P;
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t ntiles = (a.nframes + kFramesPerTile - 1) / kFramesPerTile;
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < ntiles; t += nwaves) {
+        u4a w[kRxU];
+        RxHdr h[kRxU];
+        float s[kRxU];
+        if constexpr (kChunksPerFrame >= kWave) {
+            // P >= 256: slice u of the tile lies in one frame, so its header and
+            // state words are wave-uniform: scalar loads (no vector-memory
+            // instructions for the per-frame metadata; pass 2 writes neither)
+#pragma unroll
+            for (int u = 0; u < kRxU; u++) {
+                const uint64_t f = t * kFramesPerTile + (u * kWave) / kChunksPerFrame;
+                if (f < a.nframes)
+                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
+                        a.frames + f * a.stride + 52 + 16ull * ((u * kWave + lane) % kChunksPerFrame)));
+            }
+            const ConstU32* hdr = reinterpret_cast<const ConstU32*>(reinterpret_cast<uintptr_t>(a.frames));
+            const ConstU64* state = reinterpret_cast<const ConstU64*>(reinterpret_cast<uintptr_t>(a.state));
+#pragma unroll
+            for (int u = 0; u < kRxU; u++) {
+                const uint64_t f = t * kFramesPerTile + (u * kWave) / kChunksPerFrame;
+                h[u] = RxHdr{0u, 0u, false};
+                s[u] = 0.0f;
+                if (f >= a.nframes) continue;
+                const uint64_t hw = (f * a.stride + 40) / 4;
+                const uint32_t d10 = hdr[hw], d11 = hdr[hw + 1], d12 = hdr[hw + 2];
+                h[u].pid = d11;
+                h[u].exp = (d12 >> 16) & 0xffu;
+                h[u].ok = (d10 >> 24) == a.job && (uint64_t)d11 < a.nblocks + a.b &&
+                          (uint32_t)(state[d11] >> 32) == rx_tag(f);
+                if (h[u].ok && d11 >= a.b) s[u] = lut[(uint32_t)state[d11 - a.b] & 0xffu];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kRxU; u++) {
+                const int c = u * kWave + lane;
+                const uint64_t f = t * kFramesPerTile + c / kChunksPerFrame;
+                h[u].ok = false;
+                if (f >= a.nframes) continue;
+                // non-temporal: 25 % faster than default-policy loads for this stream (hbm_probe)
+                w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(a.frames + f * a.stride + 52 +
+                                                                               16ull * (c % kChunksPerFrame)));
+                h[u] = rx_header(a, f);
+            }
+#pragma unroll
+            for (int u = 0; u < kRxU; u++) {
+                if (!h[u].ok) continue;
+                const uint64_t f = t * kFramesPerTile + (u * kWave + lane) / kChunksPerFrame;
+                h[u].ok = (uint32_t)(a.state[h[u].pid] >> 32) == rx_tag(f);
+                s[u] = h[u].pid >= a.b ? lut[(uint32_t)a.state[h[u].pid - a.b] & 0xffu] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kRxU; u++) {
+            if (!h[u].ok || h[u].pid < a.b) continue;
+            const uint64_t off = (uint64_t)(h[u].pid - a.b) * P + 4ull * ((u * kWave + lane) % kChunksPerFrame);
+            if (off >= a.numel) continue;
+            const f4 o = mkf4(dequantize1(bswap(w[u].x), s[u]), dequantize1(bswap(w[u].y), s[u]),
+                              dequantize1(bswap(w[u].z), s[u]), dequantize1(bswap(w[u].w), s[u]));
+            float* p = a.out + off;
+            if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o;
+            else store4_guarded(p, o, 0, a.numel - off);
+        }
+    }
+}
+
+// Pass 3, thread per pkt_id: the winners of this call retire their pkt_id
+// (state -> kRxDone, keeping the exponent byte) and publish the exponent to
+// exps[pkt_id] — one coalesced sweep instead of two scattered 1-8 byte
+// stores per frame inside pass 2 (partial-line stores from many waves).
+__global__ __launch_bounds__(kBlockThreads) void k_rx_commit(RxArgs a) {
+    const uint64_t n = a.nblocks + a.b;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; k < n; k += stride) {
+        const unsigned long long st = a.state[k];
+        const uint32_t hi = (uint32_t)(st >> 32);
+        if (hi == 0u || hi == kRxDone) continue;
+        a.state[k] = ((unsigned long long)kRxDone << 32) | (st & 0xffull);
+        if (k < a.nblocks) a.exps[k] = (int8_t)(st & 0xffull);
+    }
+}
+
+// ------------------------------------------------------------ host side
+
+template <bool ALIGNED, bool GLOBAL>
+static void launch_frames_p(uint32_t P, dim3 grid, hipStream_t st, const FrameArgs& a) {
+    switch (P) {
+        case 64:   k_quantize_frames<64, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_quantize_frames<128, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_quantize_frames<256, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_quantize_frames<512, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_quantize_frames<1024, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
+static void launch_rx_apply(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
+    switch (P) {
+        case 64:   k_rx_apply<64><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_rx_apply<128><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_rx_apply<256><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_rx_apply<512><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_rx_apply<1024><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
+}  // namespace sml
+
+using namespace sml;
+
+extern "C" {
+
+uint64_t sml_frame_bytes(uint32_t packet_numel) { return 52ull + 4ull * packet_numel; }
+
+sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_t P, uint16_t W,
+                                      const int8_t* d_global_exps, uint32_t batch_max,
+                                      const sml_frame_params* prm, void* frames, uint64_t stride, void* stream) {
+    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
+    if (W == 0 || !prm || batch_max == 0) return SML_ERR_INVALID_ARG;
+    if (numel == 0) return SML_OK;
+    if (!d_in || !aligned4(d_in) || !frames) return SML_ERR_INVALID_ARG;
+    if (!aligned4(frames) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
+    FrameArgs a;
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    a.in = d_in;
+    a.numel = numel;
+    a.nblocks = sml_num_blocks(numel, P);
+    a.ntiles = (a.nblocks * P + kTileElems - 1) / kTileElems;
+    a.b = a.nblocks < batch_max ? a.nblocks : batch_max;
+    a.gexp = d_global_exps;
+    a.frames = static_cast<uint8_t*>(frames);
+    a.stride = stride;
+    a.W = W;
+    a.pool_start = prm->pool_index_start;
+    a.pool_shift = prm->pool_index_shift;
+    a.mop = prm->max_outstanding_pkts ? prm->max_outstanding_pkts : 1;
+    // Constant header bytes 0..43 (BuildPacket, dpdk_worker_thread_utils.inc:76-126).
+    uint8_t h[44];
+    memset(h, 0, sizeof(h));
+    const uint32_t data_len = (uint32_t)sml_frame_bytes(P);
+    memcpy(h + 0, prm->dst_mac, 6);
+    memcpy(h + 6, prm->src_mac, 6);
+    h[12] = 0x08; h[13] = 0x00;                              // RTE_ETHER_TYPE_IPV4
+    h[14] = 0x45;                                            // version_ihl
+    h[16] = (uint8_t)((data_len - 14) >> 8); h[17] = (uint8_t)(data_len - 14);
+    h[22] = 128;                                             // time_to_live
+    h[23] = 17;                                              // IPPROTO_UDP
+    memcpy(h + 26, &prm->src_ip_be, 4);
+    memcpy(h + 30, &prm->dst_ip_be, 4);
+    memcpy(h + 34, &prm->src_port_be, 2);
+    memcpy(h + 36, &prm->dst_port_be, 2);
+    h[38] = (uint8_t)((data_len - 34) >> 8); h[39] = (uint8_t)(data_len - 34);
+    // udp->dgram_cksum = rte_ipv4_phdr_cksum(ip, ol_flags): raw 16-bit sum of the pseudo header
+    uint8_t psd[12] = {h[26], h[27], h[28], h[29], h[30], h[31], h[32], h[33], 0, 17,
+                       (uint8_t)((data_len - 34) >> 8), (uint8_t)(data_len - 34)};
+    uint32_t sum = 0;
+    for (int i = 0; i < 12; i += 2) sum += (uint32_t)psd[i] | ((uint32_t)psd[i + 1] << 8);
+    sum = (sum & 0xffff) + (sum >> 16);
+    sum = (sum & 0xffff) + (sum >> 16);
+    h[40] = (uint8_t)sum; h[41] = (uint8_t)(sum >> 8);
+    h[42] = (uint8_t)((1 << 4) + (P < 64 ? 0 : P < 128 ? 1 : P < 256 ? 2 : 3));  // job_type_size
+    h[43] = (uint8_t)prm->job_id;                                                // short_job_id
+    memcpy(a.hdr, h, 44);
+    dim3 grid(grid_for_tiles(a.ntiles));
+    hipStream_t st = (hipStream_t)stream;
+    const bool al = aligned16(d_in);
+    if (d_global_exps) { if (al) launch_frames_p<true, true>(P, grid, st, a); else launch_frames_p<false, true>(P, grid, st, a); }
+    else               { if (al) launch_frames_p<true, false>(P, grid, st, a); else launch_frames_p<false, false>(P, grid, st, a); }
+    return launch_check();
+}
+
+sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint64_t stride,
+                                   uint64_t numel, uint32_t P, uint16_t W, uint32_t batch_max,
+                                   uint64_t job_id, int8_t* d_exps, uint64_t* d_state, float* d_out,
+                                   uint64_t* d_counts, void* stream) {
+    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
+    if (W == 0 || batch_max == 0) return SML_ERR_INVALID_ARG;
+    if (num_frames == 0) return SML_OK;
+    if (num_frames >= 0xFFFFFFFEull) return SML_ERR_UNSUPPORTED;
+    if (!frames || !d_state || (numel && (!d_exps || !d_out))) return SML_ERR_INVALID_ARG;
+    if (!aligned4(frames) || !aligned4(d_out) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
+    if (((uintptr_t)d_state & 7u) || (d_counts && ((uintptr_t)d_counts & 7u))) return SML_ERR_ALIGNMENT;
+    RxArgs a;
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    a.frames = static_cast<const uint8_t*>(frames);
+    a.nframes = num_frames;
+    a.stride = stride;
+    a.numel = numel;
+    a.nblocks = sml_num_blocks(numel, P);
+    a.b = a.nblocks < batch_max ? a.nblocks : batch_max;
+    a.state = reinterpret_cast<unsigned long long*>(d_state);
+    a.exps = d_exps;
+    a.out = d_out;
+    a.counts = reinterpret_cast<unsigned long long*>(d_counts);
+    a.W = W;
+    a.job = (uint8_t)job_id;
+    hipStream_t st = (hipStream_t)stream;
+    k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
+    const uint64_t ntiles = (num_frames * P + kRxTileElems - 1) / kRxTileElems;
+    launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
+    k_rx_commit<<<grid_for_vec(a.nblocks + a.b), kBlockThreads, 0, st>>>(a);
+    return launch_check();
+}
+
+}  // extern "C"

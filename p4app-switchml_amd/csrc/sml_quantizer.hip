@@ -1,372 +1,20 @@
-// sml_quantizer.hip — CDNA4 (gfx950) kernels for SwitchML's end-host
-// pre/post-processor and the C-ABI entry points of include/switchml_hip.h.
-//
-// What the reference does per 1 KiB LTU on one CPU thread
-// (client_lib/src/prepostprocessors/cpu_exponent_quantizer_ppp.cc, "ppp.cc"),
-// these kernels do for a whole job slice per launch.  The work is a pure
-// HBM stream (8 B/element for quantize+pack), so the design rules are the
-// streaming ones: 16-B-per-lane coalesced loads/stores (1 KiB per wave
-// instruction), several loads in flight per lane, the per-packet max-|x|
-// reduce in registers + cross-lane (DPP/ds_swizzle via __shfl_xor), no LDS
-// round trip for the data, no MFMA (nothing here is a contraction).
-//
-// Work unit: a "tile" = 1024 consecutive elements of the slice = 4 x f4
-// per lane of one wave64.  Slice u of a tile (u = 0..3) is 256 consecutive
-// elements, lane l holds elements [u*256 + 4l, u*256 + 4l + 4).  A packet of
-// P elements therefore spans P/4 lanes of one slice (P <= 256) or P/256
-// whole slices (P = 512, 1024); every packet lies inside one tile.
-//
-// Arithmetic parity with the VCL=0 reference build:
-//  * exponent: integer max of (bits & 0x7fffffff) with NaN bit patterns
-//    mapped to 0 == the float '>' scan from 0 at ppp.cc:141-146; then
-//    ((m >> 23) & 0xff) - 126 truncated to int8 (ppp.cc:154).
-//  * scale: (float)(double(INT32_MAX) / ((float)W * 2^e)) (ppp.cc:257-258),
-//    computed once per workgroup into an LDS table.
-//  * quantize: roundf(x * s) half away from zero, then the x86-64
-//    cvttss2si-to-64-bit-then-truncate conversion (NaN/inf/|r| >= 2^63 -> 0,
-//    2^31 <= |r| < 2^63 wraps mod 2^32), then bswap (htonl) — ppp.cc:103.
-//  * dequantize: (float)(int32)ntohl(q) / s with IEEE division (ppp.cc:240-241).
-//  * f32 denormals are preserved (the kernels are built without
-//    -fgpu-flush-denormals-to-zero and without fast-math).
-#include <hip/hip_runtime.h>
-
-#include <stdint.h>
-#include <string.h>
-
-#include <atomic>
-
-#include "switchml_hip.h"
+// sml_quantizer.hip — CDNA4 (gfx950) kernels for the planes of SwitchML's
+// end-host pre/post-processor (CpuExponentQuantizerPPP,
+// client_lib/src/prepostprocessors/cpu_exponent_quantizer_ppp.cc = "ppp.cc")
+// and their C-ABI entry points (include/switchml_hip.h): K1 fused exponent +
+// quantize + pack, K2 exponents, K3 quantize with given exponents, K4
+// dequantize, the fused loopback round trip, the word streams (loopback x W,
+// INT32 byteswap), RDMA immediates and the copy probe.  Tile layout, numerics
+// and parity notes: sml_device.h; DPDK frames: sml_frames.hip.
+#include "sml_host.h"
 
 namespace sml {
 
-typedef float f4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-// 16-byte vector with 4-byte alignment: gfx950 runs in unaligned-access mode,
-// so this is still one global_store_dwordx4 (used at the 52-byte frame offset).
-typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
-typedef float f4a __attribute__((ext_vector_type(4), aligned(4)));
-// Read-only views through the scalar data cache (s_load) for wave-uniform
-// metadata (exponent bytes, frame headers, rx state); loads only — nothing in
-// this file writes through the scalar cache.
-typedef const uint32_t __attribute__((address_space(4))) ConstU32;
-typedef const unsigned long long __attribute__((address_space(4))) ConstU64;
-
-__device__ __forceinline__ f4 mkf4(float a, float b, float c, float d) { return f4{a, b, c, d}; }
-__device__ __forceinline__ u4 mku4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) { return u4{a, b, c, d}; }
-
-constexpr int kWave = 64;
-constexpr int kBlockThreads = 256;
-constexpr int kWavesPerBlock = kBlockThreads / kWave;
-constexpr int kU = 4;                          // f4 slices per lane per tile
-constexpr int kTileElems = kWave * 4 * kU;     // 1024
-
-// ----------------------------------------------------------------- numerics
-
-// ppp.cc:257-258.  powf(2, e) is exactly 2^e for every int8 e (2^-127 and
-// 2^-128 are denormal but exact), so ldexp gives the same float; the product
-// with (float)W is a float multiply (overflow -> inf -> scale 0, as on x86);
-// the quotient is a correctly rounded double division, rounded to float.
-__device__ __forceinline__ float scale_of(uint32_t W, int e) {
-    float denom = (float)W * __builtin_ldexpf(1.0f, e);
-    return (float)(2147483647.0 / (double)denom);
-}
-
-// |x| bits with NaN mapped to 0: a NaN never wins the reference's '>' scan.
-__device__ __forceinline__ uint32_t absbits(float x) {
-    uint32_t a = __float_as_uint(x) & 0x7fffffffu;
-    return a > 0x7f800000u ? 0u : a;
-}
-
-__device__ __forceinline__ int exponent_of(uint32_t maxbits) {
-    // ppp.cc:154 computes in int and stores through int8_t*: 129 -> -127, 128 -> -128.
-    return (int)(int8_t)(uint8_t)(((maxbits >> 23) & 0xffu) - 126u);
-}
-
-// gcc/x86-64 lowering of the float -> uint32 conversion at ppp.cc:103:
-// cvttss2si into a 64-bit register, low 32 bits kept.  Needed only for
-// |r| >= 2^31 or NaN (r is already integral); below that it equals v_cvt_i32_f32.
-__device__ __forceinline__ uint32_t x86_wrap(float r) {
-    uint32_t b = __float_as_uint(r);
-    uint32_t E = (b >> 23) & 0xffu;
-    if (E >= 190u) return 0u;                  // |r| >= 2^63, inf, NaN -> 0x8000...0 -> low 0
-    uint32_t m = (b & 0x7fffffu) | 0x800000u;
-    uint32_t sh = E - 150u;                    // >= 8 here
-    uint32_t low = sh < 32u ? (m << sh) : 0u;
-    return (b >> 31) ? (0u - low) : low;
-}
-
-// Quantize 4 consecutive elements with one scale (host byte order result).
-// RNE_BODY: lanes [0, body) use the VCL=1 roundi() semantics (RNE, out of
-// range / NaN -> 0x80000000); the rest use the VCL=0 scalar path.  With
-// RNE == false every element takes the scalar path.
-template <bool RNE>
-__device__ __forceinline__ u4 quantize4(f4 x, float s, uint64_t idx, uint64_t body) {
-    const float p[4] = {x.x * s, x.y * s, x.z * s, x.w * s};
-    uint32_t q[4];
-    bool wide = false;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        if (RNE && idx + j < body) {
-            q[j] = fabsf(p[j]) < 0x1p31f ? (uint32_t)(int32_t)__builtin_rintf(p[j]) : 0x80000000u;
-        } else {
-            float r = __builtin_roundf(p[j]);      // half away from zero, like std::round(float)
-            q[j] = (uint32_t)(int32_t)r;           // exact whenever |r| < 2^31
-            wide |= !(fabsf(r) < 0x1p31f);
-        }
-    }
-    if (__builtin_expect(wide, 0)) {               // rare: out-of-range / NaN / inf products
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (RNE && idx + j < body) continue;
-            float r = __builtin_roundf(p[j]);
-            if (!(fabsf(r) < 0x1p31f)) q[j] = x86_wrap(r);
-        }
-    }
-    return mku4(q[0], q[1], q[2], q[3]);
-}
-
-__device__ __forceinline__ float dequantize1(uint32_t q_host_order, float s) {
-    return (float)(int32_t)q_host_order / s;
-}
-
-__device__ __forceinline__ uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
-
-// ------------------------------------------------------------- memory ops
-
-// ALIGNED = false: slices that start at any 4-byte offset (FIFO slices,
-// fifo_scheduler.cc:93-109).  gfx950 runs in unaligned mode and moves 4-byte
-// aligned 16-B accesses at the full stream rate (hbm_probe: +4 B offset
-// loads 7.15 TB/s, stores 7.20 TB/s vs 7.23 aligned), so both forms are one
-// dwordx4 per lane.
-template <bool ALIGNED>
-__device__ __forceinline__ f4 load4(const float* p) {
-    if constexpr (ALIGNED) {
-        return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
-    } else {
-        const f4a v = __builtin_nontemporal_load(reinterpret_cast<const f4a*>(p));
-        return mkf4(v.x, v.y, v.z, v.w);
-    }
-}
-
-__device__ __forceinline__ f4 load4_guarded(const float* p, uint64_t idx, uint64_t numel) {
-    f4 v;
-    v.x = idx + 0 < numel ? p[0] : 0.0f;
-    v.y = idx + 1 < numel ? p[1] : 0.0f;
-    v.z = idx + 2 < numel ? p[2] : 0.0f;
-    v.w = idx + 3 < numel ? p[3] : 0.0f;
-    return v;
-}
-
-template <bool ALIGNED>
-__device__ __forceinline__ void store4(float* p, f4 v) {
-    if constexpr (ALIGNED) {
-        *reinterpret_cast<f4*>(p) = v;   // default policy: faster than nt stores here
-    } else {
-        *reinterpret_cast<f4a*>(p) = f4a{v.x, v.y, v.z, v.w};
-    }
-}
-
-__device__ __forceinline__ void store4_guarded(float* p, f4 v, uint64_t idx, uint64_t numel) {
-    if (idx + 0 < numel) p[0] = v.x;
-    if (idx + 1 < numel) p[1] = v.y;
-    if (idx + 2 < numel) p[2] = v.z;
-    if (idx + 3 < numel) p[3] = v.w;
-}
-
-// Payload stores keep the default cache policy: measured 9 % faster than
-// non-temporal stores on the 256 MiB bucket (loads stay non-temporal,
-// which is 15 % faster than default-policy loads) — profiles/r01/ab*.json.
-__device__ __forceinline__ void store_payload(u4* dst, u4 q) { *dst = q; }
-
-// ---------------------------------------------------- per-packet reductions
-
-// Max of `m` over the P/4 lanes of this lane's packet (P <= 256).
-// Inside each 16-lane row: four DPP steps (quad_perm xor 1, quad_perm xor 2,
-// row_half_mirror, row_mirror) leave the row max in every lane of the row,
-// with no LDS traffic.  Across rows: v_readlane of lanes 0/16/32/48 into
-// SGPRs — for P >= 256 the packet max is then wave-uniform (scalar).
-__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
-
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
-}
-
-template <int P>
-__device__ __forceinline__ uint32_t group_max(uint32_t m) {
-    static_assert(P == 64 || P == 128 || P == 256, "row-based reduce covers 16..64 lanes");
-    m = umax(m, dpp<0xB1>(m));    // quad_perm [1,0,3,2]
-    m = umax(m, dpp<0x4E>(m));    // quad_perm [2,3,0,1]
-    m = umax(m, dpp<0x141>(m));   // row_half_mirror
-    m = umax(m, dpp<0x140>(m));   // row_mirror
-    if constexpr (P == 64) return m;
-    const uint32_t r0 = __builtin_amdgcn_readlane(m, 0), r1 = __builtin_amdgcn_readlane(m, 16);
-    const uint32_t r2 = __builtin_amdgcn_readlane(m, 32), r3 = __builtin_amdgcn_readlane(m, 48);
-    if constexpr (P == 128) return (threadIdx.x & 32) ? umax(r2, r3) : umax(r0, r1);
-    return umax(umax(r0, r1), umax(r2, r3));
-}
-
-__device__ __forceinline__ uint32_t max4(f4 v) {
-    uint32_t a = absbits(v.x), b = absbits(v.y), c = absbits(v.z), d = absbits(v.w);
-    a = a > b ? a : b;
-    c = c > d ? c : d;
-    return a > c ? a : c;
-}
-
-// Exponents e[u] of the packet each lane's slice u belongs to.
-template <int P>
-__device__ __forceinline__ void tile_exponents(const f4 (&v)[kU], int (&e)[kU]) {
-    uint32_t m[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) m[u] = max4(v[u]);
-    if constexpr (P <= 256) {
-#pragma unroll
-        for (int u = 0; u < kU; u++) e[u] = exponent_of(group_max<P>(m[u]));
-    } else if constexpr (P == 512) {
-        uint32_t a = group_max<256>(m[0] > m[1] ? m[0] : m[1]);
-        uint32_t b = group_max<256>(m[2] > m[3] ? m[2] : m[3]);
-        e[0] = e[1] = exponent_of(a);
-        e[2] = e[3] = exponent_of(b);
-    } else {
-        static_assert(P == 1024, "packet_numel must be 64..1024, power of two");
-        uint32_t a = m[0] > m[1] ? m[0] : m[1];
-        uint32_t b = m[2] > m[3] ? m[2] : m[3];
-        uint32_t t = group_max<256>(a > b ? a : b);
-        e[0] = e[1] = e[2] = e[3] = exponent_of(t);
-    }
-}
-
-// The lane that owns packet `pkt` of slice u writes its exponent byte.
-template <int P>
-__device__ __forceinline__ void store_exponents(int8_t* exps_out, uint64_t tile_base, int lane,
-                                                const int (&e)[kU], uint64_t nblocks) {
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-        bool leader;
-        if constexpr (P <= 256) leader = (lane % (P / 4)) == 0;
-        else leader = lane == 0 && (u % (P / 256)) == 0;
-        uint64_t pkt = (tile_base + (uint64_t)(u * kWave + lane) * 4) / P;
-        if (leader && pkt < nblocks) exps_out[pkt] = (int8_t)e[u];
-    }
-}
-
-// A full tile's kPk = 1024 / P exponent bytes are contiguous in exps_out:
-// lane 0 gathers them (v_readlane of each packet's first lane) and writes them
-// with one 1/2/4/8/16-byte store — per-packet byte stores cost ~10 % on the
-// 256 MiB bucket (partial-line writes).  dst must be kPk-byte aligned.
-template <int P>
-__device__ __forceinline__ void store_tile_exponents(int8_t* dst, int lane, const int (&e)[kU]) {
-    constexpr int kPk = kTileElems / P;
-    constexpr int kLanesPerPk = P / 4 < kWave ? P / 4 : kWave;
-    constexpr int kWords = (kPk + 3) / 4;
-    uint32_t w[kWords];
-#pragma unroll
-    for (int i = 0; i < kWords; i++) w[i] = 0;
-#pragma unroll
-    for (int j = 0; j < kPk; j++) {
-        const int u = (j * P) / 256;
-        uint32_t ej = 0;
-#pragma unroll
-        for (int uu = 0; uu < kU; uu++)
-            if (uu == u) ej = (uint32_t)__builtin_amdgcn_readlane(e[uu], (j * kLanesPerPk) % kWave);
-        w[j / 4] |= (ej & 0xffu) << (8 * (j % 4));
-    }
-    if (lane != 0) return;
-    if constexpr (kPk == 16) *reinterpret_cast<u4*>(dst) = mku4(w[0], w[1], w[2], w[3]);
-    else if constexpr (kPk == 8) *reinterpret_cast<u2*>(dst) = u2{w[0], w[1]};
-    else if constexpr (kPk == 4) *reinterpret_cast<uint32_t*>(dst) = w[0];
-    else if constexpr (kPk == 2) *reinterpret_cast<uint16_t*>(dst) = (uint16_t)w[0];
-    else *dst = (int8_t)w[0];
-}
-
-// Exponent byte of each lane's packet in slice u of a tile, with one
-// wave-uniform scalar load per slice (base must be wave-uniform).  A slice
-// holds 4, 2 or 1 packets (P = 64, 128, >= 256); their bytes lie in one
-// aligned dword whenever exps is 4-byte aligned, and always for P > 256.
-template <int P>
-__device__ __forceinline__ bool slice_exps_scalar_ok(const int8_t* exps) {
-    return P > 256 || (reinterpret_cast<uintptr_t>(exps) & 3u) == 0;
-}
-template <int P>
-__device__ __forceinline__ uint32_t slice_exponent_byte(const int8_t* exps, uint64_t base, int u, int lane) {
-    const uintptr_t e0 = reinterpret_cast<uintptr_t>(exps);
-    const uintptr_t first = e0 + base / P + (uint64_t)(u * 256) / P;
-    const uint32_t word = *reinterpret_cast<ConstU32*>(first & ~(uintptr_t)3);
-    const uintptr_t mine = e0 + (base + (uint64_t)(u * kWave + lane) * 4) / P;
-    return (word >> (8 * (mine & 3u))) & 0xffu;
-}
-
-// scale_of for W = 2^k without the double division: 2147483647 / 2^(e+k)
-// rounds to 2^(31-e-k) (normal range for every int8 e and k <= 16), +inf when
-// 31-e-k > 127, and 0 when W * 2^e overflows float (e + k >= 128).
-__device__ __forceinline__ float scale_of_pow2(uint32_t log2W, int e) {
-    const int m = e + (int)log2W;
-    if (m >= 128) return 0.0f;
-    const int x = 31 - m;                      // result 2^x
-    if (x > 127) return __builtin_huge_valf();
-    return __uint_as_float((uint32_t)(x + 127) << 23);
-}
-
-// The scale every kernel uses (power-of-two W takes the division-free form).
-__device__ __forceinline__ float scale_for(uint32_t W, int e) {
-    return (W & (W - 1)) == 0 ? scale_of_pow2(31 - __builtin_clz(W), e) : scale_of(W, e);
-}
-
-// Per-workgroup scale table, lut[(uint8_t)e], built once per launch-block.
-__device__ __forceinline__ void build_lut(float* lut, uint32_t W) {
-    lut[threadIdx.x] = scale_for(W, (int)(int8_t)(uint8_t)threadIdx.x);
-    __syncthreads();
-}
+thread_local char g_last_error[256] = "";
+std::atomic<uint32_t> g_grid_limit{0};
+std::atomic<uint32_t> g_xcd_chunk{64};
 
 // -------------------------------------------------------------- kernels
-
-// Workgroup -> data order for the HBM streams.  The dispatcher places
-// workgroup b on XCD b % 8; with chunk C > 0 the first (nb / 8C) * 8C
-// workgroups are permuted so that each XCD sweeps runs of C consecutive
-// workgroups' data (C x 16 KiB with 4 tiles per workgroup) instead of every
-// 8th one; the tail keeps its order (a bijection on [0, nb) either way).
-// Measured on the 256 MiB bucket: C = 64 moves a 1:1 read:write stream
-// 4 % faster than the plain order (profiles/r01/ab5_xcd_chunk.json, hbm_probe_*.json).
-// The wave's index in its workgroup, as a wave-uniform (SGPR) value, so that
-// tile bases and per-tile metadata addresses are scalar.
-__device__ __forceinline__ uint32_t wave_index() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
-
-__device__ __forceinline__ uint64_t xcd_block(uint32_t C) {
-    const uint64_t b = blockIdx.x;
-    if (C == 0) return b;
-    const uint64_t span = 8ull * C, full = (uint64_t)gridDim.x / span * span;
-    if (b >= full) return b;
-    const uint64_t r = b / 8;
-    return (r / C) * span + (b % 8) * C + r % C;
-}
-
-
-struct QuantArgs {
-    const float* in;
-    uint64_t numel;
-    uint64_t nblocks;       // B
-    uint64_t ntiles;        // ceil(B*P / 1024)
-    const int8_t* gexp;     // global exponents (K3) or nullptr (K1)
-    u4* payload;          // B*P words, 16-B aligned (nullptr: exponents only)
-    int8_t* exps_out;       // nullable
-    uint32_t W;
-    uint32_t xcd;           // xcd_block chunk (0 = plain order)
-};
-
-template <bool ALIGNED>
-__device__ __forceinline__ void load_tile(const QuantArgs& a, uint64_t base, int lane, f4 (&v)[kU]) {
-    if (base + kTileElems <= a.numel) {
-#pragma unroll
-        for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
-    } else {
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-            v[u] = load4_guarded(a.in + idx, idx, a.numel);
-        }
-    }
-}
 
 // Exponents, quantize and pack of one loaded tile.
 template <int P, bool GLOBAL, bool BE, bool RNE>
@@ -434,333 +82,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
 #pragma unroll
         for (int k = 0; k < TPW; k++)
             if (k == 0 || t + k < a.ntiles) quant_tile<P, GLOBAL, BE, RNE>(a, (t + k) * kTileElems, lane, v[k], lut);
-    }
-}
-
-// ---------------------------------------------------------- DPDK frames
-
-struct FrameArgs {
-    const float* in;
-    uint64_t numel;
-    uint64_t nblocks;       // B
-    uint64_t ntiles;        // ceil(B*P / 1024)
-    uint64_t b;             // extra-batch size = min(batch_max, B)
-    const int8_t* gexp;     // global exponents or nullptr
-    uint8_t* frames;        // B + b frames, 4-byte aligned
-    uint64_t stride;        // bytes between frames, multiple of 4
-    uint32_t W;
-    uint32_t xcd;           // xcd_block chunk (0 = plain order)
-    uint32_t pool_start, pool_shift, mop;
-    uint32_t hdr[11];       // frame bytes 0..43: Eth, IPv4, UDP, job_type_size, short_job_id
-};
-
-// PktId2PoolIndex, dpdk_worker_thread_utils.inc:42-52.
-__device__ __forceinline__ uint32_t pool_index(uint64_t p, const FrameArgs& a) {
-    const uint32_t i = (uint32_t)((p + a.pool_shift) % (2ull * a.mop));
-    return i < a.mop ? ((a.pool_start + i) & 0xffffu) : (((a.pool_start + (i - a.mop)) | 0x8000u) & 0xffffu);
-}
-
-// Lanes 0..12 write the 52 header bytes of frame p (one dword each):
-// dwords 0-10 constant, 11 = pkt_id (host order), 12 = pool index (BE16),
-// exponent byte, zero byte.  (Extra-batch frames; the bulk of the headers is
-// written lane-parallel by k_quantize_frames.)
-__device__ __forceinline__ void write_frame_header(const FrameArgs& a, uint64_t p, int lane, uint32_t exp_byte) {
-    if (lane > 12) return;
-    uint32_t dw = a.hdr[0];
-#pragma unroll
-    for (int i = 1; i < 11; i++) dw = lane == i ? a.hdr[i] : dw;
-    if (lane == 11) dw = (uint32_t)p;
-    if (lane == 12) {
-        const uint32_t pool = pool_index(p, a);
-        dw = (pool >> 8) | ((pool & 0xffu) << 8) | ((exp_byte & 0xffu) << 16);
-    }
-    *reinterpret_cast<uint32_t*>(a.frames + p * a.stride + 4 * lane) = dw;
-}
-
-// Fused quantize + pack into DPDK frames (BuildPacket + PreprocessSingle for
-// every packet of the slice, dpdk_worker_thread_utils.inc:67-135 + ppp.cc:69-156).
-//
-// Frame f carries the exponent of block f (f < B) in header dword 12 (pool
-// index BE16, exponent byte, zero byte) and the payload of block f - b.  The
-// wave of block k therefore writes:
-//  * frame k + b: header dwords 0-11 and the payload — one wave writes all
-//    of the frame but dword 12 (and dword 12 too once k + b >= B: those
-//    frames carry exponent 0);
-//  * dword 12 of frame k (k >= b), or the whole of extra-batch frame k
-//    (k < b: header with this exponent, zero payload).
-// One dword store instruction covers 4 frames: lane l < 48 writes dword
-// l % 12 of payload frame l / 12, lanes 48-51 write dword 12 of the 4
-// exponent frames.  Constant dwords are picked once per wave; the pool index
-// (PktId2PoolIndex) costs one 64-bit modulo per tile.
-__device__ __forceinline__ uint32_t pool_dword(const FrameArgs& a, uint32_t i, uint32_t exp_byte) {
-    const uint32_t pool = i < a.mop ? ((a.pool_start + i) & 0xffffu) : (((a.pool_start + (i - a.mop)) | 0x8000u) & 0xffffu);
-    return (pool >> 8) | ((pool & 0xffu) << 8) | ((exp_byte & 0xffu) << 16);
-}
-
-template <int P, bool ALIGNED, bool GLOBAL>
-__global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) {
-    __shared__ float lut[256];
-    build_lut(lut, a.W);
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t padded = a.nblocks * P;
-    constexpr int kPk = kTileElems / P;                   // packets per tile
-    constexpr int kLanesPerPk = P / 4 < kWave ? P / 4 : kWave;
-    const int hd = lane % 12;                              // header dword of lanes 0..47
-    const int hj = lane < 48 ? lane / 12 : lane - 48;      // frame (of 4) of lanes 0..51
-    uint32_t hconst = a.hdr[0];
-#pragma unroll
-    for (int i = 1; i < 11; i++) hconst = hd == i ? a.hdr[i] : hconst;
-    const uint32_t m2 = 2u * a.mop;
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
-        const uint64_t base = t * kTileElems;
-        const uint64_t pk0 = base / P;                     // first block of the tile
-        QuantArgs qa;                                      // reuse the K1 tile loader
-        qa.in = a.in;
-        qa.numel = a.numel;
-        f4 v[kU];
-        load_tile<ALIGNED>(qa, base, lane, v);
-        int eloc[kU];
-        tile_exponents<P>(v, eloc);
-        // exponent of packet j of the tile: slice j*P/256, lane (j*P/4) % 64
-        uint32_t ej[kPk];
-#pragma unroll
-        for (int j = 0; j < kPk; j++) {
-            const int u = (j * P) / 256;
-            ej[j] = 0;
-#pragma unroll
-            for (int uu = 0; uu < kU; uu++)
-                if (uu == u) ej[j] = (uint32_t)__builtin_amdgcn_readlane(eloc[uu], (j * kLanesPerPk) % kWave);
-        }
-        const uint32_t r = (uint32_t)((pk0 + a.pool_shift) % m2);   // pool slot of frame pk0
-        const bool extra = pk0 < a.b;                               // wave-uniform, first b / kPk tiles
-#pragma unroll
-        for (int j0 = 0; j0 < kPk; j0 += 4) {
-            const int j = j0 + hj;
-            if (lane < 48) {
-                if (j < kPk && pk0 + j < a.nblocks) {
-                    const uint64_t f = pk0 + j + a.b;
-                    *reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 4 * hd) = hd == 11 ? (uint32_t)f : hconst;
-                }
-            } else if (lane < 52 && !extra) {
-                if (j < kPk && pk0 + j < a.nblocks) {
-                    uint32_t e = 0;
-#pragma unroll
-                    for (int jj = 0; jj < kPk; jj++) e = j == jj ? ej[jj] : e;
-                    *reinterpret_cast<uint32_t*>(a.frames + (pk0 + j) * a.stride + 48) = pool_dword(a, (r + (uint32_t)j) % m2, e);
-                }
-            }
-        }
-        if (__builtin_expect(pk0 + kPk + a.b > a.nblocks, 0)) {
-            // tail: payload frames at or past B carry exponent 0; their dword 12 is ours
-            if (lane < kPk && pk0 + lane < a.nblocks && pk0 + lane + a.b >= a.nblocks) {
-                const uint64_t f = pk0 + lane + a.b;
-                *reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 48) =
-                    pool_dword(a, (uint32_t)((f + a.pool_shift) % m2), 0u);
-            }
-        }
-        if (__builtin_expect(extra, 0)) {
-            // extra-batch frames: header with this tile's exponent, zero payload; all ours
-#pragma unroll
-            for (int j = 0; j < kPk; j++) {
-                const uint64_t pk = pk0 + j;
-                if (pk >= a.nblocks) break;
-                if (pk < a.b) {
-                    write_frame_header(a, pk, lane, ej[j]);
-                    uint32_t* pl = reinterpret_cast<uint32_t*>(a.frames + pk * a.stride + 52);
-                    for (int i = lane; i < P / 4; i += kWave) *reinterpret_cast<u4a*>(pl + 4 * i) = u4a{0u, 0u, 0u, 0u};
-                } else if (lane == 0) {
-                    *reinterpret_cast<uint32_t*>(a.frames + pk * a.stride + 48) =
-                        pool_dword(a, (uint32_t)((pk + a.pool_shift) % m2), ej[j]);
-                }
-            }
-        }
-        // payloads
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-            if (idx >= padded) continue;
-            const uint64_t k = idx / P;
-            int e = eloc[u];
-            if constexpr (GLOBAL) e = a.gexp[k];
-            const u4 q = quantize4<false>(v[u], lut[(uint8_t)e], idx, 0);
-            uint32_t* dst = reinterpret_cast<uint32_t*>(a.frames + (k + a.b) * a.stride + 52) + (idx - k * P);
-            *reinterpret_cast<u4a*>(dst) = u4a{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)};
-        }
-    }
-}
-
-// ------------------------------------------------- DPDK frames, receive side
-//
-// The rx bitmap of DpdkWorkerThread (dpdk_worker_thread.cc:316-342) becomes a
-// per-slice 64-bit state word per packet id: high half 0 = not received,
-// kRxDone = received in an earlier call, otherwise the claim tag of the frame
-// that won it in the current call (larger tag = earlier frame, so a 64-bit
-// atomicMax picks the first copy); low byte = that frame's exponent byte, so
-// the winner's exponent travels with the claim (PostprocessSingle's
-// scaling_factors_[pkt_id], ppp.cc:254-260) and needs no separate pass.
-constexpr uint32_t kRxDone = 0xFFFFFFFFu;
-__device__ __forceinline__ uint32_t rx_tag(uint64_t f) { return 0xFFFFFFFEu - (uint32_t)f; }
-
-struct RxArgs {
-    const uint8_t* frames;
-    uint64_t nframes;
-    uint64_t stride;
-    uint64_t numel;
-    uint64_t nblocks;           // B
-    uint64_t b;                 // extra batch
-    unsigned long long* state;  // [B + b]
-    int8_t* exps;               // [B]
-    float* out;
-    unsigned long long* counts; // {accepted, discarded} or nullptr
-    uint32_t W;
-    uint32_t xcd;           // xcd_block chunk (0 = plain order)
-    uint32_t job;               // (uint8_t)job_id
-};
-
-// Header dwords 10..12 of frame f: short_job_id = byte 43, pkt_id = bytes
-// 44-47 (host order), exponent = byte 50.
-struct RxHdr {
-    uint32_t pid;
-    uint32_t exp;
-    bool ok;                    // this job, pkt_id in range
-};
-
-__device__ __forceinline__ RxHdr rx_header(const RxArgs& a, uint64_t f) {
-    const uint32_t* h = reinterpret_cast<const uint32_t*>(a.frames + f * a.stride + 40);
-    const uint32_t d10 = h[0], d11 = h[1], d12 = h[2];
-    RxHdr r;
-    r.pid = d11;
-    r.exp = (d12 >> 16) & 0xffu;
-    r.ok = (d10 >> 24) == a.job && (uint64_t)d11 < a.nblocks + a.b;
-    return r;
-}
-
-// Pass 1, thread per frame: frames of another job, out-of-range or already
-// received pkt_ids are discarded; the others claim their pkt_id.  Counting:
-// accepted = frames - discarded, so block 0 adds the frame count once and only
-// workgroups that saw a discard touch the counters (same-address atomics from
-// every workgroup serialize in one L2 channel: ~40 us at 262 k frames).
-__global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
-    __shared__ uint32_t disc;
-    if (threadIdx.x == 0) disc = 0;
-    __syncthreads();
-    uint32_t mine = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
-    for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
-        const RxHdr h = rx_header(a, f);
-        if (!h.ok) { mine++; continue; }
-        const unsigned long long v = ((unsigned long long)rx_tag(f) << 32) | h.exp;
-        if (atomicMax(a.state + h.pid, v) != 0ull) mine++;          // duplicate or received earlier
-    }
-    if (a.counts) {
-        if (mine) atomicAdd(&disc, mine);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long acc = blockIdx.x == 0 ? (unsigned long long)a.nframes : 0ull;
-            acc -= disc;                                                 // mod 2^64
-            if (acc) atomicAdd(a.counts + 0, acc);
-            if (disc) atomicAdd(a.counts + 1, (unsigned long long)disc);
-        }
-    }
-}
-
-// Pass 2: PostprocessSingle for every winning frame, 1024 payload elements per
-// wave (1024 / P frames; lane-chunk c = u*64 + lane is 16 bytes of frame
-// c / (P/4)).  The payload loads are issued first, independent of the header;
-// a frame is the winner of its pkt_id iff state[pkt_id] holds its claim tag;
-// the exponent of block k is the low byte of state[k], whoever holds it (a
-// winner of this call or kRxDone).  Pass 3 retires the winners.
-constexpr int kRxU = 4;                        // 16-B chunks per lane per iteration
-constexpr int kRxTileElems = kRxU * kWave * 4;
-
-template <int P>
-__global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
-    __shared__ float lut[256];
-    build_lut(lut, a.W);
-    constexpr int kChunksPerFrame = P / 4;     // 16-B chunks per payload
-    constexpr int kFramesPerTile = kRxTileElems / P;
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t ntiles = (a.nframes + kFramesPerTile - 1) / kFramesPerTile;
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < ntiles; t += nwaves) {
-        u4a w[kRxU];
-        RxHdr h[kRxU];
-        float s[kRxU];
-        if constexpr (kChunksPerFrame >= kWave) {
-            // P >= 256: slice u of the tile lies in one frame, so its header and
-            // state words are wave-uniform: scalar loads (no vector-memory
-            // instructions for the per-frame metadata; pass 2 writes neither)
-#pragma unroll
-            for (int u = 0; u < kRxU; u++) {
-                const uint64_t f = t * kFramesPerTile + (u * kWave) / kChunksPerFrame;
-                if (f < a.nframes)
-                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
-                        a.frames + f * a.stride + 52 + 16ull * ((u * kWave + lane) % kChunksPerFrame)));
-            }
-            const ConstU32* hdr = reinterpret_cast<const ConstU32*>(reinterpret_cast<uintptr_t>(a.frames));
-            const ConstU64* state = reinterpret_cast<const ConstU64*>(reinterpret_cast<uintptr_t>(a.state));
-#pragma unroll
-            for (int u = 0; u < kRxU; u++) {
-                const uint64_t f = t * kFramesPerTile + (u * kWave) / kChunksPerFrame;
-                h[u] = RxHdr{0u, 0u, false};
-                s[u] = 0.0f;
-                if (f >= a.nframes) continue;
-                const uint64_t hw = (f * a.stride + 40) / 4;
-                const uint32_t d10 = hdr[hw], d11 = hdr[hw + 1], d12 = hdr[hw + 2];
-                h[u].pid = d11;
-                h[u].exp = (d12 >> 16) & 0xffu;
-                h[u].ok = (d10 >> 24) == a.job && (uint64_t)d11 < a.nblocks + a.b &&
-                          (uint32_t)(state[d11] >> 32) == rx_tag(f);
-                if (h[u].ok && d11 >= a.b) s[u] = lut[(uint32_t)state[d11 - a.b] & 0xffu];
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kRxU; u++) {
-                const int c = u * kWave + lane;
-                const uint64_t f = t * kFramesPerTile + c / kChunksPerFrame;
-                h[u].ok = false;
-                if (f >= a.nframes) continue;
-                // non-temporal: 25 % faster than default-policy loads for this stream (hbm_probe)
-                w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(a.frames + f * a.stride + 52 +
-                                                                               16ull * (c % kChunksPerFrame)));
-                h[u] = rx_header(a, f);
-            }
-#pragma unroll
-            for (int u = 0; u < kRxU; u++) {
-                if (!h[u].ok) continue;
-                const uint64_t f = t * kFramesPerTile + (u * kWave + lane) / kChunksPerFrame;
-                h[u].ok = (uint32_t)(a.state[h[u].pid] >> 32) == rx_tag(f);
-                s[u] = h[u].pid >= a.b ? lut[(uint32_t)a.state[h[u].pid - a.b] & 0xffu] : 0.0f;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kRxU; u++) {
-            if (!h[u].ok || h[u].pid < a.b) continue;
-            const uint64_t off = (uint64_t)(h[u].pid - a.b) * P + 4ull * ((u * kWave + lane) % kChunksPerFrame);
-            if (off >= a.numel) continue;
-            const f4 o = mkf4(dequantize1(bswap(w[u].x), s[u]), dequantize1(bswap(w[u].y), s[u]),
-                              dequantize1(bswap(w[u].z), s[u]), dequantize1(bswap(w[u].w), s[u]));
-            float* p = a.out + off;
-            if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o;
-            else store4_guarded(p, o, 0, a.numel - off);
-        }
-    }
-}
-
-// Pass 3, thread per pkt_id: the winners of this call retire their pkt_id
-// (state -> kRxDone, keeping the exponent byte) and publish the exponent to
-// exps[pkt_id] — one coalesced sweep instead of two scattered 1-8 byte
-// stores per frame inside pass 2 (partial-line stores from many waves).
-__global__ __launch_bounds__(kBlockThreads) void k_rx_commit(RxArgs a) {
-    const uint64_t n = a.nblocks + a.b;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
-    for (uint64_t k = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; k < n; k += stride) {
-        const unsigned long long st = a.state[k];
-        const uint32_t hi = (uint32_t)(st >> 32);
-        if (hi == 0u || hi == kRxDone) continue;
-        a.state[k] = ((unsigned long long)kRxDone << 32) | (st & 0xffull);
-        if (k < a.nblocks) a.exps[k] = (int8_t)(st & 0xffull);
     }
 }
 
@@ -967,43 +288,6 @@ __global__ void k_scale_lut(float* lut, uint32_t W) {
 
 // ------------------------------------------------------------ host side
 
-static thread_local char g_last_error[256] = "";
-static std::atomic<uint32_t> g_grid_limit{0};
-static std::atomic<uint32_t> g_xcd_chunk{64};
-
-static sml_status_t hip_check(hipError_t err) {
-    if (err == hipSuccess) return SML_OK;
-    strncpy(g_last_error, hipGetErrorString(err), sizeof(g_last_error) - 1);
-    return SML_ERR_HIP;
-}
-
-static sml_status_t launch_check() { return hip_check(hipGetLastError()); }
-
-static inline bool valid_packet(uint32_t P) {
-    return P == 64 || P == 128 || P == 256 || P == 512 || P == 1024;
-}
-
-static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
-static inline bool aligned4(const void* p) { return ((uintptr_t)p & 3u) == 0; }
-
-static inline uint32_t grid_for_tiles(uint64_t ntiles) {
-    uint64_t g = (ntiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (g == 0) g = 1;
-    const uint32_t lim = g_grid_limit.load(std::memory_order_relaxed);
-    if (lim && g > lim) g = lim;
-    if (g > 0x7fffffffull) g = 0x7fffffffull;
-    return (uint32_t)g;
-}
-
-static inline uint32_t grid_for_vec(uint64_t nvec) {
-    uint64_t g = (nvec + kBlockThreads - 1) / kBlockThreads;
-    const uint32_t lim = g_grid_limit.load(std::memory_order_relaxed);
-    uint64_t cap = lim ? lim : 8192;
-    if (g > cap) g = cap;
-    if (g == 0) g = 1;
-    return (uint32_t)g;
-}
-
 // Dispatch tables: runtime (P, alignment, mode) -> template instance.
 template <bool ALIGNED, bool GLOBAL, bool BE, bool RNE, int TPW>
 static void launch_quant_t(uint32_t P, dim3 grid, hipStream_t st, const QuantArgs& a) {
@@ -1066,27 +350,6 @@ template <bool ALIGNED>
 static void launch_rt_a(bool be, bool rne, uint32_t P, dim3 g, hipStream_t st, const RoundTripArgs& a) {
     if (be) { if (rne) launch_rt_p<ALIGNED, true, true>(P, g, st, a); else launch_rt_p<ALIGNED, true, false>(P, g, st, a); }
     else    { if (rne) launch_rt_p<ALIGNED, false, true>(P, g, st, a); else launch_rt_p<ALIGNED, false, false>(P, g, st, a); }
-}
-
-template <bool ALIGNED, bool GLOBAL>
-static void launch_frames_p(uint32_t P, dim3 grid, hipStream_t st, const FrameArgs& a) {
-    switch (P) {
-        case 64:   k_quantize_frames<64, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_quantize_frames<128, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_quantize_frames<256, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_quantize_frames<512, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_quantize_frames<1024, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
-    }
-}
-
-static void launch_rx_apply(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
-    switch (P) {
-        case 64:   k_rx_apply<64><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_rx_apply<128><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_rx_apply<256><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_rx_apply<512><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_rx_apply<1024><<<grid, kBlockThreads, 0, st>>>(a); break;
-    }
 }
 
 }  // namespace sml
@@ -1249,98 +512,6 @@ sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t B, uint32_t batch_max, 
     if (!d_exps || !d_imm || batch_max == 0) return SML_ERR_INVALID_ARG;
     const uint64_t total = B + (B < batch_max ? B : batch_max);
     k_rdma_imm<<<grid_for_vec(total), kBlockThreads, 0, (hipStream_t)stream>>>(d_exps, B, total, d_imm);
-    return launch_check();
-}
-
-uint64_t sml_frame_bytes(uint32_t packet_numel) { return 52ull + 4ull * packet_numel; }
-
-sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_t P, uint16_t W,
-                                      const int8_t* d_global_exps, uint32_t batch_max,
-                                      const sml_frame_params* prm, void* frames, uint64_t stride, void* stream) {
-    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
-    if (W == 0 || !prm || batch_max == 0) return SML_ERR_INVALID_ARG;
-    if (numel == 0) return SML_OK;
-    if (!d_in || !aligned4(d_in) || !frames) return SML_ERR_INVALID_ARG;
-    if (!aligned4(frames) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
-    FrameArgs a;
-    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
-    a.in = d_in;
-    a.numel = numel;
-    a.nblocks = sml_num_blocks(numel, P);
-    a.ntiles = (a.nblocks * P + kTileElems - 1) / kTileElems;
-    a.b = a.nblocks < batch_max ? a.nblocks : batch_max;
-    a.gexp = d_global_exps;
-    a.frames = static_cast<uint8_t*>(frames);
-    a.stride = stride;
-    a.W = W;
-    a.pool_start = prm->pool_index_start;
-    a.pool_shift = prm->pool_index_shift;
-    a.mop = prm->max_outstanding_pkts ? prm->max_outstanding_pkts : 1;
-    // Constant header bytes 0..43 (BuildPacket, dpdk_worker_thread_utils.inc:76-126).
-    uint8_t h[44];
-    memset(h, 0, sizeof(h));
-    const uint32_t data_len = (uint32_t)sml_frame_bytes(P);
-    memcpy(h + 0, prm->dst_mac, 6);
-    memcpy(h + 6, prm->src_mac, 6);
-    h[12] = 0x08; h[13] = 0x00;                              // RTE_ETHER_TYPE_IPV4
-    h[14] = 0x45;                                            // version_ihl
-    h[16] = (uint8_t)((data_len - 14) >> 8); h[17] = (uint8_t)(data_len - 14);
-    h[22] = 128;                                             // time_to_live
-    h[23] = 17;                                              // IPPROTO_UDP
-    memcpy(h + 26, &prm->src_ip_be, 4);
-    memcpy(h + 30, &prm->dst_ip_be, 4);
-    memcpy(h + 34, &prm->src_port_be, 2);
-    memcpy(h + 36, &prm->dst_port_be, 2);
-    h[38] = (uint8_t)((data_len - 34) >> 8); h[39] = (uint8_t)(data_len - 34);
-    // udp->dgram_cksum = rte_ipv4_phdr_cksum(ip, ol_flags): raw 16-bit sum of the pseudo header
-    uint8_t psd[12] = {h[26], h[27], h[28], h[29], h[30], h[31], h[32], h[33], 0, 17,
-                       (uint8_t)((data_len - 34) >> 8), (uint8_t)(data_len - 34)};
-    uint32_t sum = 0;
-    for (int i = 0; i < 12; i += 2) sum += (uint32_t)psd[i] | ((uint32_t)psd[i + 1] << 8);
-    sum = (sum & 0xffff) + (sum >> 16);
-    sum = (sum & 0xffff) + (sum >> 16);
-    h[40] = (uint8_t)sum; h[41] = (uint8_t)(sum >> 8);
-    h[42] = (uint8_t)((1 << 4) + (P < 64 ? 0 : P < 128 ? 1 : P < 256 ? 2 : 3));  // job_type_size
-    h[43] = (uint8_t)prm->job_id;                                                // short_job_id
-    memcpy(a.hdr, h, 44);
-    dim3 grid(grid_for_tiles(a.ntiles));
-    hipStream_t st = (hipStream_t)stream;
-    const bool al = aligned16(d_in);
-    if (d_global_exps) { if (al) launch_frames_p<true, true>(P, grid, st, a); else launch_frames_p<false, true>(P, grid, st, a); }
-    else               { if (al) launch_frames_p<true, false>(P, grid, st, a); else launch_frames_p<false, false>(P, grid, st, a); }
-    return launch_check();
-}
-
-sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint64_t stride,
-                                   uint64_t numel, uint32_t P, uint16_t W, uint32_t batch_max,
-                                   uint64_t job_id, int8_t* d_exps, uint64_t* d_state, float* d_out,
-                                   uint64_t* d_counts, void* stream) {
-    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
-    if (W == 0 || batch_max == 0) return SML_ERR_INVALID_ARG;
-    if (num_frames == 0) return SML_OK;
-    if (num_frames >= 0xFFFFFFFEull) return SML_ERR_UNSUPPORTED;
-    if (!frames || !d_state || (numel && (!d_exps || !d_out))) return SML_ERR_INVALID_ARG;
-    if (!aligned4(frames) || !aligned4(d_out) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
-    if (((uintptr_t)d_state & 7u) || (d_counts && ((uintptr_t)d_counts & 7u))) return SML_ERR_ALIGNMENT;
-    RxArgs a;
-    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
-    a.frames = static_cast<const uint8_t*>(frames);
-    a.nframes = num_frames;
-    a.stride = stride;
-    a.numel = numel;
-    a.nblocks = sml_num_blocks(numel, P);
-    a.b = a.nblocks < batch_max ? a.nblocks : batch_max;
-    a.state = reinterpret_cast<unsigned long long*>(d_state);
-    a.exps = d_exps;
-    a.out = d_out;
-    a.counts = reinterpret_cast<unsigned long long*>(d_counts);
-    a.W = W;
-    a.job = (uint8_t)job_id;
-    hipStream_t st = (hipStream_t)stream;
-    k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
-    const uint64_t ntiles = (num_frames * P + kRxTileElems - 1) / kRxTileElems;
-    launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
-    k_rx_commit<<<grid_for_vec(a.nblocks + a.b), kBlockThreads, 0, st>>>(a);
     return launch_check();
 }
 
