@@ -92,6 +92,36 @@ __global__ __launch_bounds__(256) void k_copy_srcoff(const unsigned char* __rest
     }
 }
 
+// Fewer, longer-lived workgroups: each processes ITER consecutive 16 KiB
+// chunks (wg256 x 4 f4 per lane per chunk), loads of chunk i+1 issued before
+// the stores of chunk i; XCD order over workgroups (runs of C).
+template <int ITER, int C>
+__global__ __launch_bounds__(256) void k_copy_multi(const u4* __restrict__ in, u4* __restrict__ out) {
+    const unsigned long long r = blockIdx.x / 8, span = 8ull * C;
+    unsigned long long b = blockIdx.x;
+    if (b < gridDim.x / span * span) b = (r / C) * span + (b % 8) * C + r % C;
+    const unsigned long long base0 = b * (1024ull * ITER) + (threadIdx.x / 64) * 256ull + (threadIdx.x % 64);
+    u4 v[4], w[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = __builtin_nontemporal_load(in + base0 + 64ull * u);
+#pragma unroll
+    for (int it = 0; it < ITER; it++) {
+        const unsigned long long base = base0 + 1024ull * it;
+        if (it + 1 < ITER) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) w[u] = __builtin_nontemporal_load(in + base + 1024 + 64ull * u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            u4 x = v[u];
+            x.x ^= 0x80000000u;
+            out[base + 64ull * u] = x;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = w[u];
+    }
+}
+
 template <int WG, int U, int LOADNT>
 __global__ __launch_bounds__(WG) void k_read(const u4* __restrict__ in, unsigned int* __restrict__ sink) {
     const unsigned long long base = blockIdx.x * (unsigned long long)(WG * U) + (threadIdx.x / 64) * (64ull * U) + (threadIdx.x % 64);
@@ -151,20 +181,16 @@ int main(int argc, char** argv) {
 #define WRITE(WG, U, SN) vs.push_back({"write wg" #WG " u" #U " stnt" #SN, 16.0, \
     [=](hipStream_t s) { unsigned long long g = nvec / (WG * U); k_write<WG, U, SN><<<g, WG, 0, s>>>(out); }, {}})
     COPY(256, 4, 1, 0, 64);  // == K1 now
-#define COPYOFF(O) vs.push_back({"copy dst+" #O " bytes (unaligned x4 stores)", 32.0, \
-    [=](hipStream_t s) { k_copy_off<O><<<nvec / 1024, 256, 0, s>>>(in, reinterpret_cast<unsigned char*>(out2)); }, {}})
-    COPYOFF(0);
-    COPYOFF(4);
-    COPYOFF(8);
-    COPYOFF(12);
-    COPYOFF(16);
-#define COPYSRC(O, NT) vs.push_back({"copy src+" #O " bytes nt" #NT " (unaligned x4 loads)", 32.0, \
-    [=](hipStream_t s) { k_copy_srcoff<O, NT><<<nvec / 1024, 256, 0, s>>>(reinterpret_cast<const unsigned char*>(out2), out); }, {}})
-    COPYSRC(0, 1);
-    COPYSRC(4, 1);
-    COPYSRC(8, 1);
-    COPYSRC(0, 0);
-    COPYSRC(4, 0);
+#define MULTI(IT, C) vs.push_back({"copy multi iter" #IT " xcd" #C, 32.0, \
+    [=](hipStream_t s) { k_copy_multi<IT, C><<<nvec / (1024 * IT), 256, 0, s>>>(in, out); }, {}})
+    MULTI(1, 64);
+    MULTI(2, 32);
+    MULTI(4, 16);
+    MULTI(8, 8);
+    MULTI(16, 4);
+    MULTI(2, 64);
+    MULTI(4, 64);
+    READ(256, 4, 1);
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
