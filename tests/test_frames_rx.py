@@ -187,3 +187,38 @@ def test_frames_tx_rx_round_trip_equals_fused_loopback(cuda, W):
     torch.cuda.synchronize()
     assert torch.equal(rx.out.view(torch.int32), ref.view(torch.int32))
     assert rx.counts.tolist() == [F, 0]
+
+
+# ------------------------------------------------------ randomized (GPU) --
+
+@pytest.mark.gpu
+def test_rx_frames_random_streams(cuda):
+    """Hypothesis (derandomized): random slice length, P, W, batch size, job id,
+    duplicate / wrong-job / bad-pkt_id counts, shuffle seed and number of rx
+    calls; the GPU receive path equals the oracle's sequential loop (output,
+    exponents and accepted/discarded counters)."""
+    hyp = pytest.importorskip("hypothesis")
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+    import torch
+    import switchml_amd as sw
+
+    @settings(max_examples=80, deadline=None, derandomize=True, suppress_health_check=list(HealthCheck))
+    @given(n=st.integers(1, 20_000), P=st.sampled_from([64, 128, 256, 512, 1024]), W=st.sampled_from([1, 2, 3, 8]),
+           bm=st.integers(1, 70), job=st.integers(0, 255), dups=st.integers(0, 6), wrong=st.integers(0, 4),
+           bad=st.booleans(), seed=st.integers(0, 2 ** 31), calls=st.integers(1, 4))
+    def check(n, P, W, bm, job, dups, wrong, bad, seed, calls):
+        x = O.splitmix_normal(seed, n)
+        frames, _ = rx_stream(x, P, W, bm, job_id=job, seed=seed, n_dups=dups, n_wrong=wrong, bad_pid=bad)
+        F = frames.shape[0]
+        calls = min(calls, F)
+        ref = O.RxState(n, P, bm)
+        cuts = np.linspace(0, F, calls + 1).astype(int)
+        for a, c in zip(cuts[:-1], cuts[1:]):
+            O.dequantize_frames(frames[a:c], int(c - a), frames.shape[1], ref, W, job_id=job)
+        out, exps, cnt = _run_gpu(torch, sw, frames, P, W, bm, job, n, "device", calls=calls)
+        assert np.array_equal(out.view(np.uint32), ref.out.view(np.uint32))
+        assert np.array_equal(exps, ref.exps)
+        assert cnt == ref.counts
+
+    check()
