@@ -442,14 +442,38 @@ def host_inclusive(sw, torch, x, N, P, chunk=8 * 1024 * 1024, reps=5):
                 he[blo:bhi].copy_(de[blo:bhi], non_blocking=True)
             evs.append(e2)
 
+    dring = [torch.empty(chunk, dtype=torch.float32, device=dev) for _ in range(2)]
+    copy_done = [torch.cuda.Event() for _ in range(2)]
+    kern_done = [torch.cuda.Event() for _ in range(2)]
+
+    def hybrid():
+        # input over PCIe by the copy engine (H2D, chunked into a 2-slot HBM
+        # ring), output by the kernel's own stores straight into the pinned
+        # host planes (D2H direction): the two PCIe directions overlap.
+        for c in range(N // chunk):
+            lo, hi = c * chunk, (c + 1) * chunk
+            blo, bhi = lo // P, hi // P
+            r = c % 2
+            with torch.cuda.stream(sa):
+                if c >= 2:
+                    sa.wait_event(kern_done[r])
+                dring[r].copy_(hx[lo:hi], non_blocking=True)
+                copy_done[r].record(sa)
+            sb.wait_event(copy_done[r])
+            sw.quantize_pack(dring[r], P, 1, payload=hp[lo:hi], exps_out=he[blo:bhi], stream=sb)
+            kern_done[r].record(sb)
+
     def zero_copy():
         # K1 reads the pinned host bucket and writes the pinned host planes
         # directly over PCIe (host memory is device-accessible under HIP's
         # unified addressing): one pass, both PCIe directions at once.
         sw.quantize_pack(hx, P, 1, payload=hp, exps_out=he, stream=s0)
 
+    ref_head = sw.quantize_pack(x[: 4 * P], P, 1)[0]
+    ref_tail = sw.quantize_pack(x[N - 4 * P:], P, 1)[0]
+    ref_e = sw.exponents(x, P)
     out = {}
-    for name, fn in (("serial", serial), ("pipelined", pipelined), ("zero_copy", zero_copy)):
+    for name, fn in (("serial", serial), ("pipelined", pipelined), ("hybrid", hybrid), ("zero_copy", zero_copy)):
         fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -458,9 +482,13 @@ def host_inclusive(sw, torch, x, N, P, chunk=8 * 1024 * 1024, reps=5):
         torch.cuda.synchronize()
         t = (time.perf_counter() - t0) / reps
         out[f"host_inclusive_{name}_input_GBps"] = round(4 * N / t / 1e9, 2)
-    ok = bool(torch.equal(hp[: 4 * P].to(dev), sw.quantize_pack(x[: 4 * P], P, 1)[0]))
-    ok = ok and bool(torch.equal(he.to(dev), sw.exponents(x, P)))
-    out["host_inclusive_check"] = ok
+        if name != "serial":   # every variant leaves the same planes in hp / he
+            tail = slice(N - 4 * P, N)
+            ok_v = bool(torch.equal(hp[: 4 * P].to(dev), ref_head)) and bool(torch.equal(hp[tail].to(dev), ref_tail))
+            ok_v = ok_v and bool(torch.equal(he.to(dev), ref_e))
+            out["host_inclusive_check"] = out.get("host_inclusive_check", True) and ok_v
+        hp.zero_()
+        he.zero_()
     return out
 
 
