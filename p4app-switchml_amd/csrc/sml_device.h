@@ -312,7 +312,26 @@ __device__ __forceinline__ float scale_for(uint32_t W, int e) {
     return (W & (W - 1)) == 0 ? scale_of_pow2(31 - __builtin_clz(W), e) : scale_of(W, e);
 }
 
+// For W = 2^k the scale is a power of two (or +inf / 0), so its reciprocal is
+// exact and q / s == q * (1 / s) bit for bit: both round the same real number
+// q * 2^-x once (2^-x is representable for every x here, 2^-127 as a
+// denormal); s = +inf -> 1/s = 0 and s = 0 -> 1/s = +inf give the same
+// signed zeros / infinities / NaN as the division.
+__device__ __forceinline__ float rcp_scale_pow2(uint32_t log2W, int e) {
+    const int m = e + (int)log2W;
+    if (m >= 128) return __builtin_huge_valf();  // scale 0
+    const int x = 31 - m;
+    if (x > 127) return 0.0f;                     // scale +inf
+    return __builtin_ldexpf(1.0f, -x);
+}
+
 // Per-workgroup scale table, lut[(uint8_t)e], built once per launch-block.
+// Reciprocal table for power-of-two W (dequantize by multiplication).
+__device__ __forceinline__ void build_rcp_lut(float* lut, uint32_t W) {
+    lut[threadIdx.x] = rcp_scale_pow2(31 - __builtin_clz(W), (int)(int8_t)(uint8_t)threadIdx.x);
+    __syncthreads();
+}
+
 __device__ __forceinline__ void build_lut(float* lut, uint32_t W) {
     lut[threadIdx.x] = scale_for(W, (int)(int8_t)(uint8_t)threadIdx.x);
     __syncthreads();

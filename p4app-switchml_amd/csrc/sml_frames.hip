@@ -247,7 +247,11 @@ constexpr int kRxTileElems = kRxU * kWave * 4;
 template <int P>
 __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     __shared__ float lut[256];
-    build_lut(lut, a.W);
+    // power-of-two W: the table holds exact reciprocals and dequantize multiplies
+    // (bit-equal to the IEEE division, rcp_scale_pow2); otherwise scales
+    const bool pow2 = (a.W & (a.W - 1)) == 0;
+    if (pow2) build_rcp_lut(lut, a.W);
+    else build_lut(lut, a.W);
     constexpr int kChunksPerFrame = P / 4;     // 16-B chunks per payload
     constexpr int kFramesPerTile = kRxTileElems / P;
     const int lane = threadIdx.x & (kWave - 1);
@@ -309,8 +313,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             if (!h[u].ok || h[u].pid < a.b) continue;
             const uint64_t off = (uint64_t)(h[u].pid - a.b) * P + 4ull * ((u * kWave + lane) % kChunksPerFrame);
             if (off >= a.numel) continue;
-            const f4 o = mkf4(dequantize1(bswap(w[u].x), s[u]), dequantize1(bswap(w[u].y), s[u]),
-                              dequantize1(bswap(w[u].z), s[u]), dequantize1(bswap(w[u].w), s[u]));
+            f4 o;
+            if (pow2)
+                o = mkf4((float)(int32_t)bswap(w[u].x) * s[u], (float)(int32_t)bswap(w[u].y) * s[u],
+                         (float)(int32_t)bswap(w[u].z) * s[u], (float)(int32_t)bswap(w[u].w) * s[u]);
+            else
+                o = mkf4(dequantize1(bswap(w[u].x), s[u]), dequantize1(bswap(w[u].y), s[u]),
+                         dequantize1(bswap(w[u].z), s[u]), dequantize1(bswap(w[u].w), s[u]));
             float* p = a.out + off;
             if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o;
             else store4_guarded(p, o, 0, a.numel - off);

@@ -96,10 +96,13 @@ struct DequantArgs {
 };
 
 // K4: dequantize the aggregated payload (PostprocessSingle, ppp.cc:197-251).
-template <int P, bool ALIGNED, bool BE>
+// RCP (power-of-two W): multiply by the exact reciprocal instead of the IEEE
+// division — same bits (rcp_scale_pow2).
+template <int P, bool ALIGNED, bool BE, bool RCP>
 __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
     __shared__ float lut[256];
-    build_lut(lut, a.W);
+    if constexpr (RCP) build_rcp_lut(lut, a.W);
+    else build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
@@ -131,8 +134,12 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
             if (!full && idx >= a.numel) continue;
             uint32_t q0 = (uint32_t)w[u].x, q1 = (uint32_t)w[u].y, q2 = (uint32_t)w[u].z, q3 = (uint32_t)w[u].w;
             if constexpr (BE) { q0 = bswap(q0); q1 = bswap(q1); q2 = bswap(q2); q3 = bswap(q3); }
-            f4 o = mkf4(dequantize1(q0, s[u]), dequantize1(q1, s[u]),
-                                   dequantize1(q2, s[u]), dequantize1(q3, s[u]));
+            f4 o;
+            if constexpr (RCP)
+                o = mkf4((float)(int32_t)q0 * s[u], (float)(int32_t)q1 * s[u], (float)(int32_t)q2 * s[u],
+                         (float)(int32_t)q3 * s[u]);
+            else
+                o = mkf4(dequantize1(q0, s[u]), dequantize1(q1, s[u]), dequantize1(q2, s[u]), dequantize1(q3, s[u]));
             if (full) store4<ALIGNED>(a.out + idx, o);
             else store4_guarded(a.out + idx, o, idx, a.numel);
         }
@@ -157,6 +164,8 @@ template <int P, bool ALIGNED, bool BE, bool RNE>
 __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
     __shared__ float lut[256];
     build_lut(lut, a.W);
+    const bool pow2 = (a.W & (a.W - 1)) == 0;
+    const uint32_t log2W = 31 - __builtin_clz(a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t padded = a.nblocks * P;
@@ -201,9 +210,17 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
                               : mku4(q[0], q[1], q[2], q[3]);
                 store_payload(a.payload + idx / 4, wq);
             }
-            // DummyBackend::ProcessPacket: int32 wrap multiply by W.
-            f4 o = mkf4(dequantize1(q[0] * a.W, s), dequantize1(q[1] * a.W, s),
-                                   dequantize1(q[2] * a.W, s), dequantize1(q[3] * a.W, s));
+            // DummyBackend::ProcessPacket: int32 wrap multiply by W; then the
+            // dequantize (exact reciprocal multiply for power-of-two W, as K4).
+            f4 o;
+            if (pow2) {
+                const float r = rcp_scale_pow2(log2W, e[u]);
+                o = mkf4((float)(int32_t)(q[0] * a.W) * r, (float)(int32_t)(q[1] * a.W) * r,
+                         (float)(int32_t)(q[2] * a.W) * r, (float)(int32_t)(q[3] * a.W) * r);
+            } else {
+                o = mkf4(dequantize1(q[0] * a.W, s), dequantize1(q[1] * a.W, s), dequantize1(q[2] * a.W, s),
+                         dequantize1(q[3] * a.W, s));
+            }
             if (full) store4<ALIGNED>(a.out + idx, o);
             else if (idx < a.numel) store4_guarded(a.out + idx, o, idx, a.numel);
         }
@@ -324,15 +341,21 @@ static void launch_quant_b(bool be, bool rne, uint32_t P, dim3 g, hipStream_t st
     else launch_quant_r<ALIGNED, GLOBAL, false>(rne, P, g, st, a);
 }
 
-template <bool ALIGNED, bool BE>
+template <bool ALIGNED, bool BE, bool RCP>
 static void launch_deq_p(uint32_t P, dim3 grid, hipStream_t st, const DequantArgs& a) {
     switch (P) {
-        case 64:   k_dequantize<64, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_dequantize<128, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_dequantize<256, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_dequantize<512, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_dequantize<1024, ALIGNED, BE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   k_dequantize<64, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_dequantize<128, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_dequantize<256, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_dequantize<512, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_dequantize<1024, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
     }
+}
+
+template <bool ALIGNED, bool BE>
+static void launch_deq_w(uint32_t P, dim3 grid, hipStream_t st, const DequantArgs& a) {
+    if ((a.W & (a.W - 1)) == 0) launch_deq_p<ALIGNED, BE, true>(P, grid, st, a);
+    else launch_deq_p<ALIGNED, BE, false>(P, grid, st, a);
 }
 
 template <bool ALIGNED, bool BE, bool RNE>
@@ -472,8 +495,8 @@ sml_status_t sml_dequantize(const int32_t* d_payload, const int8_t* d_exps, uint
     dim3 grid(grid_for_tiles(a.ntiles));
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_out), be = !(flags & SML_FLAG_PAYLOAD_LE);
-    if (al) { if (be) launch_deq_p<true, true>(packet_numel, grid, st, a); else launch_deq_p<true, false>(packet_numel, grid, st, a); }
-    else    { if (be) launch_deq_p<false, true>(packet_numel, grid, st, a); else launch_deq_p<false, false>(packet_numel, grid, st, a); }
+    if (al) { if (be) launch_deq_w<true, true>(packet_numel, grid, st, a); else launch_deq_w<true, false>(packet_numel, grid, st, a); }
+    else    { if (be) launch_deq_w<false, true>(packet_numel, grid, st, a); else launch_deq_w<false, false>(packet_numel, grid, st, a); }
     return launch_check();
 }
 
