@@ -235,14 +235,22 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
     }
 }
 
-// Pass 2: PostprocessSingle for every winning frame, 1024 payload elements per
-// wave (1024 / P frames; lane-chunk c = u*64 + lane is 16 bytes of frame
-// c / (P/4)).  The payload loads are issued first, independent of the header;
-// a frame is the winner of its pkt_id iff state[pkt_id] holds its claim tag;
-// the exponent of block k is the low byte of state[k], whoever holds it (a
-// winner of this call or kRxDone).  Pass 3 retires the winners.
+// Pass 2: PostprocessSingle for every winning frame, walked in block order:
+// the wave of blocks k .. k + 1024/P - 1 reads state[k + b] (the claim tag of
+// the frame that won pkt_id k + b in this call, which names that frame) and
+// state[k] (low byte = exponent of block k, held by a winner of this call or
+// kRxDone), then gathers the winner's payload and writes out[k*P ..]
+// contiguously.  No header is read again; pkt_ids without a winner in this
+// call (not received, or received earlier) write nothing.  Pass 3 retires the
+// winners.
 constexpr int kRxU = 4;                        // 16-B chunks per lane per iteration
 constexpr int kRxTileElems = kRxU * kWave * 4;
+
+__device__ __forceinline__ bool rx_winner(unsigned long long sw, uint64_t nframes, uint64_t& f) {
+    const uint32_t hi = (uint32_t)(sw >> 32);
+    f = 0xFFFFFFFEull - hi;                    // rx_tag inverse
+    return hi != 0u && hi != kRxDone && f < nframes;
+}
 
 template <int P>
 __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
@@ -253,65 +261,53 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     if (pow2) build_rcp_lut(lut, a.W);
     else build_lut(lut, a.W);
     constexpr int kChunksPerFrame = P / 4;     // 16-B chunks per payload
-    constexpr int kFramesPerTile = kRxTileElems / P;
+    constexpr int kBlocksPerTile = kRxTileElems / P;
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t ntiles = (a.nframes + kFramesPerTile - 1) / kFramesPerTile;
+    const uint64_t ntiles = (a.nblocks + kBlocksPerTile - 1) / kBlocksPerTile;
     for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < ntiles; t += nwaves) {
         u4a w[kRxU];
-        RxHdr h[kRxU];
+        bool ok[kRxU];
         float s[kRxU];
         if constexpr (kChunksPerFrame >= kWave) {
-            // P >= 256: slice u of the tile lies in one frame, so its header and
-            // state words are wave-uniform: scalar loads (no vector-memory
-            // instructions for the per-frame metadata; pass 2 writes neither)
-#pragma unroll
-            for (int u = 0; u < kRxU; u++) {
-                const uint64_t f = t * kFramesPerTile + (u * kWave) / kChunksPerFrame;
-                if (f < a.nframes)
-                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
-                        a.frames + f * a.stride + 52 + 16ull * ((u * kWave + lane) % kChunksPerFrame)));
-            }
-            const ConstU32* hdr = reinterpret_cast<const ConstU32*>(reinterpret_cast<uintptr_t>(a.frames));
+            // P >= 256: slice u of the tile lies in one block, so its state
+            // words are wave-uniform: scalar loads
             const ConstU64* state = reinterpret_cast<const ConstU64*>(reinterpret_cast<uintptr_t>(a.state));
+            uint64_t f[kRxU];
 #pragma unroll
             for (int u = 0; u < kRxU; u++) {
-                const uint64_t f = t * kFramesPerTile + (u * kWave) / kChunksPerFrame;
-                h[u] = RxHdr{0u, 0u, false};
+                const uint64_t k = t * kBlocksPerTile + (u * kWave) / kChunksPerFrame;
+                ok[u] = false;
                 s[u] = 0.0f;
-                if (f >= a.nframes) continue;
-                const uint64_t hw = (f * a.stride + 40) / 4;
-                const uint32_t d10 = hdr[hw], d11 = hdr[hw + 1], d12 = hdr[hw + 2];
-                h[u].pid = d11;
-                h[u].exp = (d12 >> 16) & 0xffu;
-                h[u].ok = (d10 >> 24) == a.job && (uint64_t)d11 < a.nblocks + a.b &&
-                          (uint32_t)(state[d11] >> 32) == rx_tag(f);
-                if (h[u].ok && d11 >= a.b) s[u] = lut[(uint32_t)state[d11 - a.b] & 0xffu];
+                if (k >= a.nblocks) continue;
+                ok[u] = rx_winner(state[k + a.b], a.nframes, f[u]);
+                s[u] = lut[(uint32_t)state[k] & 0xffu];
             }
+#pragma unroll
+            for (int u = 0; u < kRxU; u++)
+                if (ok[u])
+                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
+                        a.frames + f[u] * a.stride + 52 + 16ull * ((u * kWave + lane) % kChunksPerFrame)));
         } else {
 #pragma unroll
             for (int u = 0; u < kRxU; u++) {
-                const int c = u * kWave + lane;
-                const uint64_t f = t * kFramesPerTile + c / kChunksPerFrame;
-                h[u].ok = false;
-                if (f >= a.nframes) continue;
+                const uint64_t k = t * kBlocksPerTile + (u * kWave + lane) / kChunksPerFrame;
+                ok[u] = false;
+                s[u] = 0.0f;
+                if (k >= a.nblocks) continue;
+                uint64_t f;
+                ok[u] = rx_winner(a.state[k + a.b], a.nframes, f);
+                s[u] = lut[(uint32_t)a.state[k] & 0xffu];
                 // non-temporal: 25 % faster than default-policy loads for this stream (hbm_probe)
-                w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(a.frames + f * a.stride + 52 +
-                                                                               16ull * (c % kChunksPerFrame)));
-                h[u] = rx_header(a, f);
-            }
-#pragma unroll
-            for (int u = 0; u < kRxU; u++) {
-                if (!h[u].ok) continue;
-                const uint64_t f = t * kFramesPerTile + (u * kWave + lane) / kChunksPerFrame;
-                h[u].ok = (uint32_t)(a.state[h[u].pid] >> 32) == rx_tag(f);
-                s[u] = h[u].pid >= a.b ? lut[(uint32_t)a.state[h[u].pid - a.b] & 0xffu] : 0.0f;
+                if (ok[u])
+                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
+                        a.frames + f * a.stride + 52 + 16ull * ((u * kWave + lane) % kChunksPerFrame)));
             }
         }
 #pragma unroll
         for (int u = 0; u < kRxU; u++) {
-            if (!h[u].ok || h[u].pid < a.b) continue;
-            const uint64_t off = (uint64_t)(h[u].pid - a.b) * P + 4ull * ((u * kWave + lane) % kChunksPerFrame);
+            if (!ok[u]) continue;
+            const uint64_t off = t * kRxTileElems + 4ull * (u * kWave + lane);
             if (off >= a.numel) continue;
             f4 o;
             if (pow2)
@@ -458,8 +454,8 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     a.job = (uint8_t)job_id;
     hipStream_t st = (hipStream_t)stream;
     k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
-    const uint64_t ntiles = (num_frames * P + kRxTileElems - 1) / kRxTileElems;
-    launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
+    const uint64_t ntiles = (a.nblocks * P + kRxTileElems - 1) / kRxTileElems;
+    if (ntiles) launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
     k_rx_commit<<<grid_for_vec(a.nblocks + a.b), kBlockThreads, 0, st>>>(a);
     return launch_check();
 }
