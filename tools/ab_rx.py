@@ -29,10 +29,13 @@ def main(paths, N=64 * 1024 * 1024, P=256, bm=64, rounds=7, reps=10):
         L.sml_dequantize_frames.argtypes = [vp, u64, u64, u64, u32, u16, u32, u64, vp, vp, vp, vp, vp]
         libs.append(L)
 
+    # AB_COUNTS=1: also pass the {accepted, discarded} counters
+    counts = torch.zeros(2, dtype=torch.int64, device="cuda") if os.environ.get("AB_COUNTS") else None
+
     def run(L):
         state.zero_()
         rc = L.sml_dequantize_frames(frames.data_ptr(), F, fb, N, P, 1, bm, 0, exps.data_ptr(), state.data_ptr(),
-                                     out.data_ptr(), None, st.cuda_stream)
+                                     out.data_ptr(), None if counts is None else counts.data_ptr(), st.cuda_stream)
         assert rc == 0, rc
 
     for p, L in zip(paths, libs):
