@@ -16,6 +16,12 @@ def main(paths, N=64 * 1024 * 1024, P=256, bm=64, rounds=7, reps=10):
     F = B + min(B, bm)
     fb = sw.frame_bytes(P)
     frames = sw.quantize_pack_frames(x, sw.frame_params(max_outstanding_pkts=bm), P, 1, batch_max=bm)
+    if os.environ.get("AB_SHUFFLE"):
+        # AB_SHUFFLE=w: frames permuted at random inside windows of w frames
+        w = int(os.environ["AB_SHUFFLE"])
+        g = torch.Generator().manual_seed(7)
+        perm = torch.cat([i + torch.randperm(min(w, F - i), generator=g) for i in range(0, F, w)]).to("cuda")
+        frames = frames.view(F, fb)[perm].reshape(-1).contiguous()
     ref = sw.roundtrip_loopback(x, P, 1)
     st = torch.cuda.current_stream()
     state = torch.zeros(F, dtype=torch.int64, device="cuda")
