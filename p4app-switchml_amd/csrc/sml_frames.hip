@@ -196,9 +196,13 @@ struct RxHdr {
     bool ok;                    // this job, pkt_id in range
 };
 
+typedef uint32_t u3a __attribute__((ext_vector_type(3), aligned(4)));
+
 __device__ __forceinline__ RxHdr rx_header(const RxArgs& a, uint64_t f) {
-    const uint32_t* h = reinterpret_cast<const uint32_t*>(a.frames + f * a.stride + 40);
-    const uint32_t d10 = h[0], d11 = h[1], d12 = h[2];
+    // one 12-byte load for dwords 10..12 (the compiler otherwise sinks the
+    // dword-12 load behind the job / range check: two round trips)
+    const u3a hv = __builtin_nontemporal_load(reinterpret_cast<const u3a*>(a.frames + f * a.stride + 40));
+    const uint32_t d10 = hv.x, d11 = hv.y, d12 = hv.z;
     RxHdr r;
     r.pid = d11;
     r.exp = (d12 >> 16) & 0xffu;
@@ -212,26 +216,33 @@ __device__ __forceinline__ RxHdr rx_header(const RxArgs& a, uint64_t f) {
 // workgroups that saw a discard touch the counters (same-address atomics from
 // every workgroup serialize in one L2 channel: ~40 us at 262 k frames).
 __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    const uint64_t f0 = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x;
+    if (!a.counts) {
+        // no counters: non-returning atomics, the wave does not wait for them
+        for (uint64_t f = f0; f < a.nframes; f += stride) {
+            const RxHdr h = rx_header(a, f);
+            if (h.ok) atomicMax(a.state + h.pid, ((unsigned long long)rx_tag(f) << 32) | h.exp);
+        }
+        return;
+    }
     __shared__ uint32_t disc;
     if (threadIdx.x == 0) disc = 0;
     __syncthreads();
     uint32_t mine = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
-    for (uint64_t f = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; f < a.nframes; f += stride) {
+    for (uint64_t f = f0; f < a.nframes; f += stride) {
         const RxHdr h = rx_header(a, f);
         if (!h.ok) { mine++; continue; }
         const unsigned long long v = ((unsigned long long)rx_tag(f) << 32) | h.exp;
         if (atomicMax(a.state + h.pid, v) != 0ull) mine++;          // duplicate or received earlier
     }
-    if (a.counts) {
-        if (mine) atomicAdd(&disc, mine);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long acc = blockIdx.x == 0 ? (unsigned long long)a.nframes : 0ull;
-            acc -= disc;                                                 // mod 2^64
-            if (acc) atomicAdd(a.counts + 0, acc);
-            if (disc) atomicAdd(a.counts + 1, (unsigned long long)disc);
-        }
+    if (mine) atomicAdd(&disc, mine);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long acc = blockIdx.x == 0 ? (unsigned long long)a.nframes : 0ull;
+        acc -= disc;                                                 // mod 2^64
+        if (acc) atomicAdd(a.counts + 0, acc);
+        if (disc) atomicAdd(a.counts + 1, (unsigned long long)disc);
     }
 }
 
