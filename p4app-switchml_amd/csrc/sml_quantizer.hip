@@ -410,7 +410,8 @@ uint32_t sml_set_tiles_per_wave(uint32_t tpw) {
 
 uint64_t sml_num_blocks(uint64_t numel, uint32_t packet_numel) {
     if (packet_numel == 0) return 0;
-    return (numel * 4 + (uint64_t)packet_numel * 4 - 1) / ((uint64_t)packet_numel * 4);
+    // ceil(numel*4 / (P*4)) of ppp.cc:56-57, without the byte-count overflow
+    return numel / packet_numel + (numel % packet_numel != 0);
 }
 
 sml_status_t sml_scale_lut(uint16_t num_workers, float lut[256]) {

@@ -39,6 +39,12 @@ def test_num_blocks_matches_oracle(sw, numel, P):
     assert sw.num_blocks(numel, P) == O.num_blocks(numel, P)
 
 
+def test_num_blocks_no_byte_count_overflow(sw):
+    # numel * 4 would wrap 64 bits; the block count must not
+    for numel, P in [(2 ** 62 + 1, 256), (2 ** 64 - 1, 64), (2 ** 64 - 1, 1024)]:
+        assert sw.num_blocks(numel, P) == -(-numel // P)
+
+
 @pytest.mark.parametrize("W", [1, 2, 3, 4, 5, 7, 8, 16, 255, 256, 1000, 4096, 65535])
 def test_host_scale_lut_matches_oracle(sw, W):
     assert np.array_equal(sw.scale_lut(W).view(np.uint32), O.scale_lut(W).view(np.uint32))
