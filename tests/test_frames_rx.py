@@ -143,6 +143,26 @@ def test_rx_frames_match_oracle(cuda, P, n, W, bm, where):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("P,pad", [(256, 12), (64, 2048 - 52 - 4 * 64), (1024, 4)])
+def test_rx_frames_padded_stride(cuda, P, pad):
+    """Frames at an mbuf-like stride (frame bytes + padding, e.g. a 2 KiB data
+    room): padding bytes are ignored, results equal the oracle's loop."""
+    import torch
+    import switchml_amd as sw
+    n, W, bm = 40_000 + P // 3, 3, 16
+    x = O.splitmix_normal(31 + P, n)
+    frames, _ = rx_stream(x, P, W, bm, job_id=7, seed=P)
+    F, fb = frames.shape
+    padded = np.full((F, fb + pad), 0xCD, dtype=np.uint8)
+    padded[:, :fb] = frames
+    ref = O.dequantize_frames(frames, F, fb, O.RxState(n, P, bm), W, job_id=7)
+    out, exps, cnt = _run_gpu(torch, sw, padded, P, W, bm, 7, n, "device")
+    assert np.array_equal(out.view(np.uint32), ref.out.view(np.uint32))
+    assert np.array_equal(exps, ref.exps)
+    assert cnt == ref.counts
+
+
+@pytest.mark.gpu
 def test_rx_frames_across_calls(cuda):
     import torch
     import switchml_amd as sw
