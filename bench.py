@@ -391,6 +391,18 @@ def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
     hframes = torch.empty(fbytes, dtype=torch.uint8).pin_memory()
     t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=hframes, stream=stream))
     res["frames_to_pinned_host_input_GBps"] = round(4 * N / t / 1e9, 2)
+    # K6: the switch's aggregation over W worker planes fused with the
+    # dequantize (the peer-to-peer switch's compute; planes local here)
+    sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=stream)
+    planes = [payload] + [payload.clone() for _ in range(7)]
+    eplanes = [exps] * 8
+    for W in (2, 4, 8):
+        t = timeit(lambda: sw.switch_aggregate(planes[:W], eplanes[:W], N, P, out=out, stream=stream))
+        res[f"switch_aggregate_W{W}_GBps"] = round((W * (4 * B * P + B) + 4 * N) / t / 1e9, 1)
+    agg = torch.empty_like(payload)
+    t = timeit(lambda: sw.switch_aggregate(planes, None, N, P, payload_out=agg, stream=stream))
+    res["switch_payload_sum_W8_GBps"] = round(9 * 4 * B * P / t / 1e9, 1)
+    del planes, agg
     t = timeit(lambda: sw.stream_copy(x, out, stream=stream))
     res["nt_tile_copy_GBps"] = round(8 * N / t / 1e9, 1)
     return res

@@ -132,6 +132,27 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
                                     int32_t* d_payload, int8_t* d_exps_out,
                                     uint32_t flags, void* stream);
 
+/* ---- The switch's aggregation ---------------------------
+ * K6: what the Tofino pipeline does to W workers' packets for one slot, over
+ * whole planes, fused with the worker's dequantize:
+ *   d_payload_out[i] = htonl(sum_w ntohl(d_payloads[w][i]))  wrapping bit<32>
+ *                      (p4/processor.p4:48-54; LE words with
+ *                      SML_FLAG_PAYLOAD_LE: no swaps), i < B*P
+ *   d_exps_out[k]    = max_w (int8) d_exps[w][k]   (p4/exponents.p4:48-54)
+ *   d_out[i]         = (float)(int32)sum_i / scale(W, e_max[i/P]), i < numel
+ *                      (PostprocessSingle, ppp.cc:197-251; W = num_workers)
+ * d_payloads / d_exps are HOST arrays of num_workers DEVICE pointers: local
+ * buffers, or peers' HBM mapped over xGMI (hipIpcOpenMemHandle) — the
+ * peer-to-peer switch.  Any of the three outputs may be NULL (not all);
+ * d_exps may be NULL when d_exps_out and d_out are.  Payload planes 16-byte
+ * aligned (B*P words each); d_payload_out may alias d_payloads[w].
+ * num_workers <= SML_MAX_SWITCH_WORKERS. */
+#define SML_MAX_SWITCH_WORKERS 16
+sml_status_t sml_switch_aggregate(const int32_t* const* d_payloads, const int8_t* const* d_exps,
+                                  uint16_t num_workers, uint64_t numel, uint32_t packet_numel,
+                                  int32_t* d_payload_out, int8_t* d_exps_out, float* d_out,
+                                  uint32_t flags, void* stream);
+
 /* ---- DPDK/UDP wire frames --------------------------------
  * The DPDK backend builds one Ethernet frame per packet
  * (client_lib/src/backends/dpdk/dpdk_worker_thread_utils.inc:67-135,

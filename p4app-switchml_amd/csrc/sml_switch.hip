@@ -1,0 +1,193 @@
+// sml_switch.hip — the switch's aggregation over W worker planes as a CDNA4
+// kernel (K6), with the worker's dequantize fused behind it.
+//
+// The Tofino data plane adds the W workers' payload slots as bit<32>
+// (p4/processor.p4:48-54, wrapping) after parsing them big-endian, takes the
+// signed int8 max of the exponents (p4/exponents.p4:48-54, types.p4:113,119)
+// and multicasts the result; every worker then runs PostprocessSingle
+// (ppp.cc:197-251) with scale(W, e_max).  Here the W planes are device
+// pointers — local buffers, or peers' HBM mapped over xGMI (IPC handles) — so
+// one pass reads W payload planes and writes the aggregated plane and/or the
+// dequantized fp32 bucket:
+//   payload_out[i] = htonl(sum_w ntohl(payload_w[i]))   (LE words: no swaps)
+//   exps_out[k]    = max_w (int8) exps_w[k]
+//   out[i]         = (float)(int32)sum_i / scale(W, e_max[i / P])
+// Bit-identical to orc_switch_payload / orc_switch_exps followed by K4.
+#include "sml_host.h"
+
+namespace sml {
+
+struct SwitchArgs {
+    const u4* payload[SML_MAX_SWITCH_WORKERS];
+    const int8_t* exps[SML_MAX_SWITCH_WORKERS];
+    u4* payload_out;        // nullable: aggregated plane (B*P words)
+    int8_t* exps_out;       // nullable: max exponents (B bytes)
+    float* out;             // nullable: dequantized bucket (numel floats)
+    uint64_t numel;
+    uint64_t nblocks;       // B
+    uint64_t ntiles;        // ceil(B*P / 1024)
+    uint32_t nw;            // planes = num_workers
+    uint32_t xcd;
+    uint32_t exps_scalar;   // every exps[w] 4-byte aligned: one scalar load per slice
+};
+
+// W payload loads per lane-slice are issued before the adds (16-B
+// non-temporal, as K4); exponent bytes come one scalar load per slice and
+// plane when the planes are 4-byte aligned.
+template <int P, bool ALIGNED, bool BE, bool RCP, bool EXPS>
+__global__ __launch_bounds__(kBlockThreads) void k_switch_aggregate(SwitchArgs a) {
+    __shared__ float lut[256];
+    if (a.out) {
+        if constexpr (RCP) build_rcp_lut(lut, a.nw);
+        else build_lut(lut, a.nw);
+    }
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t padded = a.nblocks * P;
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
+        const uint64_t base = t * kTileElems;
+        const bool full = base + kTileElems <= padded;
+        u4 acc[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) acc[u] = mku4(0, 0, 0, 0);
+        for (uint32_t w = 0; w < a.nw; w++) {
+            u4 v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+                v[u] = (full || idx < padded) ? __builtin_nontemporal_load(a.payload[w] + idx / 4) : mku4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                if constexpr (BE) {
+                    acc[u].x += bswap(v[u].x); acc[u].y += bswap(v[u].y);
+                    acc[u].z += bswap(v[u].z); acc[u].w += bswap(v[u].w);
+                } else {
+                    acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+                }
+            }
+        }
+        int e[kU];
+        if constexpr (EXPS) {
+#pragma unroll
+            for (int u = 0; u < kU; u++) e[u] = -128;
+            for (uint32_t w = 0; w < a.nw; w++) {
+                if (full && a.exps_scalar) {
+#pragma unroll
+                    for (int u = 0; u < kU; u++) {
+                        const int ew = (int)(int8_t)(uint8_t)slice_exponent_byte<P>(a.exps[w], base, u, lane);
+                        e[u] = ew > e[u] ? ew : e[u];
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < kU; u++) {
+                        const uint64_t pkt = (base + (uint64_t)(u * kWave + lane) * 4) / P;
+                        const int ew = pkt < a.nblocks ? (int)a.exps[w][pkt] : -128;
+                        e[u] = ew > e[u] ? ew : e[u];
+                    }
+                }
+            }
+            if (a.exps_out) {
+                constexpr int kPk = kTileElems / P;
+                if (((uintptr_t)a.exps_out & (kPk - 1)) == 0 && full)
+                    store_tile_exponents<P>(a.exps_out + base / P, lane, e);
+                else
+                    store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            if (!full && idx >= padded) continue;
+            if (a.payload_out) {
+                const u4 q = acc[u];
+                store_payload(a.payload_out + idx / 4,
+                              BE ? mku4(bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)) : q);
+            }
+            if constexpr (EXPS) {
+                if (a.out && idx < a.numel) {
+                    const float s = lut[(uint8_t)e[u]];
+                    const u4 q = acc[u];
+                    f4 o;
+                    if constexpr (RCP)
+                        o = mkf4((float)(int32_t)q.x * s, (float)(int32_t)q.y * s, (float)(int32_t)q.z * s,
+                                 (float)(int32_t)q.w * s);
+                    else
+                        o = mkf4(dequantize1(q.x, s), dequantize1(q.y, s), dequantize1(q.z, s), dequantize1(q.w, s));
+                    if (idx + 4 <= a.numel) store4<ALIGNED>(a.out + idx, o);
+                    else store4_guarded(a.out + idx, o, idx, a.numel);
+                }
+            }
+        }
+    }
+}
+
+template <bool ALIGNED, bool BE, bool RCP, bool EXPS>
+static void launch_switch_p(uint32_t P, dim3 grid, hipStream_t st, const SwitchArgs& a) {
+    switch (P) {
+        case 64:   k_switch_aggregate<64, ALIGNED, BE, RCP, EXPS><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_switch_aggregate<128, ALIGNED, BE, RCP, EXPS><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_switch_aggregate<256, ALIGNED, BE, RCP, EXPS><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_switch_aggregate<512, ALIGNED, BE, RCP, EXPS><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_switch_aggregate<1024, ALIGNED, BE, RCP, EXPS><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
+template <bool ALIGNED, bool BE>
+static void launch_switch_m(bool exps, bool rcp, uint32_t P, dim3 g, hipStream_t st, const SwitchArgs& a) {
+    if (!exps) launch_switch_p<ALIGNED, BE, false, false>(P, g, st, a);
+    else if (rcp) launch_switch_p<ALIGNED, BE, true, true>(P, g, st, a);
+    else launch_switch_p<ALIGNED, BE, false, true>(P, g, st, a);
+}
+
+}  // namespace sml
+
+using namespace sml;
+
+extern "C" {
+
+sml_status_t sml_switch_aggregate(const int32_t* const* d_payloads, const int8_t* const* d_exps,
+                                  uint16_t num_workers, uint64_t numel, uint32_t packet_numel,
+                                  int32_t* d_payload_out, int8_t* d_exps_out, float* d_out,
+                                  uint32_t flags, void* stream) {
+    if (!valid_packet(packet_numel)) return SML_ERR_UNSUPPORTED;
+    if (num_workers == 0 || !d_payloads) return SML_ERR_INVALID_ARG;
+    if (num_workers > SML_MAX_SWITCH_WORKERS) return SML_ERR_UNSUPPORTED;
+    if (numel == 0) return SML_OK;
+    if (!d_payload_out && !d_exps_out && !d_out) return SML_ERR_INVALID_ARG;
+    const bool exps = d_exps_out || d_out;
+    if (exps && !d_exps) return SML_ERR_INVALID_ARG;
+    if (d_out && !aligned4(d_out)) return SML_ERR_INVALID_ARG;
+    if (d_payload_out && !aligned16(d_payload_out)) return SML_ERR_ALIGNMENT;
+    SwitchArgs a{};
+    a.exps_scalar = 1;
+    for (uint32_t w = 0; w < num_workers; w++) {
+        if (!d_payloads[w]) return SML_ERR_INVALID_ARG;
+        if (!aligned16(d_payloads[w])) return SML_ERR_ALIGNMENT;
+        a.payload[w] = reinterpret_cast<const u4*>(d_payloads[w]);
+        if (exps) {
+            if (!d_exps[w]) return SML_ERR_INVALID_ARG;
+            a.exps[w] = d_exps[w];
+            if (!aligned4(d_exps[w])) a.exps_scalar = 0;
+        }
+    }
+    a.payload_out = reinterpret_cast<u4*>(d_payload_out);
+    a.exps_out = d_exps_out;
+    a.out = d_out;
+    a.numel = numel;
+    a.nblocks = sml_num_blocks(numel, packet_numel);
+    a.ntiles = (a.nblocks * packet_numel + kTileElems - 1) / kTileElems;
+    a.nw = num_workers;
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    const dim3 grid(grid_for_tiles(a.ntiles));
+    const hipStream_t st = (hipStream_t)stream;
+    const bool al = !d_out || aligned16(d_out), be = !(flags & SML_FLAG_PAYLOAD_LE);
+    const bool rcp = (num_workers & (num_workers - 1)) == 0;
+    if (al) { if (be) launch_switch_m<true, true>(exps, rcp, packet_numel, grid, st, a);
+              else launch_switch_m<true, false>(exps, rcp, packet_numel, grid, st, a); }
+    else    { if (be) launch_switch_m<false, true>(exps, rcp, packet_numel, grid, st, a);
+              else launch_switch_m<false, false>(exps, rcp, packet_numel, grid, st, a); }
+    return launch_check();
+}
+
+}  // extern "C"

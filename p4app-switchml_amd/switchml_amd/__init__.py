@@ -116,6 +116,8 @@ def lib():
     L.sml_set_xcd_chunk.argtypes = [u32]
     L.sml_dequantize_frames.restype = i32
     L.sml_dequantize_frames.argtypes = [vp, u64, u64, u64, u32, u16, u32, u64, vp, vp, vp, vp, vp]
+    L.sml_switch_aggregate.restype = i32
+    L.sml_switch_aggregate.argtypes = [vp, vp, u16, u64, u32, vp, vp, vp, u32, vp]
     _lib = L
     return L
 
@@ -282,6 +284,46 @@ def roundtrip_loopback(x, packet_numel: int = 256, num_workers: int = 1, out=Non
     _check("sml_roundtrip_loopback", lib().sml_roundtrip_loopback(
         _dev(x, torch.float32, "x"), _dev(out, torch.float32, "out"), x.numel(), packet_numel,
         num_workers, p, e, flags, _stream(stream, x)))
+    return out
+
+
+MAX_SWITCH_WORKERS = 16
+
+
+def switch_aggregate(payloads, exps=None, numel: int | None = None, packet_numel: int = 256,
+                     payload_out=None, exps_out=None, out=None, flags: int = 0, stream=None):
+    """K6: the switch's per-slot aggregation over W worker planes, fused with
+    the dequantize (p4/processor.p4:48-54 wrapping bit<32> sum,
+    p4/exponents.p4:48-54 signed int8 max, then PostprocessSingle with
+    scale(W, e_max), ppp.cc:197-251).  `payloads`: W int32 planes of B*P
+    words (BE unless FLAG_PAYLOAD_LE); `exps`: W int8 planes of B bytes.
+    Writes whichever of payload_out / exps_out / out is given; with none
+    given, returns a new fp32 bucket `out` of `numel` elements."""
+    torch = _torch()
+    W = len(payloads)
+    if W == 0 or W > MAX_SWITCH_WORKERS:
+        raise ValueError(f"1 <= workers <= {MAX_SWITCH_WORKERS}, got {W}")
+    n_words = payloads[0].numel()
+    if any(p.numel() != n_words for p in payloads):
+        raise ValueError("payload planes differ in size")
+    if numel is None:
+        numel = n_words
+    B = num_blocks(numel, packet_numel)
+    if B * packet_numel != n_words:
+        raise ValueError(f"payload planes hold {n_words} words, B*P = {B * packet_numel}")
+    if exps is not None:
+        if len(exps) != W or any(e.numel() != B for e in exps):
+            raise ValueError("need one exponent plane of B bytes per payload plane")
+    if payload_out is None and exps_out is None and out is None:
+        out = torch.empty(numel, dtype=torch.float32, device=payloads[0].device)
+    pp = (ctypes.c_void_p * W)(*[_dev(p, torch.int32, "payloads[w]").value for p in payloads])
+    ep = None if exps is None else (ctypes.c_void_p * W)(*[_dev(e, torch.int8, "exps[w]").value for e in exps])
+    _check("sml_switch_aggregate", lib().sml_switch_aggregate(
+        ctypes.cast(pp, ctypes.c_void_p), None if ep is None else ctypes.cast(ep, ctypes.c_void_p), W, numel,
+        packet_numel,
+        None if payload_out is None else _dev(payload_out, torch.int32, "payload_out"),
+        None if exps_out is None else _dev(exps_out, torch.int8, "exps_out"),
+        None if out is None else _dev(out, torch.float32, "out"), flags, _stream(stream, payloads[0])))
     return out
 
 
