@@ -153,6 +153,16 @@ sml_status_t sml_switch_aggregate(const int32_t* const* d_payloads, const int8_t
                                   int32_t* d_payload_out, int8_t* d_exps_out, float* d_out,
                                   uint32_t flags, void* stream);
 
+/* Plane sharing for the peer-to-peer switch: export the allocation holding
+ * d_ptr as an IPC handle of sml_ipc_handle_bytes() bytes plus d_ptr's byte
+ * offset inside it; open a peer's handle in this process (returns the
+ * allocation base: add the offset; the mapping reaches the peer GPU's HBM
+ * over xGMI, peer access enabled on first use); close it again. */
+uint32_t sml_ipc_handle_bytes(void);
+sml_status_t sml_ipc_get_handle(const void* d_ptr, void* handle_out, uint64_t* offset_out);
+sml_status_t sml_ipc_open_handle(const void* handle, void** d_ptr_out);
+sml_status_t sml_ipc_close_handle(void* d_ptr);
+
 /* ---- DPDK/UDP wire frames --------------------------------
  * The DPDK backend builds one Ethernet frame per packet
  * (client_lib/src/backends/dpdk/dpdk_worker_thread_utils.inc:67-135,

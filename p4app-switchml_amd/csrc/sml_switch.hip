@@ -191,3 +191,38 @@ sml_status_t sml_switch_aggregate(const int32_t* const* d_payloads, const int8_t
 }
 
 }  // extern "C"
+
+// ---- plane sharing for the peer-to-peer switch (hipIpc*) ----------------
+extern "C" {
+
+uint32_t sml_ipc_handle_bytes(void) { return (uint32_t)sizeof(hipIpcMemHandle_t); }
+
+sml_status_t sml_ipc_get_handle(const void* d_ptr, void* handle_out, uint64_t* offset_out) {
+    if (!d_ptr || !handle_out || !offset_out) return SML_ERR_INVALID_ARG;
+    // the handle names the whole allocation (a caching allocator may have
+    // sub-allocated d_ptr from it): report where d_ptr lies inside it
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    sml_status_t s = hip_check(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)d_ptr));
+    if (s != SML_OK) return s;
+    hipIpcMemHandle_t h;
+    s = hip_check(hipIpcGetMemHandle(&h, (void*)base));
+    if (s != SML_OK) return s;
+    memcpy(handle_out, &h, sizeof(h));
+    *offset_out = (uint64_t)((const char*)d_ptr - (const char*)base);
+    return SML_OK;
+}
+
+sml_status_t sml_ipc_open_handle(const void* handle, void** d_ptr_out) {
+    if (!handle || !d_ptr_out) return SML_ERR_INVALID_ARG;
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    return hip_check(hipIpcOpenMemHandle(d_ptr_out, h, hipIpcMemLazyEnablePeerAccess));
+}
+
+sml_status_t sml_ipc_close_handle(void* d_ptr) {
+    if (!d_ptr) return SML_ERR_INVALID_ARG;
+    return hip_check(hipIpcCloseMemHandle(d_ptr));
+}
+
+}  // extern "C"

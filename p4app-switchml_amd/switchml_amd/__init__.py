@@ -118,6 +118,13 @@ def lib():
     L.sml_dequantize_frames.argtypes = [vp, u64, u64, u64, u32, u16, u32, u64, vp, vp, vp, vp, vp]
     L.sml_switch_aggregate.restype = i32
     L.sml_switch_aggregate.argtypes = [vp, vp, u16, u64, u32, vp, vp, vp, u32, vp]
+    L.sml_ipc_handle_bytes.restype = u32
+    L.sml_ipc_get_handle.restype = i32
+    L.sml_ipc_get_handle.argtypes = [vp, vp, ctypes.POINTER(u64)]
+    L.sml_ipc_open_handle.restype = i32
+    L.sml_ipc_open_handle.argtypes = [vp, ctypes.POINTER(vp)]
+    L.sml_ipc_close_handle.restype = i32
+    L.sml_ipc_close_handle.argtypes = [vp]
     _lib = L
     return L
 
@@ -316,7 +323,10 @@ def switch_aggregate(payloads, exps=None, numel: int | None = None, packet_numel
             raise ValueError("need one exponent plane of B bytes per payload plane")
     if payload_out is None and exps_out is None and out is None:
         out = torch.empty(numel, dtype=torch.float32, device=payloads[0].device)
-    pp = (ctypes.c_void_p * W)(*[_dev(p, torch.int32, "payloads[w]").value for p in payloads])
+    # planes are int32 tensors, or (peer-to-peer switch) mapped peer planes
+    # exposing data_ptr()/numel() only
+    pp = (ctypes.c_void_p * W)(*[_dev(p, torch.int32, "payloads[w]").value if isinstance(p, torch.Tensor)
+                                 else p.data_ptr() for p in payloads])
     ep = None if exps is None else (ctypes.c_void_p * W)(*[_dev(e, torch.int8, "exps[w]").value for e in exps])
     _check("sml_switch_aggregate", lib().sml_switch_aggregate(
         ctypes.cast(pp, ctypes.c_void_p), None if ep is None else ctypes.cast(ep, ctypes.c_void_p), W, numel,

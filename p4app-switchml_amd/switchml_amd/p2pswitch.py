@@ -1,0 +1,157 @@
+"""Peer-to-peer switch: W workers (one process per GPU) aggregate through
+each other's HBM over xGMI instead of through a ring all-reduce.
+
+The Tofino switch gives every worker the slot-wise wrapping sum of the W
+workers' payload words and the signed int8 max of their exponents
+(p4/processor.p4:48-54, p4/exponents.p4:48-54).  Here each worker keeps its
+BE payload plane (the wire words of its packets) in its own HBM, maps every
+peer's plane once (hipIpc handles, sml_ipc_*), and per all-reduce:
+
+  K2 exponents --all_reduce MAX (B bytes)--> global exps
+  K3 quantize with the global exps -> own BE payload plane        | barrier
+  K6 on this rank's shard of blocks: read the W peers' planes over xGMI,
+     wrapping sum + fused dequantize -> fp32 shard of `out`       | barrier
+  all_gather of the fp32 shards -> every rank holds the whole bucket
+
+So the payload exchange is one-shot over all point-to-point links at once:
+each rank pulls (W-1)/W of its shard's payload from the peers in parallel
+(every xGMI link busy), instead of the ring's 2(W-1) dependent steps.  The
+result is bit-identical to SwitchSimAllReduce (and to the oracle switch).
+
+Shards: block ranges of S = ceil(B / W) blocks, rank r owns blocks
+[r*S, min((r+1)*S, B)); `out` is padded to W*S*P elements internally so the
+all-gather moves equal shards.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _check, exponents, lib, num_blocks, quantize_pack, switch_aggregate
+
+
+def _handle_of(t: torch.Tensor):
+    L = lib()
+    buf = (ctypes.c_uint8 * L.sml_ipc_handle_bytes())()
+    off = ctypes.c_uint64()
+    _check("sml_ipc_get_handle", L.sml_ipc_get_handle(ctypes.c_void_p(t.data_ptr()), buf, ctypes.byref(off)))
+    return bytes(buf), off.value
+
+
+class _PeerPlane:
+    """A peer's int32 plane mapped into this process (a raw device pointer)."""
+
+    def __init__(self, handle: bytes, offset: int):
+        L = lib()
+        buf = (ctypes.c_uint8 * len(handle)).from_buffer_copy(handle)
+        base = ctypes.c_void_p()
+        _check("sml_ipc_open_handle", L.sml_ipc_open_handle(buf, ctypes.byref(base)))
+        self.base = base.value
+        self.ptr = base.value + offset
+
+    def close(self):
+        if self.base:
+            _check("sml_ipc_close_handle", lib().sml_ipc_close_handle(ctypes.c_void_p(self.base)))
+            self.base = None
+
+
+class _Ptr:
+    """Duck-typed int32 plane for switch_aggregate: a raw device pointer."""
+    dtype = torch.int32
+    is_cuda = True
+
+    def __init__(self, ptr: int, numel: int, device):
+        self._ptr, self._n, self.device = ptr, numel, device
+
+    def data_ptr(self):
+        return self._ptr
+
+    def numel(self):
+        return self._n
+
+    def is_contiguous(self):
+        return True
+
+    def is_pinned(self):
+        return False
+
+
+class PeerSwitchAllReduce:
+    """Reusable planes + peer mappings for repeated all-reduces of one bucket
+    size.  Needs one GPU per rank (or ranks sharing one GPU, for tests) and a
+    process group whose backend can all_reduce int8 and all_gather fp32
+    tensors on the device ("nccl" = RCCL); with "gloo" those two small /
+    final collectives go through host memory (CPU tests of the plumbing)."""
+
+    def __init__(self, numel: int, packet_numel: int = 256, device=None, group=None):
+        self.numel, self.P, self.group = numel, packet_numel, group
+        self.W = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.B = num_blocks(numel, packet_numel)
+        self.S = -(-self.B // self.W)
+        self.dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.host_collectives = dist.get_backend(group) == "gloo"
+        self.exps = torch.empty(self.B, dtype=torch.int8, device=self.dev)
+        self.payload = torch.empty(self.B * packet_numel, dtype=torch.int32, device=self.dev)
+        self.out_pad = torch.empty(self.W * self.S * packet_numel, dtype=torch.float32, device=self.dev)
+        torch.cuda.synchronize(self.dev)
+        mine = _handle_of(self.payload)
+        allh = [None] * self.W
+        dist.all_gather_object(allh, mine, group=group)
+        self.peers = {}
+        for w, (h, off) in enumerate(allh):
+            if w != self.rank:
+                self.peers[w] = _PeerPlane(h, off)
+        dist.barrier(group=group)
+
+    def _plane(self, w: int, blk0: int, nblk: int):
+        if w == self.rank:
+            return self.payload[blk0 * self.P:(blk0 + nblk) * self.P]
+        return _Ptr(self.peers[w].ptr + blk0 * self.P * 4, nblk * self.P, self.dev)
+
+    def _barrier(self):
+        torch.cuda.current_stream(self.dev).synchronize()
+        dist.barrier(group=self.group)
+
+    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if x.numel() != self.numel:
+            raise ValueError("bucket size changed; build a new PeerSwitchAllReduce")
+        if out is None:
+            out = torch.empty_like(x)
+        P, S = self.P, self.S
+        exponents(x, P, out=self.exps)                                          # K2
+        if self.host_collectives:
+            e = self.exps.cpu()
+            dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.group)
+            self.exps.copy_(e)
+        else:
+            dist.all_reduce(self.exps, op=dist.ReduceOp.MAX, group=self.group)  # switch: int8 max
+        quantize_pack(x, P, self.W, global_exps=self.exps, payload=self.payload)  # K3, BE wire words
+        self._barrier()                                                         # every plane written
+        blk0 = self.rank * S
+        nblk = max(0, min(S, self.B - blk0))
+        # gather straight into `out` when the shards tile it exactly
+        dst = out if out.numel() == self.W * S * P and out.is_contiguous() else self.out_pad
+        shard = dst[self.rank * S * P:(self.rank + 1) * S * P]
+        if nblk:
+            n_el = min(nblk * P, self.numel - blk0 * P)
+            planes = [self._plane(w, blk0, nblk) for w in range(self.W)]
+            ex = self.exps[blk0:blk0 + nblk]
+            switch_aggregate(planes, [ex] * self.W, n_el, P, out=shard[:n_el])  # K6 over xGMI
+        self._barrier()                                                         # peers done reading
+        if self.host_collectives:
+            parts = [torch.empty(S * P, dtype=torch.float32) for _ in range(self.W)]
+            dist.all_gather(parts, shard.cpu(), group=self.group)
+            dst.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(dst, shard, group=self.group)
+        if dst is not out:
+            out.copy_(dst[:self.numel])
+        return out
+
+    def close(self):
+        for p in self.peers.values():
+            p.close()
+        self.peers = {}
