@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--extra", action="store_true", help="also time dequantize / fused round trip / copy")
+    ap.add_argument("--p2p", action="store_true",
+                    help="N > 1: also time the peer-to-peer switch (K6 over the peers' HBM, hipIpc)")
     ap.add_argument("--graph-steps", type=int, default=1,
                     help="capture this many steps per hipGraph replay (1 = eager launches)")
     return ap.parse_args()
@@ -242,6 +244,16 @@ def main():
             extra["switchsim"] = switchsim_measure(sw, torch, dist, x, N, P, world, dev)
         except Exception as e:  # reported, never fatal to the headline line
             extra["switchsim"] = {"error": repr(e)[:300]}
+        if args.p2p and world > 1:
+            # peer-to-peer switch (opt-in): K6 reads the peers' planes over xGMI
+            try:
+                from switchml_amd.p2pswitch import PeerSwitchAllReduce
+                extra["p2p_switch"] = switchsim_measure(
+                    sw, torch, dist, x, N, P, world, dev, cls=PeerSwitchAllReduce,
+                    pipeline="K2 exps -> all_reduce(int8, MAX) -> K3 BE payload -> K6 over peers' planes "
+                             "(hipIpc, xGMI) on this rank's block shard -> all_gather(fp32)")
+            except Exception as e:
+                extra["p2p_switch"] = {"error": repr(e)[:300]}
     if args.extra and rank == 0:
         extra.update(extra_measurements(sw, torch, x, payload, exps, N, P, stream))
 
@@ -299,13 +311,15 @@ def main():
         dist.destroy_process_group()
 
 
-def switchsim_measure(sw, torch, dist, x, N, P, world, dev, reps=5):
-    """Time the switch-sim all-reduce of the same 256 MiB bucket per GPU
-    (switchml_amd/switchsim.py); max over ranks.  algbw = 4N / t."""
+def switchsim_measure(sw, torch, dist, x, N, P, world, dev, reps=5, cls=None,
+                      pipeline="K2 exps -> all_reduce(int8, MAX) -> K3 LE payload -> all_reduce(int32, SUM) -> K4"):
+    """Time a switch-sim all-reduce of the same 256 MiB bucket per GPU
+    (switchml_amd/switchsim.py, or the peer-to-peer switch); max over ranks.
+    algbw = 4N / t."""
     from switchml_amd.switchsim import SwitchSimAllReduce
     if world == 1 and not dist.is_initialized():
         return {"note": "single rank: no exchange to time"}
-    ar = SwitchSimAllReduce(N, P, dev)
+    ar = (cls or SwitchSimAllReduce)(N, P, dev)
     out = torch.empty_like(x)
     ar(x, out)
     torch.cuda.synchronize()
@@ -317,8 +331,10 @@ def switchsim_measure(sw, torch, dist, x, N, P, world, dev, reps=5):
     t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t = float(t[0])
+    if hasattr(ar, "close"):
+        ar.close()
     return {"workers": world, "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * N / t / 1e9, 2),
-            "pipeline": "K2 exps -> all_reduce(int8, MAX) -> K3 LE payload -> all_reduce(int32, SUM) -> K4"}
+            "pipeline": pipeline}
 
 
 def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
