@@ -15,6 +15,11 @@
 // Bit-identical to orc_switch_payload / orc_switch_exps followed by K4.
 #include "sml_host.h"
 
+// Planes whose loads are issued together per loop trip (A/B knob).
+#ifndef SML_SWITCH_UNROLL
+#define SML_SWITCH_UNROLL 2
+#endif
+
 namespace sml {
 
 struct SwitchArgs {
@@ -50,6 +55,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_switch_aggregate(SwitchArgs a
         u4 acc[kU];
 #pragma unroll
         for (int u = 0; u < kU; u++) acc[u] = mku4(0, 0, 0, 0);
+#pragma unroll SML_SWITCH_UNROLL
         for (uint32_t w = 0; w < a.nw; w++) {
             u4 v[kU];
 #pragma unroll
