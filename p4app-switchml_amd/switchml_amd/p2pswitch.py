@@ -152,6 +152,10 @@ class PeerSwitchAllReduce:
         return out
 
     def close(self):
+        """Unmap the peers' planes; collective (every rank calls it), so no
+        rank frees its own plane while a peer still has it mapped."""
+        torch.cuda.current_stream(self.dev).synchronize()
         for p in self.peers.values():
             p.close()
         self.peers = {}
+        dist.barrier(group=self.group)
