@@ -16,24 +16,28 @@ std::atomic<uint32_t> g_xcd_chunk{64};
 
 // -------------------------------------------------------------- kernels
 
-// Exponents, quantize and pack of one loaded tile.
+// K3: the tile's global exponents (one scalar load per slice when aligned).
+template <int P>
+__device__ __forceinline__ void global_tile_exponents(const QuantArgs& a, uint64_t base, int lane, int (&e)[kU]) {
+    if (base + kTileElems <= a.nblocks * P && slice_exps_scalar_ok<P>(a.gexp)) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) e[u] = (int)(int8_t)slice_exponent_byte<P>(a.gexp, base, u, lane);
+    } else {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            uint64_t pkt = (base + (uint64_t)(u * kWave + lane) * 4) / P;
+            e[u] = pkt < a.nblocks ? (int)a.gexp[pkt] : 0;
+        }
+    }
+}
+
+// Exponents, quantize and pack of one loaded tile (K3: `e` holds the global
+// exponents already).
 template <int P, bool GLOBAL, bool BE, bool RNE>
 __device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, int lane, const f4 (&v)[kU],
-                                           const float* lut) {
+                                           const float* lut, int (&e)[kU]) {
     const uint64_t padded = a.nblocks * P;
-    int e[kU];
-    if constexpr (GLOBAL) {
-        if (base + kTileElems <= padded && slice_exps_scalar_ok<P>(a.gexp)) {
-#pragma unroll
-            for (int u = 0; u < kU; u++) e[u] = (int)(int8_t)slice_exponent_byte<P>(a.gexp, base, u, lane);
-        } else {
-#pragma unroll
-            for (int u = 0; u < kU; u++) {
-                uint64_t pkt = (base + (uint64_t)(u * kWave + lane) * 4) / P;
-                e[u] = pkt < a.nblocks ? (int)a.gexp[pkt] : 0;
-            }
-        }
-    } else {
+    if constexpr (!GLOBAL) {
         tile_exponents<P>(v, e);
         if (a.exps_out) {
             constexpr int kPk = kTileElems / P;   // packets per tile
@@ -76,12 +80,20 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
     const uint64_t wave = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
     for (uint64_t t = wave * TPW; t < a.ntiles; t += nwaves * TPW) {
         f4 v[TPW][kU];
+        int e[TPW][kU];
 #pragma unroll
         for (int k = 0; k < TPW; k++)
             if (k == 0 || t + k < a.ntiles) load_tile<ALIGNED>(a, (t + k) * kTileElems, lane, v[k]);
+        // K3: the exponent dword is read after the data loads are in flight
+        // (read first, the compiler waits on it before issuing them: asm)
+        if constexpr (GLOBAL) {
+#pragma unroll
+            for (int k = 0; k < TPW; k++)
+                if (k == 0 || t + k < a.ntiles) global_tile_exponents<P>(a, (t + k) * kTileElems, lane, e[k]);
+        }
 #pragma unroll
         for (int k = 0; k < TPW; k++)
-            if (k == 0 || t + k < a.ntiles) quant_tile<P, GLOBAL, BE, RNE>(a, (t + k) * kTileElems, lane, v[k], lut);
+            if (k == 0 || t + k < a.ntiles) quant_tile<P, GLOBAL, BE, RNE>(a, (t + k) * kTileElems, lane, v[k], lut, e[k]);
     }
 }
 
