@@ -32,6 +32,14 @@ import torch.distributed as dist
 from . import _check, exponents, lib, num_blocks, quantize_pack, switch_aggregate
 
 
+def shard_blocks(num_blocks: int, world: int, rank: int) -> tuple[int, int]:
+    """(first block, block count) of `rank`'s shard: S = ceil(B / W) blocks
+    per rank, the last shards shorter or empty."""
+    S = -(-num_blocks // world)
+    blk0 = min(rank * S, num_blocks)
+    return blk0, max(0, min(S, num_blocks - blk0))
+
+
 def _handle_of(t: torch.Tensor):
     L = lib()
     buf = (ctypes.c_uint8 * L.sml_ipc_handle_bytes())()
@@ -130,8 +138,7 @@ class PeerSwitchAllReduce:
             dist.all_reduce(self.exps, op=dist.ReduceOp.MAX, group=self.group)  # switch: int8 max
         quantize_pack(x, P, self.W, global_exps=self.exps, payload=self.payload)  # K3, BE wire words
         self._barrier()                                                         # every plane written
-        blk0 = self.rank * S
-        nblk = max(0, min(S, self.B - blk0))
+        blk0, nblk = shard_blocks(self.B, self.W, self.rank)
         # gather straight into `out` when the shards tile it exactly
         dst = out if out.numel() == self.W * S * P and out.is_contiguous() else self.out_pad
         shard = dst[self.rank * S * P:(self.rank + 1) * S * P]

@@ -224,3 +224,16 @@ def test_sharding_mode_ranks_one_gpu(cuda, world):
         p.join(timeout=60)
     for rank, ok, err in res:
         assert ok, (rank, err)
+
+
+@pytest.mark.parametrize("B,world", [(1, 2), (7, 3), (262144, 8), (5, 8), (1025, 4)])
+def test_p2p_shards_tile_the_blocks(B, world):
+    """Peer-to-peer switch shards: disjoint, in rank order, covering [0, B)."""
+    from switchml_amd.p2pswitch import shard_blocks
+    nxt = 0
+    for r in range(world):
+        b0, n = shard_blocks(B, world, r)
+        assert n >= 0 and (n == 0 or b0 == nxt)
+        nxt += n
+        assert n <= -(-B // world)
+    assert nxt == B
