@@ -29,7 +29,7 @@ import ctypes
 import torch
 import torch.distributed as dist
 
-from . import _check, exponents, lib, num_blocks, quantize_pack, switch_aggregate
+from . import _check, bswap_i32, exponents, lib, num_blocks, quantize_pack, switch_aggregate
 
 
 def shard_blocks(num_blocks: int, world: int, rank: int) -> tuple[int, int]:
@@ -124,32 +124,49 @@ class PeerSwitchAllReduce:
         dist.barrier(group=self.group)
 
     def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """All-reduce (SUM) of a FLOAT32 bucket (quantized, as the exponent
+        quantizer PPP does) or an INT32 bucket (byte order only: ppp.cc:158-190,
+        262-298; no exponents, no extra batch)."""
         if x.numel() != self.numel:
             raise ValueError("bucket size changed; build a new PeerSwitchAllReduce")
+        if x.dtype not in (torch.float32, torch.int32):
+            raise TypeError("FLOAT32 or INT32 buckets only (common.h:51-55)")
         if out is None:
             out = torch.empty_like(x)
+        if out.dtype != x.dtype:
+            raise TypeError("out must have the bucket's dtype")
         P, S = self.P, self.S
-        exponents(x, P, out=self.exps)                                          # K2
-        if self.host_collectives:
-            e = self.exps.cpu()
-            dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.group)
-            self.exps.copy_(e)
+        is_int = x.dtype == torch.int32
+        if is_int:
+            bswap_i32(x, out=self.payload[:self.numel])                         # INT32 PPP: wire words
         else:
-            dist.all_reduce(self.exps, op=dist.ReduceOp.MAX, group=self.group)  # switch: int8 max
-        quantize_pack(x, P, self.W, global_exps=self.exps, payload=self.payload)  # K3, BE wire words
+            exponents(x, P, out=self.exps)                                      # K2
+            if self.host_collectives:
+                e = self.exps.cpu()
+                dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.group)
+                self.exps.copy_(e)
+            else:
+                dist.all_reduce(self.exps, op=dist.ReduceOp.MAX, group=self.group)  # switch: int8 max
+            quantize_pack(x, P, self.W, global_exps=self.exps, payload=self.payload)  # K3, BE wire words
         self._barrier()                                                         # every plane written
         blk0, nblk = shard_blocks(self.B, self.W, self.rank)
         # gather straight into `out` when the shards tile it exactly
-        dst = out if out.numel() == self.W * S * P and out.is_contiguous() else self.out_pad
+        pad = self.out_pad.view(torch.int32) if is_int else self.out_pad
+        dst = out if out.numel() == self.W * S * P and out.is_contiguous() else pad
         shard = dst[self.rank * S * P:(self.rank + 1) * S * P]
         if nblk:
             n_el = min(nblk * P, self.numel - blk0 * P)
             planes = [self._plane(w, blk0, nblk) for w in range(self.W)]
-            ex = self.exps[blk0:blk0 + nblk]
-            switch_aggregate(planes, [ex] * self.W, n_el, P, out=shard[:n_el])  # K6 over xGMI
+            if is_int:
+                # the switch's wrapping sum of the BE words, then ntohl
+                switch_aggregate(planes, None, nblk * P, P, payload_out=shard[:nblk * P])
+                bswap_i32(shard[:n_el], out=shard[:n_el])
+            else:
+                ex = self.exps[blk0:blk0 + nblk]
+                switch_aggregate(planes, [ex] * self.W, n_el, P, out=shard[:n_el])  # K6 over xGMI
         self._barrier()                                                         # peers done reading
         if self.host_collectives:
-            parts = [torch.empty(S * P, dtype=torch.float32) for _ in range(self.W)]
+            parts = [torch.empty(S * P, dtype=dst.dtype) for _ in range(self.W)]
             dist.all_gather(parts, shard.cpu(), group=self.group)
             dst.copy_(torch.cat(parts))
         else:

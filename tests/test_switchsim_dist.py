@@ -146,6 +146,42 @@ def _gpu_p2p(rank, world, port, n, P, q):
         q.put((rank, False, repr(ex)))
 
 
+def _gpu_p2p_int32(rank, world, port, n, P, q):
+    try:
+        dist = _init(rank, world, port)
+        from switchml_amd.p2pswitch import PeerSwitchAllReduce
+        dev = torch.device("cuda:0")
+        xs = [np.random.default_rng(77 + r).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+              for r in range(world)]
+        # INT32 jobs: htonl per word, the switch's wrapping bit<32> sum, ntohl (ppp.cc:158-190, 262-298)
+        ref = O.bswap32(O.switch_payload([O.bswap32(xx) for xx in xs]))
+        ar = PeerSwitchAllReduce(n, P, dev)
+        out = ar(torch.from_numpy(xs[rank]).to(dev))
+        ok = np.array_equal(out.cpu().numpy().view(np.uint32), ref)
+        ar.close()
+        q.put((rank, ok, ""))
+        dist.destroy_process_group()
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, False, repr(ex)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n,P", [(2, 100_003, 256), (3, 4 * 1024 * 64 * 3, 64)])
+def test_p2p_switch_int32_ranks_one_gpu(cuda, world, n, P):
+    """INT32 buckets through the peer-to-peer switch: wrapping sum, bit-exact."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_p2p_int32, args=(r, world, port, n, P, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, err in res:
+        assert ok, (rank, err)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,n,P", [(2, 100_003, 256), (3, 100_003, 64), (2, 4 * 1024 * 256, 256),
                                        (4, 77_777, 1024)])
