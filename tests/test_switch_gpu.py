@@ -68,6 +68,22 @@ def test_switch_aggregate_matches_oracle(P, W):
     assert float_bits_equal_nan_ok(host(o), out)
 
 
+@pytest.mark.parametrize("P", (64, 256))
+def test_switch_aggregate_max_workers(P):
+    """SML_MAX_SWITCH_WORKERS (16) planes, fused dequantize, W = 16 scale."""
+    import torch
+    dev = torch.device("cuda:0")
+    W, n = 16, 5 * 1024 + 33
+    _, gexp, pls = worker_planes(W, n, P, seed=16 + P)
+    exps = [gexp] * W
+    agg, e, out = oracle_switch(pls, exps, n, P, W)
+    d_pl = [to_dev(p.view(np.int32), dev) for p in pls]
+    d_ex = [to_dev(gexp, dev)] * W
+    o = sw().switch_aggregate(d_pl, d_ex, n, P)
+    torch.cuda.synchronize()
+    assert float_bits_equal_nan_ok(host(o), out)
+
+
 @pytest.mark.parametrize("W", (2, 5, 16))
 def test_switch_aggregate_le_payload_only(W):
     """LE words (SML_FLAG_PAYLOAD_LE), payload only, in place into plane 0."""
