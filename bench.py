@@ -4,26 +4,36 @@
 
 One step = one pass of the hot path (CpuExponentQuantizerPPP's
 PreprocessSingle over a whole job slice: per-packet exponent, fp32->int32
-scale+round, big-endian pack — ppp.cc:69-156) over one 256 MiB fp32 bucket
-that is already resident in HBM, as one launch of the fused HIP kernel
-sml_quantize_pack (K1).  Exponents are the loopback's (the dummy backend
-returns them unchanged, so the local exponent is the global one: W = 1).
+scale+round, big-endian pack — ppp.cc:69-156) over fp32 data already resident
+in HBM, as one launch of the fused HIP kernel sml_quantize_pack (K1) per GPU.
+Exponents are the loopback's (the dummy backend returns them unchanged, so
+the local exponent is the global one: W = 1).
 
-Multi-GPU (launched by torch.distributed.run): "sharding mode" — every rank
-owns its own 256 MiB slice of a G x 256 MiB job (FifoScheduler slicing,
-fifo_scheduler.cc:93-109, slice g -> GPU g); the path has no exchange step
-at W = 1, so there is no collective in the timed region (weak scaling).
-value = all ranks' algorithmic bytes / max-over-ranks time.
+N = 1 (default): the step is K1 over one 256 MiB bucket (configs[2]'s bucket).
+N > 1 (`--gpus N`; the N ranks are started here when WORLD_SIZE is unset, or
+by torch.distributed.run): the step is configs[3] — ONE 1 GiB job split over
+the N GPUs by the FIFO rule (fifo_scheduler.cc:93-109, slice g -> GPU g); the
+path has no exchange step at W = 1, so no collective runs in the timed region
+(strong scaling: total work fixed).  Beside it, first-class fields time the
+switch simulation with W = N real workers (each holding its own 1 GiB bucket):
+  switchsim   K2 -> RCCL int8 MAX -> K3 -> RCCL int32 SUM -> K4 (ring, xGMI)
+  p2p_switch  K2 -> RCCL int8 MAX -> K3 -> K6 over the peers' HBM (hipIpc,
+              xGMI) on this rank's block shard -> RCCL all_gather (fp32)
+each checked (bit-equal to each other, and within the quantization bound of
+an fp32 all-reduce of the same buckets) and set against its xGMI bound.  A
+failed check or an exception exits non-zero.
 
 Units: value / roofline.achieved = ALGORITHMIC bytes per second: 4N read
 (fp32 in) + 4N written (int32 payload) + B written (int8 exponents),
-B = N/256 — see DESIGN.md §4.  input_GBps = 4N / t is reported alongside.
+B = ceil(N/256) per slice — see DESIGN.md §4.  input_GBps = 4N / t alongside.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,10 +41,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+XGMI_LINK_GBPS = 153.0   # per xGMI link and direction; 7 links per GPU, one to each peer of an 8-GPU node
+CFG3_JOB_NUMEL = 268_435_456   # configs[3]: 1 GiB fp32 (also allreduce_benchmark's default tensor-numel, main.cc:101)
+METRIC = "fp32→int32 quantize+pack GB/s (device-resident), 256 MiB bucket, 1/2/4/8 GPU"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -42,37 +55,71 @@ def parse():
     ap.add_argument("--settle-ms", type=float, default=50.0,
                     help="untimed launches of the same step for this long before the warmup steps "
                          "(HBM/fabric clocks ramp under load: profiles/r01/bench_warmup_sweep.jsonl)")
-    ap.add_argument("--numel", type=int, default=64 * 1024 * 1024, help="fp32 elements per GPU (256 MiB)")
+    ap.add_argument("--numel", type=int, default=64 * 1024 * 1024, help="fp32 elements per GPU at N=1 (256 MiB)")
     ap.add_argument("--packet-numel", type=int, default=256)
-    ap.add_argument("--job-numel", type=int, default=0,
+    ap.add_argument("--job-numel", type=int, default=-1,
                     help="strong scaling: one job of this many fp32 elements split over the ranks by the FIFO "
-                         "rule (configs[3]: 268435456 = 1 GiB); 0 = --numel per GPU (weak scaling, default)")
+                         "rule; -1 = configs[3]'s 268435456 (1 GiB) when N > 1, --numel per GPU when N = 1; "
+                         "0 = --numel per GPU (weak scaling) at any N")
+    ap.add_argument("--switch-numel", type=int, default=CFG3_JOB_NUMEL,
+                    help="N > 1: fp32 elements per worker for the switchsim / p2p_switch fields (0 = skip them)")
+    ap.add_argument("--buckets", type=int, default=1,
+                    help="distinct input buckets (and output planes) the timed steps cycle through: 1 = one "
+                         "resident bucket (the headline); >= 4 streams past the 256 MiB Infinity Cache (cold HBM)")
     ap.add_argument("--grid-limit", type=int, default=0, help="workgroups per launch (0 = one per 4 tiles)")
     ap.add_argument("--xcd-chunk", type=int, default=64,
                     help="workgroups per contiguous run on one XCD (0 = plain blockIdx order)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-side", action="store_true", help="skip the cold-HBM and 1 GiB single-GPU side fields")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
-    ap.add_argument("--extra", action="store_true", help="also time dequantize / fused round trip / copy")
-    ap.add_argument("--p2p", action="store_true",
-                    help="N > 1: also time the peer-to-peer switch (K6 over the peers' HBM, hipIpc)")
+    ap.add_argument("--extra", action="store_true", help="also time dequantize / fused round trip / copy / plugin")
     ap.add_argument("--graph-steps", type=int, default=1,
                     help="capture this many steps per hipGraph replay (1 = eager launches)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def load_traffic(numel, P):
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N rank processes with
+    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) as CHILD
+    processes and exit with their status.  Runs before anything touches the
+    GPU (no exec from a GPU-initialised process)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def load_traffic(numel, P, key="quantize_pack"):
     """HBM bytes per launch from the PMC passes (profiles/pmc_traffic.json,
     written by profiles/collect_pmc.py from separate rocprofv3 --pmc runs)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        k = d.get("quantize_pack", {})
+        k = d.get(key, {})
         if k.get("numel") == numel and k.get("packet_numel") == P:
             return k.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     return None
+
+
+def host_cores():
+    """CPU threads this process may run on (its affinity mask), and the
+    lease's own share as the box announces it (OMP_NUM_THREADS)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    return aff, share
 
 
 def cpu_baseline(numel, P, budget_s):
@@ -82,13 +129,14 @@ def cpu_baseline(numel, P, budget_s):
 
     `value` is the reference's DEFAULT build, VCL=1 (client_lib/Makefile:26,
     113-120): its 16-element vector loops restated with SSE2 intrinsics — the
-    instruction set that build targets (no -m flags) — on all cores used.  The
-    scalar VCL=0 path (roundf per element) is reported beside it."""
+    instruction set that build targets (no -m flags) — with one worker thread
+    per core of this process's affinity mask.  The lease's announced share
+    (OMP_NUM_THREADS), the reference's default 4 worker threads, 1 thread, and
+    the scalar VCL=0 path (roundf per element) are reported beside it."""
     import numpy as np
     from oracle import oracle as O
 
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    cores = max(1, min(cores, 16))
+    aff, share = host_cores()
     x = O.splitmix_normal(42, numel)
     out = np.empty_like(x)
     alg = 8 * numel + O.num_blocks(numel, P)
@@ -97,17 +145,18 @@ def cpu_baseline(numel, P, budget_s):
         rates, t_end, reps = [], time.perf_counter() + deadline_s, 0
         while reps < min_reps or time.perf_counter() < t_end:
             t0 = time.perf_counter()
-            O.dummy_allreduce(x, P=P, max_outstanding_packets=256, num_worker_threads=T,
+            O.dummy_allreduce(x, P=P, max_outstanding_packets=max(256, 4 * T), num_worker_threads=T,
                               num_workers=1, threaded=T > 1, mode=O.MODE_PREPROCESS, out=out, vcl=vcl)
             rates.append(alg / (time.perf_counter() - t0) / 1e9)
             reps += 1
         return float(np.median(rates)), reps
 
-    multi, repsT = run(cores, budget_s * 0.35, 3, True)
-    four, reps4 = run(4, budget_s * 0.1, 3, True) if cores > 4 else (None, 0)
-    single, reps1 = run(1, budget_s * 0.1, 2, True)
-    s_multi, s_repsT = run(cores, budget_s * 0.25, 3, False)
-    s_single, s_reps1 = run(1, budget_s * 0.2, 2, False)
+    multi, repsT = run(aff, budget_s * 0.3, 3, True)
+    sh = run(share, budget_s * 0.1, 3, True)[0] if share and share != aff else None
+    four = run(4, budget_s * 0.1, 3, True)[0] if aff > 4 else None
+    single = run(1, budget_s * 0.1, 2, True)[0]
+    s_multi = run(aff, budget_s * 0.2, 3, False)[0]
+    s_single = run(1, budget_s * 0.2, 2, False)[0]
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -117,14 +166,17 @@ def cpu_baseline(numel, P, budget_s):
     return {
         "value": round(multi, 3),
         "unit": "GB/s (8N+B algorithmic bytes, same as value)",
-        "cores": cores,
+        "cores": aff,
         "kind": "port",
         "sample": (f"oracle/sml_oracle.c restatement of CpuExponentQuantizerPPP as the reference builds it by "
                    f"default (VCL=1, vector loops in SSE2), driven in DummyWorkerThread order, PreprocessSingle "
                    f"only (exponent + quantize + BE pack into the b-packet ring), the full {numel * 4 >> 20} MiB "
-                   f"bucket, packet_numel {P}, max_outstanding_packets 256; {cores} worker threads x {repsT} reps "
-                   f"(median); 1 thread: {single:.3f} GB/s; scalar VCL=0 build: {s_multi:.3f} GB/s on {cores} "
-                   f"threads, {s_single:.3f} on 1; host CPU {model}"),
+                   f"bucket, packet_numel {P}; {aff} worker threads (= this process's CPU affinity mask) x {repsT} "
+                   f"reps (median); lease share OMP_NUM_THREADS={share}: {sh}; 1 thread: {single:.3f} GB/s; "
+                   f"scalar VCL=0 build: {s_multi:.3f} GB/s on {aff} threads, {s_single:.3f} on 1; host CPU {model}"),
+        "cores_source": "len(os.sched_getaffinity(0))",
+        "lease_share_threads": share,
+        "lease_share_value": None if sh is None else round(sh, 3),
         "single_thread_value": round(single, 3),
         "ref_default_4_threads_value": None if four is None else round(four, 3),
         "vcl0_scalar_value": round(s_multi, 3),
@@ -134,13 +186,24 @@ def cpu_baseline(numel, P, budget_s):
     }
 
 
+class Fail(RuntimeError):
+    """A check of the run failed: the line is still printed, the exit status is 1."""
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+        world = 1
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
+
     import torch
     import torch.distributed as dist
     import switchml_amd as sw
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # SML_BENCH_REHEARSE=1: rehearse the N>1 path on a 1-GPU box (all ranks on
@@ -161,49 +224,46 @@ def main():
     sw.set_xcd_chunk(args.xcd_chunk)
 
     P = args.packet_numel
-    if args.job_numel:
+    job_numel = args.job_numel if args.job_numel >= 0 else (CFG3_JOB_NUMEL if world > 1 else 0)
+    if job_numel:
         # configs[3]: one job sharded over the ranks, slice g -> GPU g (fifo_scheduler.cc:93-109)
-        N = sw.fifo_slice(args.job_numel, world, rank)[1]
+        N = sw.fifo_slice(job_numel, world, rank)[1]
         total_alg = sum(8 * n + sw.num_blocks(n, P)
-                        for n in (sw.fifo_slice(args.job_numel, world, r)[1] for r in range(world)))
+                        for n in (sw.fifo_slice(job_numel, world, r)[1] for r in range(world)))
     else:
         N = args.numel
         total_alg = world * (8 * N + sw.num_blocks(N, P))
     B = sw.num_blocks(N, P)
+    alg_bytes = 8 * N + B
+    stream = torch.cuda.current_stream()
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
-    x = torch.randn(N, dtype=torch.float32, device=dev, generator=gen)
-    payload = torch.empty(B * P, dtype=torch.int32, device=dev)
-    exps = torch.empty(B, dtype=torch.int8, device=dev)
-    stream = torch.cuda.current_stream()
-    alg_bytes = 8 * N + B
+    nb = max(1, args.buckets)
+    xs = [torch.randn(N, dtype=torch.float32, device=dev, generator=gen) for _ in range(nb)]
+    pls = [torch.empty(B * P, dtype=torch.int32, device=dev) for _ in range(nb)]
+    exs = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nb)]
+    x, payload, exps = xs[0], pls[0], exs[0]
+    cyc = [0]
 
     def launch():
-        sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=torch.cuda.current_stream())
+        i = cyc[0]
+        cyc[0] = (i + 1) % nb
+        sw.quantize_pack(xs[i], P, 1, payload=pls[i], exps_out=exs[i], stream=stream)
 
     step, per_call = launch, 1
     if args.graph_steps > 1:
-        # G consecutive steps captured into one hipGraph (G kernel nodes, the
-        # same launch each time): the Python/ctypes launch path leaves the
-        # timed loop; each replay still runs exactly G full steps.
+        # G consecutive steps captured into one hipGraph (G kernel nodes);
+        # each replay still runs exactly G full steps.
         launch()
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, stream=stream):
             for _ in range(args.graph_steps):
                 launch()
         step, per_call = graph.replay, args.graph_steps
         assert args.steps % per_call == 0 and args.warmup % per_call == 0, "steps/warmup must be multiples of --graph-steps"
 
-    # Clock settle: the first ~20-40 ms of streaming after idle run ~4 % slower
-    # (warmup 10 -> 78-79 us per launch, >= 500 -> 76 us); run the same step
-    # untimed for settle_ms first so the K timed steps see steady-state clocks
-    # whatever W the caller passes.
-    t_settle = time.perf_counter() + args.settle_ms * 1e-3
-    while time.perf_counter() < t_settle:
-        for _ in range(10):
-            step()
-        torch.cuda.synchronize()
+    settle(step, args.settle_ms)
     for _ in range(args.warmup // per_call):
         step()
     torch.cuda.synchronize()
@@ -212,8 +272,7 @@ def main():
     # and a device sync on both sides (wall clock -> value), and by two HIP
     # events recorded on the launch stream itself (-> average launch duration
     # for the roofline; includes the inter-launch gaps, so it is conservative
-    # against rocprofv3's per-dispatch durations).  Per-launch event pairs
-    # were measured to add ~4 us per launch and are not used.
+    # against rocprofv3's per-dispatch durations).
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
@@ -235,34 +294,43 @@ def main():
 
     # sanity: the timed output is the HIP kernel's and it is deterministic
     ok = bool(torch.equal(exps[:4].cpu(), sw.exponents(x[:4 * P], P).cpu()))
+    ok_t = torch.tensor([int(ok)], dtype=torch.int32, device=dev)
+    if world > 1:
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+    ok = bool(ok_t.item())
+    del xs, pls, exs, x, payload, exps
 
-    extra = {}
-    if world > 1 or args.extra:
-        # Switch-sim mode (not the headline): W = world workers all-reduce their
-        # buckets through K2 -> RCCL int8 MAX -> K3 -> RCCL int32 SUM -> K4.
+    failures = [] if ok else ["self_check: K1 exponent plane != K2 exponents"]
+    side, fields = {}, {}
+    if world == 1 and not args.no_side:
+        side["cold_hbm"] = cold_measure(sw, torch, args.numel, P, stream)
+        side["configs3_1gpu"] = job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev)
+    if world > 1 and args.switch_numel:
         try:
-            extra["switchsim"] = switchsim_measure(sw, torch, dist, x, N, P, world, dev)
-        except Exception as e:  # reported, never fatal to the headline line
-            extra["switchsim"] = {"error": repr(e)[:300]}
-        if args.p2p and world > 1:
-            # peer-to-peer switch (opt-in): K6 reads the peers' planes over xGMI
-            try:
-                from switchml_amd.p2pswitch import PeerSwitchAllReduce
-                extra["p2p_switch"] = switchsim_measure(
-                    sw, torch, dist, x, N, P, world, dev, cls=PeerSwitchAllReduce,
-                    pipeline="K2 exps -> all_reduce(int8, MAX) -> K3 BE payload -> K6 over peers' planes "
-                             "(hipIpc, xGMI) on this rank's block shard -> all_gather(fp32)")
-            except Exception as e:
-                extra["p2p_switch"] = {"error": repr(e)[:300]}
+            fields = exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev)
+        except Exception as e:  # noqa: BLE001 - recorded, then the run fails
+            fields = {"switchsim": {"error": repr(e)[:400]}}
+        for k in ("switchsim", "p2p_switch"):
+            f = fields.get(k, {})
+            if "error" in f or not f.get("verified", False):
+                failures.append(f"{k}: {f.get('error', 'not verified')}")
+    extra = {}
     if args.extra and rank == 0:
-        extra.update(extra_measurements(sw, torch, x, payload, exps, N, P, stream))
+        extra.update(extra_measurements(sw, torch, torch.randn(args.numel, device=dev, generator=gen), P, stream))
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
         value = total_alg / (elapsed / args.steps) / 1e9
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
+        if job_numel:
+            workload = (f"configs[3]: one {job_numel * 4 >> 20} MiB fp32 job sharded over {world} GPU(s) by the FIFO "
+                        f"rule ({N} elements on rank 0), fused exponent+quantize+BE pack (sml_quantize_pack, K1), "
+                        "loopback exponents (W=1)")
+        else:
+            workload = (f"configs[2]-sized bucket: {N * 4 >> 20} MiB fp32 per GPU, fused exponent+quantize+BE pack "
+                        "(sml_quantize_pack, K1), loopback exponents (W=1)")
         line = {
-            "metric": "fp32→int32 quantize+pack GB/s (device-resident), 256 MiB bucket, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -271,25 +339,23 @@ def main():
             "settle_ms": args.settle_ms,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "strong" if args.job_numel else "weak",
+            "scaling": "strong" if job_numel else "weak",
             "vs_baseline": None,
             "dtype": "f32->i32",
             "data": "synthetic N(0,1) fp32 (torch.randn on device, seed 42+rank)",
             "config": {
-                "workload": (f"configs[3]-style job: {args.job_numel * 4 >> 20} MiB fp32 sharded over {world} GPU(s) "
-                             "by the FIFO rule, fused exponent+quantize+BE pack (sml_quantize_pack, K1), loopback "
-                             "exponents (W=1)") if args.job_numel else
-                            ("configs[2]-sized bucket: 256 MiB fp32 per GPU, fused exponent+quantize+BE pack "
-                             "(sml_quantize_pack, K1), loopback exponents (W=1)"),
+                "workload": workload,
+                "job_numel": job_numel or world * N,
                 "numel_per_gpu": N,
                 "packet_numel": P,
                 "num_blocks_per_gpu": B,
                 "parallelism": f"shard{world} (FIFO slices, no data-path collective)",
                 "bytes_per_step_per_gpu": alg_bytes,
+                "buckets_cycled": nb,
                 "xcd_chunk": args.xcd_chunk,
                 "launch": "eager" if args.graph_steps <= 1 else f"hipGraph replay, {args.graph_steps} steps per graph",
             },
-            "input_GBps": round(4 * (args.job_numel or world * N) / (elapsed / args.steps) / 1e9, 2),
+            "input_GBps": round(4 * (job_numel or world * N) / (elapsed / args.steps) / 1e9, 2),
             "kernel_ms": round(kern_ms_max, 5),
             "roofline": {
                 "bound": "hbm",
@@ -297,64 +363,194 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": load_traffic(N, P),
+                "traffic": load_traffic(N, P, "quantize_pack" if nb == 1 else "quantize_pack_cold"),
                 "kernel": f"sml::k_quantize_pack<{P},aligned,fused,BE,half-away>",
             },
             "self_check": ok,
         }
+        if "cold_hbm" in side:
+            c = side["cold_hbm"]
+            line["roofline"]["frac_cold"] = c["frac"]
+            line["roofline"]["traffic_cold"] = load_traffic(args.numel, P, "quantize_pack_cold")
+        line.update(fields)
+        if side:
+            line["side"] = side
         if extra:
             line["extra"] = extra
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(N, P, args.cpu_seconds)
+        if failures:
+            line["failures"] = failures
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if failures:
+        sys.exit(1)
 
 
-def switchsim_measure(sw, torch, dist, x, N, P, world, dev, reps=5, cls=None,
-                      pipeline="K2 exps -> all_reduce(int8, MAX) -> K3 LE payload -> all_reduce(int32, SUM) -> K4"):
-    """Time a switch-sim all-reduce of the same 256 MiB bucket per GPU
-    (switchml_amd/switchsim.py, or the peer-to-peer switch); max over ranks.
-    algbw = 4N / t."""
-    from switchml_amd.switchsim import SwitchSimAllReduce
-    if world == 1 and not dist.is_initialized():
-        return {"note": "single rank: no exchange to time"}
-    ar = (cls or SwitchSimAllReduce)(N, P, dev)
-    out = torch.empty_like(x)
-    ar(x, out)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
+def settle(step, settle_ms):
+    """Clock settle: the first ~20-40 ms of streaming after idle run ~4 %
+    slower; run the same step untimed for settle_ms first."""
+    import torch
+    t_settle = time.perf_counter() + settle_ms * 1e-3
+    while time.perf_counter() < t_settle:
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize()
+
+
+def time_launches(torch, fn, stream, reps, warm=3):
+    for _ in range(warm):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
     for _ in range(reps):
-        ar(x, out)
+        fn()
+    b.record(stream)
     torch.cuda.synchronize()
-    t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t = float(t[0])
-    if hasattr(ar, "close"):
-        ar.close()
-    return {"workers": world, "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * N / t / 1e9, 2),
-            "pipeline": pipeline}
+    return a.elapsed_time(b) / reps * 1e-3
 
 
-def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
+def cold_measure(sw, torch, N, P, stream, nbuf=4, reps=200):
+    """K1 with the steps cycling through nbuf distinct 256 MiB buckets and
+    output planes (nbuf x 512 MiB >> the 256 MiB Infinity Cache): every launch
+    streams from / to HBM proper.  The headline re-reads one resident bucket."""
+    B = sw.num_blocks(N, P)
+    g = torch.Generator(device=stream.device)
+    g.manual_seed(4242)
+    xs = [torch.randn(N, device=stream.device, generator=g) for _ in range(nbuf)]
+    pls = [torch.empty(B * P, dtype=torch.int32, device=stream.device) for _ in range(nbuf)]
+    exs = [torch.empty(B, dtype=torch.int8, device=stream.device) for _ in range(nbuf)]
+    i = [0]
+
+    def fn():
+        k = i[0]
+        i[0] = (k + 1) % nbuf
+        sw.quantize_pack(xs[k], P, 1, payload=pls[k], exps_out=exs[k], stream=stream)
+
+    settle(fn, 30.0)
+    t = time_launches(torch, fn, stream, reps)
+    alg = 8 * N + B
+    return {"buckets": nbuf, "bucket_MiB": N * 4 >> 20, "kernel_ms": round(t * 1e3, 5),
+            "achieved_GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
+            "note": "K1 cycling distinct buckets and planes: HBM-proper rate (no Infinity Cache reuse)"}
+
+
+def job_measure(sw, torch, job_numel, P, stream, dev, reps=50):
+    """configs[3] on ONE GPU: the whole 1 GiB job (T = 1 slice) through K1 —
+    the single-GPU point of the strong-scaling curve the N > 1 runs report."""
+    B = sw.num_blocks(job_numel, P)
+    g = torch.Generator(device=dev)
+    g.manual_seed(42)
+    x = torch.randn(job_numel, device=dev, generator=g)
+    pl = torch.empty(B * P, dtype=torch.int32, device=dev)
+    ex = torch.empty(B, dtype=torch.int8, device=dev)
+    fn = lambda: sw.quantize_pack(x, P, 1, payload=pl, exps_out=ex, stream=stream)  # noqa: E731
+    settle(fn, 20.0)
+    t = time_launches(torch, fn, stream, reps)
+    alg = 8 * job_numel + B
+    return {"job_numel": job_numel, "kernel_ms": round(t * 1e3, 4), "value_GBps": round(alg / t / 1e9, 1),
+            "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}
+
+
+def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
+    """The switch simulation with W = world real workers, each holding its
+    own n-element fp32 bucket (distinct per rank).  Two exchange paths:
+      switchsim   ring all-reduces (RCCL) of the int8 exponents (MAX) and the
+                  host-order int32 payload (SUM, wrapping)
+      p2p_switch  the payload summed at the reader from the peers' planes
+                  mapped over xGMI (K6), fp32 shards all-gathered
+    Verified: the two outputs are bit-identical, and both are within the
+    quantization bound of an fp32 all-reduce of the same buckets.  Timed:
+    max over ranks of the mean of `reps` calls.  xGMI bound: each GPU moves
+    2(W-1)/W x 4n bytes over its W-1 links to the other W-1 GPUs."""
+    from switchml_amd.switchsim import SwitchSimAllReduce
+    from switchml_amd.p2pswitch import PeerSwitchAllReduce
+
+    W = world
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    x = torch.randn(n, device=dev, generator=g) * float(2.0 ** (rank % 4 - 1))
+    B = sw.num_blocks(n, P)
+    bound_s = 2 * (W - 1) / W * 4 * n / ((W - 1) * XGMI_LINK_GBPS * 1e9)
+
+    # reference sum (fp32, RCCL) and the per-element tolerance from the global exponents
+    ref = x.clone()
+    dist.all_reduce(ref)
+    ge = sw.exponents(x, P)
+    dist.all_reduce(ge, op=dist.ReduceOp.MAX)
+    scale = torch.pow(2.0, ge.float()).repeat_interleave(P)[:n]
+    tol = scale * (W * W * 2.0 ** -32 + W * W * 2.0 ** -23)
+    del ge
+
+    res, outs = {}, {}
+    for name, cls, pipe in (
+            ("switchsim", SwitchSimAllReduce,
+             "K2 exps -> all_reduce(int8, MAX) -> K3 LE payload -> all_reduce(int32, SUM) -> K4"),
+            ("p2p_switch", PeerSwitchAllReduce,
+             "K2 exps -> all_reduce(int8, MAX) -> K3 BE payload -> K6 over the peers' planes (hipIpc, xGMI) "
+             "on this rank's block shard -> all_gather(fp32)")):
+        try:
+            ar = cls(n, P, dev)
+            out = torch.empty_like(x)
+            ar(x, out)
+            torch.cuda.synchronize()
+            err = (out - ref).abs()
+            within = bool((err <= tol).all().item())
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ar(x, out)
+            torch.cuda.synchronize()
+            tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = float(tt[0])
+            if hasattr(ar, "close"):
+                ar.close()
+            del ar
+            ok_t = torch.tensor([int(within)], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+            outs[name] = out
+            res[name] = {"workers": W, "numel_per_worker": n, "packet_numel": P,
+                         "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * n / t / 1e9, 2),
+                         "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
+                         "xgmi_bound_ms": round(bound_s * 1e3, 3),
+                         "frac_of_xgmi_bound": round(bound_s / t, 4),
+                         "within_quantization_bound": bool(ok_t.item()),
+                         "max_abs_err_vs_fp32_allreduce": float(err.max().item()),
+                         "pipeline": pipe}
+            del err
+        except Exception as e:  # noqa: BLE001
+            res[name] = {"error": repr(e)[:400], "pipeline": pipe}
+    same = None
+    if "switchsim" in outs and "p2p_switch" in outs:
+        eq = torch.tensor([int(torch.equal(outs["switchsim"], outs["p2p_switch"]))], dtype=torch.int32, device=dev)
+        dist.all_reduce(eq, op=dist.ReduceOp.MIN)
+        same = bool(eq.item())
+    for name in ("switchsim", "p2p_switch"):
+        r = res[name]
+        if "error" not in r:
+            r["bit_equal_to_other_path"] = same
+            r["verified"] = bool(r["within_quantization_bound"] and same)
+        r["xgmi_link_GBps_assumed"] = XGMI_LINK_GBPS
+    res["p2p_switch"]["status"] = "experimental (first cross-GPU run is the driver's multi-GPU bench)"
+    return res
+
+
+def extra_measurements(sw, torch, x, P, stream, reps=20):
     """Side measurements (not the headline): dequantize, fused loopback round
     trip, and a plain device copy as the practical HBM ceiling."""
+    N = x.numel()
+    B = sw.num_blocks(N, P)
+    payload = torch.empty(B * P, dtype=torch.int32, device=x.device)
+    exps = torch.empty(B, dtype=torch.int8, device=x.device)
+    sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=stream)
     out = torch.empty_like(x)
     res = {}
 
     def timeit(fn):
-        for _ in range(3):
-            fn()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(reps):
-            fn()
-        b.record(stream)
-        torch.cuda.synchronize()
-        return a.elapsed_time(b) / reps * 1e-3
+        return time_launches(torch, fn, stream, reps)
 
-    B = exps.numel()
     t = timeit(lambda: sw.dequantize(payload, exps, N, P, 1, out=out, stream=stream))
     res["dequantize_GBps"] = round((8 * N + B) / t / 1e9, 1)
     t = timeit(lambda: sw.roundtrip_loopback(x, P, 1, out=out, stream=stream))
@@ -407,6 +603,7 @@ def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
     hframes = torch.empty(fbytes, dtype=torch.uint8).pin_memory()
     t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=hframes, stream=stream))
     res["frames_to_pinned_host_input_GBps"] = round(4 * N / t / 1e9, 2)
+    del hframes
     # K6: the switch's aggregation over W worker planes fused with the
     # dequantize (the peer-to-peer switch's compute; planes local here)
     sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=stream)
@@ -421,6 +618,51 @@ def extra_measurements(sw, torch, x, payload, exps, N, P, stream, reps=20):
     del planes, agg
     t = timeit(lambda: sw.stream_copy(x, out, stream=stream))
     res["nt_tile_copy_GBps"] = round(8 * N / t / 1e9, 1)
+    del out
+    res["configs4_plugin"] = plugin_buckets(torch, x.device)
+    return res
+
+
+RESNET50_BUCKETS = [6_553_600, 6_553_600, 6_553_600, 5_896_232]   # DDP 25 MiB buckets of 25,557,032 fp32
+
+
+def plugin_buckets(torch, dev, iters=10):
+    """configs[4]: ResNet-50-sized gradient buckets handed to the RCCL CollNet
+    plugin's iallreduce and polled with test() (switchml_plugin.cc:293-387),
+    all four buckets in flight per iteration, as RCCL's proxy posts them.
+    Placements: device buffers (ptrSupport CUDA: the HIP quantizer works in
+    place in HBM) and pinned host buffers (what the reference's HOST-only
+    plugin is handed: staged H2D -> kernels -> D2H by the worker threads).
+    Backend: the loopback (W = 8, T = 4, fused round trip)."""
+    import numpy as np
+    os.environ["SWITCHML_CONFIG_INI"] = (
+        "[general]\nnum_workers = 8\nnum_worker_threads = 4\npacket_numel = 256\nmax_outstanding_packets = 256\n"
+        "[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = fused\n")
+    os.environ["SWITCHML_COLLNET_LOOPBACK"] = "1"
+    from switchml_amd.collnet import CollNetComm, NCCL_FLOAT32
+    comm = CollNetComm()
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    dsend = [torch.randn(n, device=dev, generator=g) * 1e-3 for n in RESNET50_BUCKETS]
+    drecv = [torch.empty_like(d) for d in dsend]
+    hsend = [d.cpu().pin_memory() for d in dsend]
+    hrecv = [torch.empty_like(h).pin_memory() for h in hsend]
+    total = sum(RESNET50_BUCKETS)
+    res = {"buckets": RESNET50_BUCKETS, "params": total, "num_workers": 8, "num_worker_threads": 4,
+           "packet_numel": 256, "mode": "fused"}
+    for name, snd, rcv in (("device", dsend, drecv), ("pinned_host", hsend, hrecv)):
+        jobs = [(s.data_ptr(), r.data_ptr(), s.numel()) for s, r in zip(snd, rcv)]
+        comm.allreduce_buckets(jobs, NCCL_FLOAT32)
+        ts = []
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            comm.allreduce_buckets(jobs, NCCL_FLOAT32)
+            ts.append(time.perf_counter() - t0)
+        t = float(np.median(ts))
+        res[name] = {"ms_per_iteration": round(t * 1e3, 4), "elements_per_s": round(total / t, 1),
+                     "fp32_GBps": round(4 * total / t / 1e9, 2)}
+    res["placements_agree"] = all(bool(torch.equal(r.cpu(), h)) for r, h in zip(drecv, hrecv))
+    comm.close()
     return res
 
 
@@ -452,7 +694,6 @@ def host_inclusive(sw, torch, x, N, P, chunk=8 * 1024 * 1024, reps=5):
     assert chunk % P == 0 and N % chunk == 0
 
     def pipelined():
-        evs = []
         for c in range(N // chunk):
             lo, hi = c * chunk, (c + 1) * chunk
             blo, bhi = lo // P, hi // P
@@ -468,7 +709,6 @@ def host_inclusive(sw, torch, x, N, P, chunk=8 * 1024 * 1024, reps=5):
             with torch.cuda.stream(sc):
                 hp[lo:hi].copy_(dp[lo:hi], non_blocking=True)
                 he[blo:bhi].copy_(de[blo:bhi], non_blocking=True)
-            evs.append(e2)
 
     dring = [torch.empty(chunk, dtype=torch.float32, device=dev) for _ in range(2)]
     copy_done = [torch.cuda.Event() for _ in range(2)]

@@ -71,6 +71,7 @@ bool Config::LoadFromString(const std::string& ini) {
         else if (full == "general.controller_port") g.controller_port = parse_uint<uint16_t>(full, val, 0xffff);
         else if (full == "backend.dummy.bandwidth") backend_.dummy.bandwidth = std::stof(val);
         else if (full == "backend.dummy.process_packets") backend_.dummy.process_packets = parse_bool(val);
+        else if (full == "backend.dummy.fail_worker_thread") backend_.dummy.fail_worker_thread = std::stoi(val);
         else if (full == "backend.hip.device") backend_.hip.device = std::stoi(val);
         else if (full == "backend.hip.mode") backend_.hip.mode = val;
         else fprintf(stderr, "[switchml] ignoring config key '%s' (not used by this build)\n", full.c_str());
@@ -131,6 +132,7 @@ std::string Config::ToString() const {
       << "\ncontroller_ip = " << g.controller_ip_str << "\ncontroller_port = " << g.controller_port
       << "\n\n[backend.dummy]\nbandwidth = " << backend_.dummy.bandwidth
       << "\nprocess_packets = " << (backend_.dummy.process_packets ? "true" : "false")
+      << "\nfail_worker_thread = " << backend_.dummy.fail_worker_thread
       << "\n\n[backend.hip]\ndevice = " << backend_.hip.device << "\nmode = " << backend_.hip.mode << "\n";
     return o.str();
 }

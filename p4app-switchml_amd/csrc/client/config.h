@@ -29,6 +29,10 @@ struct GeneralConfig {
 struct DummyBackendConfig {
     float bandwidth = 1000.0f;             // Mbps; <= 0 disables the simulated wire time
     bool process_packets = true;           // multiply payloads by num_workers (the "switch")
+    // Fault injection for tests (the client-side analogue of the reference's
+    // P4 drop simulator, controller/drop_simulator.py): the worker thread with
+    // this id fails every slice it is handed without touching the buffers.
+    int fail_worker_thread = -1;
 };
 
 // MI355X-specific knobs of the loopback backend.

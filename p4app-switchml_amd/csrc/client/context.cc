@@ -154,9 +154,11 @@ bool Context::GetJobSlice(WorkerTid tid, JobSlice& job_slice) {
 }
 
 void Context::NotifyJobSliceCompletion(WorkerTid tid, const JobSlice& job_slice, bool ok) {
-    if (!ok) job_slice.job->SetJobStatus(FAILED);
+    if (!ok) job_slice.job->MarkFailed();
     if (!scheduler_->NotifyJobSliceCompletion(tid, job_slice)) return;
-    job_slice.job->SetJobStatus(FINISHED);  // no-op if a slice failed
+    // The job's last running slice: only now is nothing touching its buffers,
+    // so only now may WaitToComplete / sml_job_wait return (FINISHED or FAILED).
+    job_slice.job->SetJobStatus(job_slice.job->HasFailed() ? FAILED : FINISHED);
     std::unique_lock<std::mutex> lock(access_mutex_);
     if (number_of_current_jobs_ > 0) number_of_current_jobs_--;
     stats_.IncJobsFinished();

@@ -49,6 +49,7 @@ bool FifoScheduler::EnqueueJob(std::shared_ptr<Job> job) {
     }
     job->SetJobStatus(QUEUED);
     finished_job_slices_[job->id_] = 0;
+    dispatched_job_slices_[job->id_] = 0;
     undispatched_job_slices_[job->id_] = config_.general_.num_worker_threads;
     queue_.push(job);
     queue_size_.store(queue_.size(), std::memory_order_release);
@@ -79,6 +80,7 @@ bool FifoScheduler::GetJobSlice(WorkerTid tid, JobSlice& job_slice) {
     if (stopped_) return false;
 
     std::shared_ptr<Job> job = queue_.front();
+    dispatched_job_slices_.at(job->id_)++;
     int& left = undispatched_job_slices_.at(job->id_);
     if (--left == 0) {
         queue_.pop();
@@ -97,13 +99,15 @@ bool FifoScheduler::GetJobSlice(WorkerTid tid, JobSlice& job_slice) {
 
 bool FifoScheduler::NotifyJobSliceCompletion(WorkerTid, const JobSlice& job_slice) {
     std::unique_lock<std::mutex> lock(access_mutex_);
-    if (stopped_) {
-        job_slice.job->SetJobStatus(FAILED);
-        return false;
-    }
-    int& done = finished_job_slices_.at(job_slice.job->id_);
-    if (++done == config_.general_.num_worker_threads) {
-        finished_job_slices_.erase(job_slice.job->id_);
+    const JobId id = job_slice.job->id_;
+    if (stopped_) job_slice.job->MarkFailed();
+    int& done = finished_job_slices_.at(id);
+    // after Stop() the slices never handed out will not run: the job is over
+    // when every slice that was handed out has come back
+    const int need = stopped_ ? dispatched_job_slices_.at(id) : config_.general_.num_worker_threads;
+    if (++done == need) {
+        finished_job_slices_.erase(id);
+        dispatched_job_slices_.erase(id);
         return true;
     }
     return false;
@@ -115,8 +119,14 @@ void FifoScheduler::Stop() {
     stopped_flag_.store(true, std::memory_order_release);
     barrier_.Destroy();
     while (!queue_.empty()) {
-        queue_.front()->SetJobStatus(FAILED);
+        std::shared_ptr<Job> job = queue_.front();
         queue_.pop();
+        job->MarkFailed();
+        if (dispatched_job_slices_.at(job->id_) == 0) {  // nothing running: publish now
+            finished_job_slices_.erase(job->id_);
+            dispatched_job_slices_.erase(job->id_);
+            job->SetJobStatus(FAILED);
+        }
     }
     queue_size_.store(0, std::memory_order_release);
     undispatched_job_slices_.clear();

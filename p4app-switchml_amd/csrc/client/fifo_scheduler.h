@@ -47,9 +47,13 @@ class FifoScheduler {
     // Blocks (after a barrier with the other worker threads) until a job is
     // queued or the scheduler stops; false when stopped.
     bool GetJobSlice(WorkerTid worker_thread_id, JobSlice& job_slice);
-    // True when this completed the job's last slice.
+    // True when this completed the job's last RUNNING slice: all T slices,
+    // or after Stop() every slice that had been handed out.  Only then may
+    // the caller publish the job's final status (its buffers are released).
     bool NotifyJobSliceCompletion(WorkerTid worker_thread_id, const JobSlice& job_slice);
-    // Fail every queued job and wake all waiting worker threads.
+    // Fail every queued job and wake all waiting worker threads.  A queued
+    // job none of whose slices is running is published FAILED here; one with
+    // running slices is marked failed and published by its last slice.
     void Stop();
 
   private:
@@ -59,6 +63,7 @@ class FifoScheduler {
     std::queue<std::shared_ptr<Job>> queue_;
     std::map<JobId, int> undispatched_job_slices_;
     std::map<JobId, int> finished_job_slices_;
+    std::map<JobId, int> dispatched_job_slices_;
     Barrier barrier_;
     bool stopped_ = false;
     // lock-free mirrors of stopped_ / queue_.size() for the short poll before

@@ -24,6 +24,11 @@ class Job {
     JobStatus GetJobStatus() const { return job_status_.load(); }
     // Statuses only move forward; FINISHED/FAILED wake waiters (job.cc:49-57).
     void SetJobStatus(JobStatus status);
+    // A slice failed (or the context stopped under it).  Recorded only: the
+    // job is published FAILED by its last running slice, so no waiter wakes
+    // while sibling slices still read in_ptr / write out_ptr.
+    void MarkFailed() { failed_.store(true, std::memory_order_release); }
+    bool HasFailed() const { return failed_.load(std::memory_order_acquire); }
 
     const JobId id_;
     const Tensor tensor_;
@@ -33,6 +38,7 @@ class Job {
   private:
     static std::atomic<JobId> next_id_;
     std::atomic<JobStatus> job_status_;
+    std::atomic<bool> failed_{false};
     std::mutex access_mutex_;
     std::condition_variable job_finished_event_;
 };

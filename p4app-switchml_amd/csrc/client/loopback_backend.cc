@@ -183,6 +183,7 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
         // (dummy_worker_thread.cc:87-93)
         const bool work = js.slice.numel > 0 && !g.instant_job_completion;
         bool ok = !work || ppp != nullptr;
+        if (work && tid == config_.backend_.dummy.fail_worker_thread) ok = false;  // injected fault
         uint64_t packets = 0;
         if (ok && work) {
             try {

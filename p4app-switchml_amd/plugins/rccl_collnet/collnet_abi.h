@@ -5,8 +5,8 @@
 // headers (net_v*.h) are not installed in this image.  The v6 layout below is
 // restated from NCCL's published ext-net example headers (nccl/net_v6.h:
 // ncclNetProperties_v6_t, ncclCollNet_v6_t) and the public enums of nccl.h.
-// Only v6 is exported: it is the oldest layout RCCL 7.2 accepts and the one
-// whose field list is certain without the headers.
+// Only v6 is exported (CollNet and net tables): it is the oldest layout RCCL
+// 7.2 accepts and the one whose field list is certain without the headers.
 #ifndef SWITCHML_AMD_COLLNET_ABI_H_
 #define SWITCHML_AMD_COLLNET_ABI_H_
 
@@ -73,6 +73,32 @@ typedef struct {
     ncclResult_t (*closeColl)(void* collComm);
     ncclResult_t (*closeListen)(void* listenComm);
 } ncclCollNet_v6_t;
+
+// The p2p net table (nccl/net_v6.h ncclNet_v6_t).  The reference plugin
+// exports one beside its CollNet table (switchml_plugin.cc:37: NCCL_PLUGIN_SYMBOL)
+// and NCCL's loader looks the CollNet table up only in a library that has
+// one; the SwitchML net table forwards to an underlying net plugin.
+typedef struct {
+    const char* name;
+    ncclResult_t (*init)(ncclDebugLogger_t logFunction);
+    ncclResult_t (*devices)(int* ndev);
+    ncclResult_t (*getProperties)(int dev, ncclNetProperties_v6_t* props);
+    ncclResult_t (*listen)(int dev, void* handle, void** listenComm);
+    ncclResult_t (*connect)(int dev, void* handle, void** sendComm);
+    ncclResult_t (*accept)(void* listenComm, void** recvComm);
+    ncclResult_t (*regMr)(void* comm, void* data, int size, int type, void** mhandle);
+    ncclResult_t (*regMrDmaBuf)(void* comm, void* data, size_t size, int type, uint64_t offset, int fd,
+                                void** mhandle);
+    ncclResult_t (*deregMr)(void* comm, void* mhandle);
+    ncclResult_t (*isend)(void* sendComm, void* data, int size, int tag, void* mhandle, void** request);
+    ncclResult_t (*irecv)(void* recvComm, int n, void** data, int* sizes, int* tags, void** mhandles,
+                          void** request);
+    ncclResult_t (*iflush)(void* recvComm, int n, void** data, int* sizes, void** mhandles, void** request);
+    ncclResult_t (*test)(void* request, int* done, int* sizes);
+    ncclResult_t (*closeSend)(void* sendComm);
+    ncclResult_t (*closeRecv)(void* recvComm);
+    ncclResult_t (*closeListen)(void* listenComm);
+} ncclNet_v6_t;
 
 }  // extern "C"
 

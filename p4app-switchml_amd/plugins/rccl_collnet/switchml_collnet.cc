@@ -15,8 +15,24 @@
 //    reporting "not done");
 //  * ncclUint8 is widened to int32 on the host as in :318-337, for host
 //    buffers; device uint8 buffers are rejected (ncclInvalidArgument).
+//  * the only backend of this client is the loopback ("dummy"): it multiplies
+//    a rank's own buffer by num_workers instead of summing across ranks, so a
+//    CollNet all-reduce through it is NOT a cross-rank reduction.  init()
+//    therefore refuses (ncclInvalidUsage) unless SWITCHML_COLLNET_LOOPBACK=1
+//    says the caller wants exactly that (tests, single-rank benchmarks).
 // Configuration: SWITCHML_CONFIG_INI (INI text) or SWITCHML_CONFIG (path),
 // else the reference's search path (/etc/switchml.cfg, ./switchml.cfg, ...).
+//
+// Beside the CollNet table the library exports a p2p net table,
+// ncclNetPlugin_v6, as the reference does (switchml_plugin.cc:37): NCCL/RCCL
+// resolve the CollNet table from a net plugin library.  The reference leaves
+// its net table empty for a patched NCCL to fill with NCCL's own IB net
+// (switchml_nccl.patch:24-81); this one forwards every call to the net plugin
+// named by SWITCHML_NET_PLUGIN (a library exporting ncclNetPlugin_v6, loaded
+// with dlopen at init).  With none named, init() fails cleanly
+// (ncclInternalError) and RCCL falls back to its internal IB / socket nets.
+#include <dlfcn.h>
+
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -68,6 +84,14 @@ int type_size(ncclDataType_t t) {
 
 ncclResult_t sml_init(ncclDebugLogger_t logger) {
     g_logger = logger;
+    const char* lb = getenv("SWITCHML_COLLNET_LOOPBACK");
+    if (!lb || strcmp(lb, "1") != 0) {
+        if (g_logger)
+            g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__,
+                     "SwitchML CollNet: the loopback backend does not reduce across ranks; "
+                     "set SWITCHML_COLLNET_LOOPBACK=1 to use it anyway");
+        return ncclInvalidUsage;
+    }
     try {
         switchml::Context& ctx = switchml::Context::GetInstance();
         if (ctx.GetContextState() == switchml::Context::RUNNING) return ncclSuccess;
@@ -215,9 +239,87 @@ ncclResult_t sml_close_listen(void* listen_comm) {
     return ncclSuccess;
 }
 
+// ------------------------------------------------------------ p2p net --
+// Forwarding table over the underlying net plugin (SWITCHML_NET_PLUGIN).
+
+void* g_net_lib = nullptr;
+ncclNet_v6_t* g_under = nullptr;
+
+ncclResult_t net_init(ncclDebugLogger_t logger) {
+    if (logger) g_logger = logger;
+    if (g_under) return ncclSuccess;
+    const char* path = getenv("SWITCHML_NET_PLUGIN");
+    if (!path || !*path) {
+        if (g_logger)
+            g_logger(NCCL_LOG_INFO, 0, __FILE__, __LINE__,
+                     "SwitchML net: no underlying net plugin (SWITCHML_NET_PLUGIN unset)");
+        return ncclInternalError;
+    }
+    void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        if (g_logger) g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__, "SwitchML net: dlopen %s: %s", path, dlerror());
+        return ncclInternalError;
+    }
+    auto* t = static_cast<ncclNet_v6_t*>(dlsym(h, "ncclNetPlugin_v6"));
+    if (!t || !t->init) {
+        if (g_logger) g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__, "SwitchML net: %s has no ncclNetPlugin_v6", path);
+        dlclose(h);
+        return ncclInternalError;
+    }
+    const ncclResult_t r = t->init(logger);
+    if (r != ncclSuccess) {
+        dlclose(h);
+        return r;
+    }
+    g_net_lib = h;
+    g_under = t;
+    return ncclSuccess;
+}
+
+#define SML_FWD(fn, ...)                          \
+    do {                                          \
+        if (!g_under) return ncclInternalError;   \
+        return g_under->fn(__VA_ARGS__);          \
+    } while (0)
+
+ncclResult_t net_devices(int* ndev) { SML_FWD(devices, ndev); }
+ncclResult_t net_get_properties(int dev, ncclNetProperties_v6_t* props) { SML_FWD(getProperties, dev, props); }
+ncclResult_t net_listen(int dev, void* handle, void** listen_comm) { SML_FWD(listen, dev, handle, listen_comm); }
+ncclResult_t net_connect(int dev, void* handle, void** send_comm) { SML_FWD(connect, dev, handle, send_comm); }
+ncclResult_t net_accept(void* listen_comm, void** recv_comm) { SML_FWD(accept, listen_comm, recv_comm); }
+ncclResult_t net_reg_mr(void* comm, void* data, int size, int type, void** mh) {
+    SML_FWD(regMr, comm, data, size, type, mh);
+}
+ncclResult_t net_reg_mr_dmabuf(void* comm, void* data, size_t size, int type, uint64_t off, int fd, void** mh) {
+    if (g_under && !g_under->regMrDmaBuf) return ncclInternalError;
+    SML_FWD(regMrDmaBuf, comm, data, size, type, off, fd, mh);
+}
+ncclResult_t net_dereg_mr(void* comm, void* mh) { SML_FWD(deregMr, comm, mh); }
+ncclResult_t net_isend(void* send_comm, void* data, int size, int tag, void* mh, void** req) {
+    SML_FWD(isend, send_comm, data, size, tag, mh, req);
+}
+ncclResult_t net_irecv(void* recv_comm, int n, void** data, int* sizes, int* tags, void** mhs, void** req) {
+    SML_FWD(irecv, recv_comm, n, data, sizes, tags, mhs, req);
+}
+ncclResult_t net_iflush(void* recv_comm, int n, void** data, int* sizes, void** mhs, void** req) {
+    SML_FWD(iflush, recv_comm, n, data, sizes, mhs, req);
+}
+ncclResult_t net_test(void* req, int* done, int* sizes) { SML_FWD(test, req, done, sizes); }
+ncclResult_t net_close_send(void* c) { SML_FWD(closeSend, c); }
+ncclResult_t net_close_recv(void* c) { SML_FWD(closeRecv, c); }
+ncclResult_t net_close_listen(void* c) { SML_FWD(closeListen, c); }
+
+#undef SML_FWD
+
 }  // namespace
 
 extern "C" {
+__attribute__((visibility("default"))) ncclNet_v6_t ncclNetPlugin_v6 = {
+    "SWITCHML",         net_init,        net_devices,       net_get_properties, net_listen,
+    net_connect,        net_accept,      net_reg_mr,        net_reg_mr_dmabuf,  net_dereg_mr,
+    net_isend,          net_irecv,       net_iflush,        net_test,           net_close_send,
+    net_close_recv,     net_close_listen};
+
 __attribute__((visibility("default"))) ncclCollNet_v6_t ncclCollNetPlugin_v6 = {
     "SWITCHMLv1",       sml_init,        sml_devices,       sml_get_properties, sml_listen,
     sml_connect,        sml_reduce_support, sml_reg_mr,     sml_reg_mr_dmabuf,  sml_dereg_mr,

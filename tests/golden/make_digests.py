@@ -21,8 +21,9 @@ W * 2^e overflows float (e = 127, W >= 2) — are canonicalized to 0x7fc00000
 before hashing: x86 divides to the negative default NaN 0xffc00000, gfx950
 to the positive one; that sign is the one non-bit-exact case.
 
-Run: python tests/golden/make_digests.py   (rewrites digests.json and
-digests_ext.json, ~1 min; --ext-only rewrites only the latter)
+Run: python tests/golden/make_digests.py   (rewrites digests.json,
+digests_ext.json and digests_switch.json, ~2 min; --ext-only rewrites only
+digests_ext.json, --switch-only digests_ext.json and digests_switch.json)
 """
 import hashlib
 import json
@@ -42,6 +43,20 @@ CASES = [
     ("cfg3_grad_W2", "grad", 43, 67_108_864, 256, 2, 1),
     ("cfg3_randbits_W8_T4", "randbits", 7, 67_108_864, 256, 8, 4),
     ("rdma_grad_P1024_W3", "grad", 44, 16_777_216 + 1000, 1024, 3, 1),
+    # configs[3]: the 1 GiB job (allreduce_benchmark's default tensor-numel,
+    # main.cc:101) split into 8 FIFO slices, slice g = GPU g's shard
+    ("cfg3_job_1GiB_randbits_T8", "randbits", 11, 268_435_456, 256, 1, 8),
+]
+
+# configs[3]'s switch simulation: W = 8 workers, each with its own 64 MiB
+# bucket (rank r: generator seed + r, scaled by 2^(r % 4 - 1) so the per-block
+# exponents differ between workers).  The switch (p4/exponents.p4:48-54 signed
+# int8 max, p4/processor.p4:48-54 wrapping bit<32> sum) sees every worker's
+# packets; digests of the global exponent plane, the aggregated BE payload
+# plane and the dequantized sum every worker ends with.
+SWITCH_CASES = [
+    # name, generator, seed, numel per worker, P, W
+    ("cfg3_switch_W8_grad_64MiB", "grad", 60, 16_777_216, 256, 8),
 ]
 
 
@@ -53,6 +68,25 @@ def make_input(gen, seed, n):
     if gen == "grad":
         return O.splitmix_grad(seed, n)
     raise ValueError(gen)
+
+
+def switch_input(gen, seed, rank, n):
+    import numpy as np
+    return make_input(gen, seed + rank, n) * np.float32(2.0 ** (rank % 4 - 1))
+
+
+def oracle_switch_digests(gen, seed, numel, P, W):
+    xs = [switch_input(gen, seed, r, numel) for r in range(W)]
+    h = {k: hashlib.sha256() for k in ("inputs", "global_exps", "payload", "out")}
+    for x in xs:
+        h["inputs"].update(x.tobytes())
+    g = O.switch_exps([O.exponents(x, P) for x in xs])
+    agg = O.switch_payload([O.quantize(x, P, W, global_exps=g) for x in xs])
+    out = O.dequantize(agg, g, numel, P, W)
+    h["global_exps"].update(g.tobytes())
+    h["payload"].update(agg.tobytes())
+    h["out"].update(canonical_nan(out).tobytes())
+    return {k: v.hexdigest() for k, v in h.items()}
 
 
 def canonical_nan(out):
@@ -126,6 +160,16 @@ def main():
         json.dump(ext, f, indent=1)
         f.write("\n")
     if "--ext-only" in sys.argv:
+        return
+    sw_res = {}
+    for name, gen, seed, numel, P, W in SWITCH_CASES:
+        sw_res[name] = {"gen": gen, "seed": seed, "numel": numel, "packet_numel": P, "num_workers": W,
+                        "sha256": oracle_switch_digests(gen, seed, numel, P, W)}
+        print(name, sw_res[name]["sha256"]["out"][:16], flush=True)
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "digests_switch.json"), "w") as f:
+        json.dump(sw_res, f, indent=1)
+        f.write("\n")
+    if "--switch-only" in sys.argv:
         return
     res = {}
     for name, gen, seed, numel, P, W, T in CASES:

@@ -127,3 +127,31 @@ def test_empty_job_finishes(ctx):
     j.wait()
     assert j.status() == C.JOB_FINISHED
     C.stop()
+
+
+def test_failed_slice_publishes_only_after_siblings(ctx):
+    """One worker thread fails its slice at once (backend.dummy.fail_worker_thread,
+    fault injection); its siblings are still on the simulated wire.  The job
+    must not be published FAILED — waking sml_job_wait / WaitToComplete —
+    until every sibling slice has stopped touching the buffers (ADVICE r1:
+    a caller freeing its buffers on FAILED raced the running slices)."""
+    import time
+    C = ctx
+    T, numel = 4, 1 << 20
+    # bypass PPP: every slice of 2^18 elements = 1024 packets of 1 KiB; at
+    # 80 Mbps x T the wire wait per healthy slice is ~0.4 s
+    C.start(C.make_config(prepostprocessor="bypass", num_worker_threads=T, packet_numel=256,
+                          max_outstanding_packets=256, bandwidth=80, fail_worker_thread=1))
+    x = np.zeros(numel, dtype=np.float32)
+    t0 = time.perf_counter()
+    j = C.allreduce_async(x)
+    with pytest.raises(C.ContextError):
+        j.wait()
+    waited = time.perf_counter() - t0
+    assert j.status() == C.JOB_FAILED
+    expect_wire = 1024 * 256 * 4 * 8 * T / 80e6
+    assert waited >= 0.8 * expect_wire, (waited, expect_wire)
+    st = C.stats()
+    assert st["slices"] == T - 1          # the three healthy slices all ran to the end
+    C.wait_for_all_jobs()
+    C.stop()

@@ -9,7 +9,8 @@ oracle's dummy-backend packet loop.
 
 A live RCCL CollNet run needs a multi-node CollNet topology (RCCL disables
 CollNet below NCCL_COLLNET_NODE_THRESHOLD nodes), so RCCL itself loading the
-plugin is not exercised here."""
+plugin is not exercised here (tools/rccl_plugin_probe.py checks that RCCL
+resolves both exported tables)."""
 import ctypes
 import os
 import subprocess
@@ -21,41 +22,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PLUGIN = os.path.join(ROOT, "p4app-switchml_amd", "switchml_amd", "librccl-net-switchml.so")
 
-R = ctypes.c_int
-vp = ctypes.c_void_p
-LOGGER = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_ulong, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p)
-
-
-class Props(ctypes.Structure):
-    _fields_ = [("name", ctypes.c_char_p), ("pciPath", ctypes.c_char_p), ("guid", ctypes.c_uint64),
-                ("ptrSupport", ctypes.c_int), ("speed", ctypes.c_int), ("port", ctypes.c_int),
-                ("latency", ctypes.c_float), ("maxComms", ctypes.c_int), ("maxRecvs", ctypes.c_int)]
-
-
-class CollNetV6(ctypes.Structure):
-    _fields_ = [
-        ("name", ctypes.c_char_p),
-        ("init", ctypes.CFUNCTYPE(R, LOGGER)),
-        ("devices", ctypes.CFUNCTYPE(R, ctypes.POINTER(ctypes.c_int))),
-        ("getProperties", ctypes.CFUNCTYPE(R, ctypes.c_int, ctypes.POINTER(Props))),
-        ("listen", ctypes.CFUNCTYPE(R, ctypes.c_int, vp, ctypes.POINTER(vp))),
-        ("connect", ctypes.CFUNCTYPE(R, ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp))),
-        ("reduceSupport", ctypes.CFUNCTYPE(R, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int))),
-        ("regMr", ctypes.CFUNCTYPE(R, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp))),
-        ("regMrDmaBuf", ctypes.CFUNCTYPE(R, vp, vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
-                                         ctypes.POINTER(vp))),
-        ("deregMr", ctypes.CFUNCTYPE(R, vp, vp)),
-        ("iallreduce", ctypes.CFUNCTYPE(R, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp,
-                                        ctypes.POINTER(vp))),
-        ("iflush", ctypes.CFUNCTYPE(R, vp, vp, ctypes.c_int, vp, ctypes.POINTER(vp))),
-        ("test", ctypes.CFUNCTYPE(R, vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int))),
-        ("closeColl", ctypes.CFUNCTYPE(R, vp)),
-        ("closeListen", ctypes.CFUNCTYPE(R, vp)),
-    ]
-
-
-NCCL_UINT8, NCCL_INT32, NCCL_FLOAT32, NCCL_FLOAT64 = 1, 2, 7, 8
-NCCL_SUM, NCCL_MAX = 0, 2
+sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
+from switchml_amd.collnet import (LOGGER, NCCL_FLOAT32, NCCL_FLOAT64, NCCL_INT32, NCCL_MAX,  # noqa: E402,F401
+                                  NCCL_SUM, NCCL_UINT8, CollNetV6, Props, vp)
 
 DRIVER = r'''
 import ctypes, sys, os, json, numpy as np
@@ -96,12 +65,15 @@ print(json.dumps(out))
 '''
 
 
-def run_driver(body, env_ini, preload=""):
+def run_driver(body, env_ini, preload="", loopback_opt_in=True):
     # With torch in the process, torch must load first: it bundles its own
     # libamdhip64.so.7 (same SONAME as /opt/rocm's), and whichever loads first
     # is the one every library in the process binds to.
     code = DRIVER.format(root=ROOT, body=body, preload=preload)
     env = dict(os.environ, SWITCHML_CONFIG_INI=env_ini)
+    env.pop("SWITCHML_COLLNET_LOOPBACK", None)
+    if loopback_opt_in:   # the loopback backend does not reduce across ranks: explicit opt-in
+        env["SWITCHML_COLLNET_LOOPBACK"] = "1"
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     import json
@@ -156,3 +128,180 @@ out["dev_u8"] = run(ctypes.c_void_p(ud.data_ptr()), ctypes.c_void_p(ud.data_ptr(
     assert out["host_size"] == 4 * 100_003 and out["host_ok"]
     assert out["int_ok"]
     assert out["dev_u8"] == 4   # device uint8: ncclInvalidArgument
+
+
+def test_loopback_collnet_needs_opt_in():
+    """the loopback backend multiplies a rank's own buffer by
+    num_workers, it does not sum across ranks — init() refuses
+    (ncclInvalidUsage) unless SWITCHML_COLLNET_LOOPBACK=1."""
+    ini = "[general]\nprepostprocessor = bypass\nnum_worker_threads = 2\n[backend.dummy]\nbandwidth = 0\n"
+    code = (f"import ctypes, sys; sys.path[:0] = [{ROOT!r}, {os.path.join(ROOT, 'tests')!r}]\n"
+            "from test_collnet_plugin import CollNetV6, LOGGER, PLUGIN\n"
+            "tbl = CollNetV6.in_dll(ctypes.CDLL(PLUGIN), 'ncclCollNetPlugin_v6')\n"
+            "print(tbl.init(LOGGER(lambda *a: None)))\n")
+    env = dict(os.environ, SWITCHML_CONFIG_INI=ini)
+    env.pop("SWITCHML_COLLNET_LOOPBACK", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == "5"   # ncclInvalidUsage
+
+
+class NetV6(ctypes.Structure):
+    """nccl/net_v6.h ncclNet_v6_t (plugins/rccl_collnet/collnet_abi.h)."""
+    _fields_ = [("name", ctypes.c_char_p), ("init", vp), ("devices", vp), ("getProperties", vp),
+                ("listen", vp), ("connect", vp), ("accept", vp), ("regMr", vp), ("regMrDmaBuf", vp),
+                ("deregMr", vp), ("isend", vp), ("irecv", vp), ("iflush", vp), ("test", vp),
+                ("closeSend", vp), ("closeRecv", vp), ("closeListen", vp)]
+
+
+# A stand-in underlying net plugin: every entry point records that it ran.
+FAKE_NET = r"""
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+typedef int R;
+static int calls[17];
+int fake_calls(int i) { return calls[i]; }
+static R init(void* l) { calls[1]++; return 0; }
+static R devices(int* n) { calls[2]++; *n = 3; return 0; }
+static R props(int d, void* p) { calls[3]++; return d == 7 ? 4 : 0; }
+static R listen_(int d, void* h, void** c) { calls[4]++; memcpy(h, "FAKE", 4); *c = (void*)0x10; return 0; }
+static R connect_(int d, void* h, void** c) { calls[5]++; *c = (void*)0x20; return 0; }
+static R accept_(void* l, void** c) { calls[6]++; *c = (void*)0x30; return 0; }
+static R regmr(void* c, void* d, int s, int t, void** m) { calls[7]++; *m = (void*)0x40; return 0; }
+static R regdma(void* c, void* d, size_t s, int t, uint64_t o, int fd, void** m) { calls[8]++; return 0; }
+static R dereg(void* c, void* m) { calls[9]++; return 0; }
+static R isend(void* c, void* d, int s, int t, void* m, void** r) { calls[10]++; *r = (void*)0x50; return 0; }
+static R irecv(void* c, int n, void** d, int* s, int* t, void** m, void** r) { calls[11]++; *r = (void*)0x60; return 0; }
+static R iflush(void* c, int n, void** d, int* s, void** m, void** r) { calls[12]++; return 0; }
+static R test(void* r, int* done, int* s) { calls[13]++; *done = 1; return 0; }
+static R cs(void* c) { calls[14]++; return 0; }
+static R cr(void* c) { calls[15]++; return 0; }
+static R cl(void* c) { calls[16]++; return 0; }
+struct { const char* name; void* f[16]; } ncclNetPlugin_v6 = {"FAKE", {
+  (void*)init, (void*)devices, (void*)props, (void*)listen_, (void*)connect_, (void*)accept_, (void*)regmr,
+  (void*)regdma, (void*)dereg, (void*)isend, (void*)irecv, (void*)iflush, (void*)test, (void*)cs, (void*)cr,
+  (void*)cl}};
+"""
+
+NET_DRIVER = r"""
+import ctypes, json, sys
+sys.path[:0] = [{root!r}, {tests!r}]
+from test_collnet_plugin import NetV6, PLUGIN, LOGGER, vp
+lib = ctypes.CDLL(PLUGIN)
+t = NetV6.in_dll(lib, "ncclNetPlugin_v6")
+F = lambda name, *types: ctypes.CFUNCTYPE(ctypes.c_int, *types)(getattr(t, name))
+P = ctypes.POINTER
+out = {{"name": t.name.decode(), "init": F("init", LOGGER)(LOGGER(lambda *a: None))}}
+if out["init"] == 0:
+    n = ctypes.c_int(); out["devices"] = [F("devices", P(ctypes.c_int))(ctypes.byref(n)), n.value]
+    out["props_bad"] = F("getProperties", ctypes.c_int, vp)(7, None)
+    h = (ctypes.c_char * 128)(); lc, sc, rc, mh, rq = vp(), vp(), vp(), vp(), vp()
+    out["listen"] = F("listen", ctypes.c_int, vp, P(vp))(0, ctypes.cast(h, vp), ctypes.byref(lc))
+    out["handle"] = bytes(h[:4]).decode()
+    out["connect"] = F("connect", ctypes.c_int, vp, P(vp))(0, ctypes.cast(h, vp), ctypes.byref(sc))
+    out["accept"] = F("accept", vp, P(vp))(lc, ctypes.byref(rc))
+    out["comms"] = [lc.value, sc.value, rc.value]
+    F("regMr", vp, vp, ctypes.c_int, ctypes.c_int, P(vp))(sc, None, 4, 1, ctypes.byref(mh))
+    F("isend", vp, vp, ctypes.c_int, ctypes.c_int, vp, P(vp))(sc, None, 4, 0, mh, ctypes.byref(rq))
+    d = ctypes.c_int(0); sz = ctypes.c_int(0)
+    out["test"] = [F("test", vp, P(ctypes.c_int), P(ctypes.c_int))(rq, ctypes.byref(d), ctypes.byref(sz)), d.value]
+    F("deregMr", vp, vp)(sc, mh)
+    for nm in ("closeSend", "closeRecv", "closeListen"):
+        F(nm, vp)(None)
+    fake = ctypes.CDLL({fake!r})
+    out["fake_calls"] = [fake.fake_calls(i) for i in range(17)]
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("with_underlying", [False, True])
+def test_net_table_chains_to_underlying_plugin(tmp_path, with_underlying):
+    """ncclNetPlugin_v6 (reference: switchml_plugin.cc:37, NCCL_PLUGIN_SYMBOL
+    beside the CollNet table): without SWITCHML_NET_PLUGIN its init fails
+    cleanly (ncclInternalError, so RCCL falls back to its internal nets);
+    with one, every call is forwarded to the underlying plugin."""
+    fake = tmp_path / "libfake_net.so"
+    src = tmp_path / "fake_net.c"
+    src.write_text(FAKE_NET)
+    subprocess.run(["gcc", "-shared", "-fPIC", "-O1", "-o", str(fake), str(src)], check=True)
+    code = NET_DRIVER.format(root=ROOT, tests=os.path.join(ROOT, "tests"), fake=str(fake))
+    env = dict(os.environ)
+    env.pop("SWITCHML_NET_PLUGIN", None)
+    if with_underlying:
+        env["SWITCHML_NET_PLUGIN"] = str(fake)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["name"] == "SWITCHML"
+    if not with_underlying:
+        assert out["init"] == 3          # ncclInternalError: no underlying net
+        return
+    assert out["init"] == 0
+    assert out["devices"] == [0, 3] and out["props_bad"] == 4
+    assert out["listen"] == 0 and out["handle"] == "FAKE"
+    assert out["connect"] == 0 and out["accept"] == 0 and out["comms"] == [0x10, 0x20, 0x30]
+    assert out["test"] == [0, 1]
+    calls = out["fake_calls"]
+    for i in (1, 2, 3, 4, 5, 6, 7, 9, 10, 13, 14, 15, 16):
+        assert calls[i] >= 1, (i, calls)
+
+
+RESNET50_BUCKETS = [6_553_600, 6_553_600, 6_553_600, 5_896_232]   # 25 MiB DDP buckets of 25,557,032 params
+
+CFG4_DRIVER = r"""
+import json, sys
+import numpy as np
+import torch
+sys.path[:0] = [{root!r}, {pkg!r}]
+from oracle import oracle as O
+from switchml_amd.collnet import CollNetComm, NCCL_FLOAT32
+sizes = {sizes!r}
+comm = CollNetComm()
+xs = [O.splitmix_normal(50 + i, n) * np.float32(1e-3) for i, n in enumerate(sizes)]
+refs = [O.dummy_allreduce(x, P=256, max_outstanding_packets=256, num_worker_threads=4, num_workers=8,
+                          threaded=True) for x in xs]
+out = {{"ptrSupport": comm.props.ptrSupport}}
+# device buffers, not in place: RCCL's send / recv buffers
+dsend = [torch.from_numpy(x).cuda() for x in xs]
+drecv = [torch.empty_like(d) for d in dsend]
+mhs = [comm.reg_mr(d.data_ptr(), 4 * d.numel(), 2) for d in dsend]
+sz = comm.allreduce_buckets([(s.data_ptr(), r.data_ptr(), s.numel()) for s, r in zip(dsend, drecv)], NCCL_FLOAT32, mhs)
+out["device_sizes"] = sz
+out["device_ok"] = [bool(np.array_equal(r.cpu().numpy().view(np.uint32), ref.view(np.uint32)))
+                    for r, ref in zip(drecv, refs)]
+out["device_send_untouched"] = all(bool(np.array_equal(s.cpu().numpy(), x)) for s, x in zip(dsend, xs))
+for m in mhs:
+    comm.dereg_mr(m)
+# pinned host buffers, in place (what the reference's NCCL_PTR_HOST plugin is handed)
+hb = [torch.from_numpy(x.copy()).pin_memory() for x in xs]
+sz = comm.allreduce_buckets([(h.data_ptr(), h.data_ptr(), h.numel()) for h in hb], NCCL_FLOAT32)
+out["host_sizes"] = sz
+out["host_ok"] = [bool(np.array_equal(h.numpy().view(np.uint32), ref.view(np.uint32))) for h, ref in zip(hb, refs)]
+comm.close()
+print(json.dumps(out))
+"""
+
+
+@pytest.mark.gpu
+def test_configs4_resnet50_buckets_through_plugin(cuda):
+    """configs[4]: ResNet-50-sized gradient buckets (DDP's 25 MiB buckets:
+    3 x 6,553,600 + 5,896,232 fp32; sizes not in the reference, so
+    parity-unpinned as a workload) posted to the plugin's iallreduce and
+    polled with test() — switchml_plugin.cc:293-387 — on device buffers
+    (send != recv) and on pinned host buffers (in place), W = 8, T = 4,
+    P = 256; every bucket bit-exact against the oracle's dummy packet loop."""
+    code = CFG4_DRIVER.format(root=ROOT, pkg=os.path.join(ROOT, "p4app-switchml_amd"), sizes=RESNET50_BUCKETS)
+    ini = ("[general]\nnum_workers = 8\nnum_worker_threads = 4\npacket_numel = 256\n"
+           "max_outstanding_packets = 256\n[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = fused\n")
+    env = dict(os.environ, SWITCHML_CONFIG_INI=ini, SWITCHML_COLLNET_LOOPBACK="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ptrSupport"] == 3
+    assert out["device_sizes"] == [4 * n for n in RESNET50_BUCKETS]
+    assert all(out["device_ok"]) and out["device_send_untouched"]
+    assert out["host_sizes"] == [4 * n for n in RESNET50_BUCKETS]
+    assert all(out["host_ok"])

@@ -39,6 +39,7 @@ elif __name__ == "__main__":
     ini = ("[general]\nnum_workers = %d\nnum_worker_threads = 2\nprepostprocessor = hip_exponent_quantizer\n"
            "[backend.dummy]\nbandwidth = 0\n[backend.hip]\ndevice = 0\n" % world)
     env = dict(os.environ, NCCL_NET_PLUGIN=PLUGIN, NCCL_COLLNET_ENABLE="1", NCCL_DEBUG="INFO",
+               SWITCHML_COLLNET_LOOPBACK="1",
                NCCL_DEBUG_SUBSYS="INIT,NET,ENV", NCCL_DEBUG_FILE=os.path.join(out_dir, "rccl.%p.log"),
                SWITCHML_CONFIG_INI=ini)
     port = 29611
