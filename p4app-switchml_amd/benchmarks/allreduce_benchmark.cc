@@ -265,6 +265,16 @@ int main(int argc, char** argv) {
                            (unsigned long)j, eout, got, error);
                     max_num_errors--;
                 }
+                if (!o.inplace) {  // main.cc:361-367: the input buffer must be left untouched
+                    float in;
+                    memcpy(&in, &src[j], 4);
+                    error = (ein - in) / (ein + std::numeric_limits<float>::epsilon()) * 100;
+                    if (error > o.err) {
+                        printf("Verification error at input buffer index [%lu]. Expected %e but found %e (%.2f%% error).\n",
+                               (unsigned long)j, ein, in, error);
+                        max_num_errors--;
+                    }
+                }
             } else {
                 int32_t ein = (int32_t)ctrl[j], got = (int32_t)out[j];
                 int32_t eout = (int32_t)((uint32_t)ein * (uint32_t)(int64_t)mult);
@@ -273,6 +283,15 @@ int main(int argc, char** argv) {
                     printf("Verification error at output buffer index [%lu]. Expected %d but found %d (%.2f%% error).\n",
                            (unsigned long)j, eout, got, error);
                     max_num_errors--;
+                }
+                if (!o.inplace) {  // main.cc:385-391
+                    const int32_t in = (int32_t)src[j];
+                    error = (ein - in) / (float(ein) + std::numeric_limits<float>::epsilon()) * 100;
+                    if (error > o.err) {
+                        printf("Verification error at input buffer index [%lu]. Expected %d but found %d (%.2f%% error).\n",
+                               (unsigned long)j, ein, in, error);
+                        max_num_errors--;
+                    }
                 }
             }
         }

@@ -74,6 +74,7 @@ bool Config::LoadFromString(const std::string& ini) {
         else if (full == "backend.dummy.fail_worker_thread") backend_.dummy.fail_worker_thread = std::stoi(val);
         else if (full == "backend.hip.device") backend_.hip.device = std::stoi(val);
         else if (full == "backend.hip.mode") backend_.hip.mode = val;
+        else if (full == "backend.hip.packet_ring") backend_.hip.packet_ring = val;
         else fprintf(stderr, "[switchml] ignoring config key '%s' (not used by this build)\n", full.c_str());
     }
     return true;
@@ -118,6 +119,9 @@ void Config::Validate() {
     if (g.backend != "dummy") throw SwitchMLFatal("'" + g.backend + "' is not a backend of this build (dummy only)");
     const std::string& m = backend_.hip.mode;
     if (m != "bulk" && m != "fused" && m != "packet") throw SwitchMLFatal("backend.hip.mode must be bulk|fused|packet");
+    const std::string& r = backend_.hip.packet_ring;
+    if (r != "device" && r != "pinned" && r != "pageable")
+        throw SwitchMLFatal("backend.hip.packet_ring must be device|pinned|pageable");
 }
 
 std::string Config::ToString() const {
@@ -133,7 +137,8 @@ std::string Config::ToString() const {
       << "\n\n[backend.dummy]\nbandwidth = " << backend_.dummy.bandwidth
       << "\nprocess_packets = " << (backend_.dummy.process_packets ? "true" : "false")
       << "\nfail_worker_thread = " << backend_.dummy.fail_worker_thread
-      << "\n\n[backend.hip]\ndevice = " << backend_.hip.device << "\nmode = " << backend_.hip.mode << "\n";
+      << "\n\n[backend.hip]\ndevice = " << backend_.hip.device << "\nmode = " << backend_.hip.mode
+      << "\npacket_ring = " << backend_.hip.packet_ring << "\n";
     return o.str();
 }
 

@@ -44,6 +44,10 @@ struct HipBackendConfig {
     //  "packet" : the reference's per-LTU PreprocessSingle/PostprocessSingle loop
     //             (DummyWorkerThread order) — API-parity mode, slow by design
     std::string mode = "bulk";
+    // Where "packet" mode's ring of b packet buffers lives: "device" (HBM),
+    // "pinned" (page-locked host memory, a NIC's DMA buffers) or "pageable"
+    // (plain malloc) — the per-LTU calls handle all three (staged or direct).
+    std::string packet_ring = "device";
 };
 
 struct BackendConfig {

@@ -64,49 +64,100 @@ void HipExponentQuantizerPPP::ensure_single_buffers() {
     }
 }
 
-// PreprocessSingle — ppp.cc:69-192.
+namespace {
+
+// Where a packet buffer lives, and the address a kernel can use for it:
+// device memory and pinned (page-locked, device-mapped) host memory are
+// written / read by the kernels directly; pageable host memory is staged.
+struct PacketMem {
+    void* dev = nullptr;   // kernel-usable address, null for pageable memory
+    bool host = true;      // the CPU may touch it right after the call returns
+};
+
+PacketMem packet_mem(void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return {};
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return {p, false};
+    if (a.type == hipMemoryTypeHost && a.devicePointer) return {a.devicePointer, true};
+    return {};
+}
+
+}  // namespace
+
+// PreprocessSingle — ppp.cc:69-192.  One kernel per half (quantize of block
+// ltu_id - b, exponent of block ltu_id), writing the packet buffer directly
+// when the device can address it.  Device-memory packets are stream-ordered
+// on stream() (no host sync); a host-memory packet is complete on return, as
+// the reference's is, because the caller hands it to the NIC next.
 void HipExponentQuantizerPPP::PreprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
     const Tensor& s = job_slice_->slice;
     const uint32_t P = (uint32_t)ltu_numel_;
     ensure_single_buffers();
+    bool sync = false;
     if (s.data_type == FLOAT32) {
         if (ltu_id >= batch_num_ltus_) {
             const uint64_t k = ltu_id - batch_num_ltus_;
             const uint64_t off = k * P, n = std::min<uint64_t>(P, s.numel - off);
+            const PacketMem m = packet_mem(entries_ptr);
+            sync |= m.host;
+            // the kernel writes all P words of the block; the reference writes
+            // only the n real ones (ppp.cc:102-109), so a partial block is staged
+            int32_t* dst = (m.dev && n == P) ? static_cast<int32_t*>(m.dev) : d_stage_;
             check(sml_quantize_pack(static_cast<const float*>(s.in_ptr) + off, n, P, config_.general_.num_workers,
-                                    d_recv_exps_ + k, d_stage_, nullptr, 0, stream_),
+                                    d_recv_exps_ + k, dst, nullptr, 0, stream_),
                   "sml_quantize_pack");
-            // only the block's n words are written, as ppp.cc:102-109
-            hip_ok(hipMemcpyAsync(entries_ptr, d_stage_, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+            if (dst == d_stage_)
+                hip_ok(hipMemcpyAsync(entries_ptr, d_stage_, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
             ltu_id = k + batch_num_ltus_;
         }
         if (ltu_id < total_main_num_ltus_) {
             const uint64_t off = ltu_id * P, n = std::min<uint64_t>(P, s.numel - off);
-            check(sml_exponents(static_cast<const float*>(s.in_ptr) + off, n, P, d_stage_exp_, stream_),
-                  "sml_exponents");
-            hip_ok(hipMemcpyAsync(extra_info, d_stage_exp_, 1, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+            const PacketMem m = packet_mem(extra_info);
+            sync |= m.host;
+            // one byte: the int8 exponent in byte 0 of the extra-info slot (byte 1 untouched)
+            int8_t* dst = m.dev ? static_cast<int8_t*>(m.dev) : d_stage_exp_;
+            check(sml_exponents(static_cast<const float*>(s.in_ptr) + off, n, P, dst, stream_), "sml_exponents");
+            if (dst == d_stage_exp_)
+                hip_ok(hipMemcpyAsync(extra_info, d_stage_exp_, 1, hipMemcpyDefault, stream_), "hipMemcpyAsync");
         }
     } else if (s.data_type == INT32) {
         const uint64_t off = ltu_id * P, n = std::min<uint64_t>(P, s.numel - off);
-        check(sml_bswap_i32(static_cast<const int32_t*>(s.in_ptr) + off, d_stage_, n, stream_), "sml_bswap_i32");
-        hip_ok(hipMemcpyAsync(entries_ptr, d_stage_, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+        const PacketMem m = packet_mem(entries_ptr);
+        sync |= m.host;
+        int32_t* dst = m.dev ? static_cast<int32_t*>(m.dev) : d_stage_;
+        check(sml_bswap_i32(static_cast<const int32_t*>(s.in_ptr) + off, dst, n, stream_), "sml_bswap_i32");
+        if (dst == d_stage_)
+            hip_ok(hipMemcpyAsync(entries_ptr, d_stage_, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
     } else {
         throw SwitchMLFatal("unsupported data type");
     }
-    hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    if (sync) hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
-// PostprocessSingle — ppp.cc:194-299.
+// PostprocessSingle — ppp.cc:194-299.  The dequantize kernel reads the packet
+// buffer in place when the device can address it (packet buffers hold P
+// words, ltu_size bytes); the caller may reuse a host-memory packet buffer
+// as soon as this returns, so those calls synchronise.
 void HipExponentQuantizerPPP::PostprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
     const Tensor& s = job_slice_->slice;
     const uint32_t P = (uint32_t)ltu_numel_;
     ensure_single_buffers();
+    bool sync = false;
     if (s.data_type == FLOAT32) {
         if (ltu_id >= batch_num_ltus_) {
             const uint64_t k = ltu_id - batch_num_ltus_;
             const uint64_t off = k * P, n = std::min<uint64_t>(P, s.numel - off);
-            hip_ok(hipMemcpyAsync(d_stage_, entries_ptr, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
-            check(sml_dequantize(d_stage_, d_recv_exps_ + k, n, P, config_.general_.num_workers,
+            const PacketMem m = packet_mem(entries_ptr);
+            sync |= m.host;
+            const int32_t* src = static_cast<const int32_t*>(m.dev);
+            if (!src) {
+                hip_ok(hipMemcpyAsync(d_stage_, entries_ptr, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+                src = d_stage_;
+            }
+            check(sml_dequantize(src, d_recv_exps_ + k, n, P, config_.general_.num_workers,
                                  static_cast<float*>(s.out_ptr) + off, 0, stream_),
                   "sml_dequantize");
             ltu_id = k + batch_num_ltus_;
@@ -114,17 +165,24 @@ void HipExponentQuantizerPPP::PostprocessSingle(uint64_t ltu_id, void* entries_p
         if (ltu_id < total_main_num_ltus_) {
             // ppp.cc:254-260 stores the scale of the received exponent; the
             // kernels derive the same scale from the stored exponent.
+            sync |= packet_mem(extra_info).host;
             hip_ok(hipMemcpyAsync(d_recv_exps_ + ltu_id, extra_info, 1, hipMemcpyDefault, stream_),
                    "hipMemcpyAsync");
         }
     } else if (s.data_type == INT32) {
         const uint64_t off = ltu_id * P, n = std::min<uint64_t>(P, s.numel - off);
-        hip_ok(hipMemcpyAsync(d_stage_, entries_ptr, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
-        check(sml_bswap_i32(d_stage_, static_cast<int32_t*>(s.out_ptr) + off, n, stream_), "sml_bswap_i32");
+        const PacketMem m = packet_mem(entries_ptr);
+        sync |= m.host;
+        const int32_t* src = static_cast<const int32_t*>(m.dev);
+        if (!src) {
+            hip_ok(hipMemcpyAsync(d_stage_, entries_ptr, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
+            src = d_stage_;
+        }
+        check(sml_bswap_i32(src, static_cast<int32_t*>(s.out_ptr) + off, n, stream_), "sml_bswap_i32");
     } else {
         throw SwitchMLFatal("unsupported data type");
     }
-    hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    if (sync) hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
 void HipExponentQuantizerPPP::ExponentsBulk(void* exps_plane) {

@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
+#include <cstring>
 #include <cstdio>
 #include <memory>
 #include <string>
@@ -57,8 +59,34 @@ struct DeviceBuffer {
     }
 };
 
+// Grow-only host buffer: page-locked (hipHostMalloc) or pageable (malloc).
+struct HostBuffer {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    void* get(size_t bytes, bool pin) {
+        if (bytes > cap || pin != pinned) {
+            release();
+            cap = std::max<size_t>(bytes, 4096);
+            pinned = pin;
+            if (pin) hip_ok(hipHostMalloc(&p, cap, hipHostMallocDefault), "hipHostMalloc");
+            else if (!(p = std::malloc(cap))) throw SwitchMLFatal("malloc failed");
+        }
+        return p;
+    }
+    void release() {
+        if (!p) return;
+        if (pinned) (void)hipHostFree(p);
+        else std::free(p);
+        p = nullptr;
+        cap = 0;
+    }
+    ~HostBuffer() { release(); }
+};
+
 struct WorkerState {
     DeviceBuffer in, out, payload, exps, ring, ring_extra;
+    HostBuffer hring, hring_extra;
 };
 
 // DummyWorkerThread's per-packet loop (dummy_worker_thread.cc:86-177) with
@@ -68,16 +96,31 @@ void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerStat
     const uint64_t B = ppp.total_main_num_ltus();
     const uint64_t b = ppp.batch_num_ltus();
     const uint64_t total = B + (extra_batch ? b : 0);
-    int32_t* ring = static_cast<int32_t*>(ws.ring.get(b * P * 4));
-    uint8_t* extra = static_cast<uint8_t*>(ws.ring_extra.get(b * 2));
-    hip_ok(hipMemsetAsync(ring, 0, b * P * 4, ppp.stream()), "hipMemsetAsync");
+    const std::string& where = cfg.backend_.hip.packet_ring;
+    int32_t* ring;
+    uint8_t* extra;
+    if (where == "device") {
+        ring = static_cast<int32_t*>(ws.ring.get(b * P * 4));
+        extra = static_cast<uint8_t*>(ws.ring_extra.get(b * 2));
+        hip_ok(hipMemsetAsync(ring, 0, b * P * 4, ppp.stream()), "hipMemsetAsync");
+    } else {
+        const bool pin = where == "pinned";
+        ring = static_cast<int32_t*>(ws.hring.get(b * P * 4, pin));
+        extra = static_cast<uint8_t*>(ws.hring_extra.get(b * 2, pin));
+        std::memset(ring, 0, b * P * 4);
+    }
+    // ProcessPacket (every entry of the packet x W) on the CPU for a host ring,
+    // as dummy_backend.cc:72-84 does, on the device for an HBM ring
+    const uint16_t W = cfg.general_.num_workers;
     for (uint64_t p = 0; p < b; p++) ppp.PreprocessSingle(p, ring + (p % b) * P, extra + (p % b) * 2);
     for (uint64_t p = 0; p < total; p++) {
         int32_t* ent = ring + (p % b) * P;
         uint8_t* ex = extra + (p % b) * 2;
-        if (cfg.backend_.dummy.process_packets)  // ProcessPacket: every entry of the packet x W
-            sml_ok(sml_loopback_aggregate(ent, P, cfg.general_.num_workers, 0, ppp.stream()),
-                   "sml_loopback_aggregate");
+        if (cfg.backend_.dummy.process_packets && where == "device")
+            sml_ok(sml_loopback_aggregate(ent, P, W, 0, ppp.stream()), "sml_loopback_aggregate");
+        else if (cfg.backend_.dummy.process_packets)
+            for (uint64_t i = 0; i < P; i++)
+                ent[i] = (int32_t)__builtin_bswap32(__builtin_bswap32((uint32_t)ent[i]) * (uint32_t)W);
         ppp.PostprocessSingle(p, ent, ex);
         const uint64_t np = p + b;
         if (np < total) ppp.PreprocessSingle(np, ent, ex);

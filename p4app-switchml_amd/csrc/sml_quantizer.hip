@@ -31,6 +31,23 @@ __device__ __forceinline__ void global_tile_exponents(const QuantArgs& a, uint64
     }
 }
 
+// Quantize + pack 4 consecutive elements (one lane's part of a slice).
+template <int P, bool BE, bool RNE>
+__device__ __forceinline__ void quant_slice(const QuantArgs& a, uint64_t idx, f4 v, const float* lut, int e) {
+    const float s = lut[(uint8_t)e];
+    uint64_t body = 0;
+    if constexpr (RNE) {
+        // VCL body = first n - n%16 elements of the block; only the last
+        // (partial) block has a scalar half-away tail.
+        const uint64_t blk0 = idx / P * P;
+        const uint64_t n = a.numel - blk0 < (uint64_t)P ? a.numel - blk0 : (uint64_t)P;
+        body = blk0 + (n - n % 16);
+    }
+    u4 q = quantize4<RNE>(v, s, idx, body);
+    if constexpr (BE) { q.x = bswap(q.x); q.y = bswap(q.y); q.z = bswap(q.z); q.w = bswap(q.w); }
+    store_payload(a.payload + idx / 4, q);
+}
+
 // Exponents, quantize and pack of one loaded tile (K3: `e` holds the global
 // exponents already).
 template <int P, bool GLOBAL, bool BE, bool RNE>
@@ -49,22 +66,22 @@ __device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, in
         }
     }
     if (!a.payload) return;
+    // A tile inside the padded plane takes a branch-free slice loop.  With a
+    // per-slice `continue` here, hipcc's wait-count pass sees paths that skip
+    // a slice and waits vmcnt(0) at the top of EVERY slice — i.e. on the
+    // previous slice's store as well — which cost K3 (whose first use of the
+    // loaded data is inside this loop) 3 % against K1 (whose exponent reduce
+    // consumes all four slices first): profiles/r02/k1_vs_k3_counters.json,
+    // ab_k3_waitcnt.json.
+    if (base + kTileElems <= padded) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) quant_slice<P, BE, RNE>(a, base + (uint64_t)(u * kWave + lane) * 4, v[u], lut, e[u]);
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < kU; u++) {
         const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-        if (idx >= padded) continue;
-        const float s = lut[(uint8_t)e[u]];
-        uint64_t body = 0;
-        if constexpr (RNE) {
-            // VCL body = first n - n%16 elements of the block; only the last
-            // (partial) block has a scalar half-away tail.
-            const uint64_t blk0 = idx / P * P;
-            const uint64_t n = a.numel - blk0 < (uint64_t)P ? a.numel - blk0 : (uint64_t)P;
-            body = blk0 + (n - n % 16);
-        }
-        u4 q = quantize4<RNE>(v[u], s, idx, body);
-        if constexpr (BE) { q.x = bswap(q.x); q.y = bswap(q.y); q.z = bswap(q.z); q.w = bswap(q.w); }
-        store_payload(a.payload + idx / 4, q);
+        if (idx < padded) quant_slice<P, BE, RNE>(a, idx, v[u], lut, e[u]);
     }
 }
 
@@ -97,6 +114,18 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
     }
 }
 
+// ntohl (BE) -> int -> float, divided by the scale (or multiplied by its
+// exact reciprocal, RCP) — PostprocessSingle's per-element arithmetic.
+template <bool BE, bool RCP>
+__device__ __forceinline__ f4 dequant_words(u4 w, float s) {
+    uint32_t q0 = (uint32_t)w.x, q1 = (uint32_t)w.y, q2 = (uint32_t)w.z, q3 = (uint32_t)w.w;
+    if constexpr (BE) { q0 = bswap(q0); q1 = bswap(q1); q2 = bswap(q2); q3 = bswap(q3); }
+    if constexpr (RCP)
+        return mkf4((float)(int32_t)q0 * s, (float)(int32_t)q1 * s, (float)(int32_t)q2 * s, (float)(int32_t)q3 * s);
+    else
+        return mkf4(dequantize1(q0, s), dequantize1(q1, s), dequantize1(q2, s), dequantize1(q3, s));
+}
+
 struct DequantArgs {
     const u4* payload;
     const int8_t* exps;
@@ -123,13 +152,22 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
         u4 w[kU];
         float s[kU];
         if (full && slice_exps_scalar_ok<P>(a.exps)) {
-            // each slice's exponent bytes with one scalar load (measured: a
-            // per-lane byte load per slice costs ~8 % at P != 256)
+            // Full tile: each slice's exponent bytes with one scalar load
+            // (measured: a per-lane byte load per slice costs ~8 % at
+            // P != 256), then a branch-free slice loop — shared per-slice
+            // blocks with the partial-tile path made hipcc wait vmcnt(0), on
+            // the previous slice's store too, before every slice.
 #pragma unroll
             for (int u = 0; u < kU; u++) {
                 w[u] = __builtin_nontemporal_load(a.payload + (base + (uint64_t)(u * kWave + lane) * 4) / 4);
                 s[u] = lut[slice_exponent_byte<P>(a.exps, base, u, lane)];
             }
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+                store4<ALIGNED>(a.out + idx, dequant_words<BE, RCP>(w[u], s[u]));
+            }
+            continue;
         } else {
 #pragma unroll
             for (int u = 0; u < kU; u++) {
@@ -144,14 +182,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
         for (int u = 0; u < kU; u++) {
             const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
             if (!full && idx >= a.numel) continue;
-            uint32_t q0 = (uint32_t)w[u].x, q1 = (uint32_t)w[u].y, q2 = (uint32_t)w[u].z, q3 = (uint32_t)w[u].w;
-            if constexpr (BE) { q0 = bswap(q0); q1 = bswap(q1); q2 = bswap(q2); q3 = bswap(q3); }
-            f4 o;
-            if constexpr (RCP)
-                o = mkf4((float)(int32_t)q0 * s[u], (float)(int32_t)q1 * s[u], (float)(int32_t)q2 * s[u],
-                         (float)(int32_t)q3 * s[u]);
-            else
-                o = mkf4(dequantize1(q0, s[u]), dequantize1(q1, s[u]), dequantize1(q2, s[u]), dequantize1(q3, s[u]));
+            const f4 o = dequant_words<BE, RCP>(w[u], s[u]);
             if (full) store4<ALIGNED>(a.out + idx, o);
             else store4_guarded(a.out + idx, o, idx, a.numel);
         }

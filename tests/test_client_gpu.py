@@ -49,6 +49,29 @@ def test_allreduce_float_host_tensors(C, mode, T, W, P):
     C.stop()
 
 
+@pytest.mark.parametrize("ring", ["device", "pinned", "pageable"])
+@pytest.mark.parametrize("T,W,P,n", [(2, 2, 256, 20_011), (1, 3, 64, 4_099), (3, 8, 1024, 30_001)])
+def test_packet_mode_ring_placements(C, ring, T, W, P, n):
+    """The per-LTU PreprocessSingle / PostprocessSingle calls with the packet
+    ring in HBM (kernels write / read the packets in place, stream-ordered),
+    in pinned host memory (kernels over PCIe, synchronous calls) and in
+    pageable host memory (staged through HBM): the reference's packet stream
+    (dummy_worker_thread.cc:86-177), bit-exact with the oracle, FLOAT32
+    and INT32."""
+    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, max_outstanding_packets=16 * T,
+                          mode="packet", packet_ring=ring, bandwidth=0))
+    x = O.splitmix_normal(n + W, n)
+    ref = O.dummy_allreduce(x, P=P, max_outstanding_packets=16 * T, num_worker_threads=T, num_workers=W)
+    out = np.empty_like(x)
+    C.allreduce(x, out)
+    assert bits_equal(out, ref)
+    xi = np.random.default_rng(n).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+    oi = np.empty_like(xi)
+    C.allreduce(xi, oi)
+    assert np.array_equal(oi, (xi.astype(np.int64) * W).astype(np.int32))
+    C.stop()
+
+
 @pytest.mark.parametrize("mode", ["bulk", "fused"])
 def test_allreduce_device_tensors(C, mode):
     import torch
@@ -83,6 +106,36 @@ def test_hello_world_binary(cuda):
     r = subprocess.run([os.path.join(BIN, "hello_world")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Data verified successfully" in r.stdout
+
+
+@pytest.mark.parametrize("ttype", ["float", "int32"])
+@pytest.mark.parametrize("device", ["cpu", "gpu"])
+def test_allreduce_benchmark_not_in_place(cuda, device, ttype):
+    """--inplace false: the output is W x input and the input buffer is
+    verified untouched, as main.cc:352-391 checks both buffers.  (float uses
+    the fixed pattern: the reference's random float bit patterns span ~2^250
+    inside one packet, so the quantizer — the reference's too — rounds the
+    small elements of a block to 0 and its own 1 % check fails on them.)"""
+    r = subprocess.run([os.path.join(BIN, "allreduce_benchmark"), "--tensor-numel", "300007",
+                        "--tensor-type", ttype, "--verify", "true", "--inplace", "false", "--num-workers", "3",
+                        "--num-jobs", "3", "--num-warmup-jobs", "1", "--bandwidth", "0", "--device", device,
+                        "--mode", "fused"] + (["--random", "true", "--seed", "5"] if ttype == "int32" else []),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Data verified successfully." in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.parametrize("mode", ["packet"])
+def test_allreduce_benchmark_packet_mode(cuda, mode):
+    """The per-LTU path at a real size (4 M elements, T = 4): every packet is
+    two stream-ordered launches into the HBM ring, no host sync per packet."""
+    r = subprocess.run([os.path.join(BIN, "allreduce_benchmark"), "--tensor-numel", "4194304",
+                        "--tensor-type", "float", "--verify", "true", "--num-workers", "2", "--num-jobs", "2",
+                        "--num-warmup-jobs", "1", "--bandwidth", "0", "--device", "gpu", "--mode", mode],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Data verified successfully." in r.stdout, r.stdout[-2000:]
+    print([l for l in r.stdout.splitlines() if l.startswith("Median")])
 
 
 @pytest.mark.parametrize("device", ["cpu", "gpu"])
