@@ -280,56 +280,78 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
         u4a w[kRxU];
         bool ok[kRxU];
         float s[kRxU];
+        uint64_t f[kRxU];
+        // The state words are read unconditionally (index clamped into the
+        // slice) so that all of them are in flight at once: per-slice guarded
+        // reads made hipcc wait for each one before issuing the next.
         if constexpr (kChunksPerFrame >= kWave) {
             // P >= 256: slice u of the tile lies in one block, so its state
             // words are wave-uniform: scalar loads
             const ConstU64* state = reinterpret_cast<const ConstU64*>(reinterpret_cast<uintptr_t>(a.state));
-            uint64_t f[kRxU];
+            unsigned long long sw[kRxU], se[kRxU];
 #pragma unroll
             for (int u = 0; u < kRxU; u++) {
                 const uint64_t k = t * kBlocksPerTile + (u * kWave) / kChunksPerFrame;
-                ok[u] = false;
-                s[u] = 0.0f;
-                if (k >= a.nblocks) continue;
-                ok[u] = rx_winner(state[k + a.b], a.nframes, f[u]);
-                s[u] = lut[(uint32_t)state[k] & 0xffu];
+                const uint64_t kc = k < a.nblocks ? k : a.nblocks - 1;
+                sw[u] = state[kc + a.b];
+                se[u] = state[kc];
             }
 #pragma unroll
-            for (int u = 0; u < kRxU; u++)
-                if (ok[u])
-                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
-                        a.frames + f[u] * a.stride + 52 + 16ull * ((u * kWave + lane) % kChunksPerFrame)));
+            for (int u = 0; u < kRxU; u++) {
+                const uint64_t k = t * kBlocksPerTile + (u * kWave) / kChunksPerFrame;
+                ok[u] = rx_winner(sw[u], a.nframes, f[u]) && k < a.nblocks;
+                s[u] = lut[(uint32_t)se[u] & 0xffu];
+            }
         } else {
+            unsigned long long sw[kRxU], se[kRxU];
 #pragma unroll
             for (int u = 0; u < kRxU; u++) {
                 const uint64_t k = t * kBlocksPerTile + (u * kWave + lane) / kChunksPerFrame;
-                ok[u] = false;
-                s[u] = 0.0f;
-                if (k >= a.nblocks) continue;
-                uint64_t f;
-                ok[u] = rx_winner(a.state[k + a.b], a.nframes, f);
-                s[u] = lut[(uint32_t)a.state[k] & 0xffu];
-                // non-temporal: 25 % faster than default-policy loads for this stream (hbm_probe)
-                if (ok[u])
-                    w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
-                        a.frames + f * a.stride + 52 + 16ull * ((u * kWave + lane) % kChunksPerFrame)));
+                const uint64_t kc = k < a.nblocks ? k : a.nblocks - 1;
+                sw[u] = a.state[kc + a.b];
+                se[u] = a.state[kc];
             }
+#pragma unroll
+            for (int u = 0; u < kRxU; u++) {
+                const uint64_t k = t * kBlocksPerTile + (u * kWave + lane) / kChunksPerFrame;
+                ok[u] = rx_winner(sw[u], a.nframes, f[u]) && k < a.nblocks;
+                s[u] = lut[(uint32_t)se[u] & 0xffu];
+            }
+        }
+        // Non-temporal payload loads (25 % faster than default-policy loads for
+        // this stream, hbm_probe), issued unconditionally so they are all in
+        // flight together: a slice without a winner reads frame 0's (L2-hot)
+        // bytes instead and its words are zeroed.
+#pragma unroll
+        for (int u = 0; u < kRxU; u++)
+            w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
+                a.frames + (ok[u] ? f[u] : 0ull) * a.stride + 52 + 16ull * ((u * kWave + lane) % kChunksPerFrame)));
+#pragma unroll
+        for (int u = 0; u < kRxU; u++)
+            if (!ok[u]) w[u] = u4a{0u, 0u, 0u, 0u};
+        // Dequantize all slices first, unconditionally (a slice without a
+        // winner computes on zeros and is not stored), then store: with the
+        // first use of the loaded words inside per-slice conditional blocks,
+        // hipcc waited vmcnt(0) — on the previous slice's store too — before
+        // every slice.
+        f4 o[kRxU];
+#pragma unroll
+        for (int u = 0; u < kRxU; u++) {
+            if (pow2)
+                o[u] = mkf4((float)(int32_t)bswap(w[u].x) * s[u], (float)(int32_t)bswap(w[u].y) * s[u],
+                            (float)(int32_t)bswap(w[u].z) * s[u], (float)(int32_t)bswap(w[u].w) * s[u]);
+            else
+                o[u] = mkf4(dequantize1(bswap(w[u].x), s[u]), dequantize1(bswap(w[u].y), s[u]),
+                            dequantize1(bswap(w[u].z), s[u]), dequantize1(bswap(w[u].w), s[u]));
         }
 #pragma unroll
         for (int u = 0; u < kRxU; u++) {
             if (!ok[u]) continue;
             const uint64_t off = t * kRxTileElems + 4ull * (u * kWave + lane);
             if (off >= a.numel) continue;
-            f4 o;
-            if (pow2)
-                o = mkf4((float)(int32_t)bswap(w[u].x) * s[u], (float)(int32_t)bswap(w[u].y) * s[u],
-                         (float)(int32_t)bswap(w[u].z) * s[u], (float)(int32_t)bswap(w[u].w) * s[u]);
-            else
-                o = mkf4(dequantize1(bswap(w[u].x), s[u]), dequantize1(bswap(w[u].y), s[u]),
-                         dequantize1(bswap(w[u].z), s[u]), dequantize1(bswap(w[u].w), s[u]));
             float* p = a.out + off;
-            if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o;
-            else store4_guarded(p, o, 0, a.numel - off);
+            if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o[u];
+            else store4_guarded(p, o[u], 0, a.numel - off);
         }
     }
 }

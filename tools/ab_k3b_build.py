@@ -56,5 +56,6 @@ if __name__ == "__main__":
         build("k3_base")
     if "k3_const" in which:
         build("k3_const", (ORIG, CONST))
-    if "k3_new" in which:
-        build("k3_new")
+    for name in which:
+        if name not in ("k3_base", "k3_const"):
+            build(name)     # any other name: the current product source
