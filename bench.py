@@ -618,7 +618,7 @@ def extra_measurements(sw, torch, x, P, stream, reps=20):
     rx = sw.RxSlice(N, P, 64, device=x.device, out=out)
 
     def rx_once():
-        rx.state.zero_()
+        rx.reset(stream)
         sw.dequantize_frames(frames, fbytes // sw.frame_bytes(P), rx, num_workers=1, stream=stream)
     with torch.cuda.stream(stream):
         t = timeit(rx_once)

@@ -221,12 +221,18 @@ sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_
  *             exponents): zero-filled by the caller before the slice's first
  *             call (rte_bitmap_reset), persists across its calls
  *   d_counts: uint64[2] {accepted, discarded}, added to; nullable, 8-B aligned
- * Three launches on `stream`: claim, dequantize, commit. */
+ * Two launches on `stream`: claim (thread per frame), then dequantize +
+ * retire the winners (wave per 1024 output elements). */
 sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint64_t frame_stride,
                                    uint64_t numel, uint32_t packet_numel, uint16_t num_workers,
                                    uint32_t batch_max, uint64_t job_id, int8_t* d_exps,
                                    uint64_t* d_state, float* d_out, uint64_t* d_counts,
                                    void* stream);
+
+/* rte_bitmap_reset for one slice (dpdk_worker_thread.cc, per job slice):
+ * zero d_state (uint64[B + b]) before the slice's first sml_dequantize_frames
+ * call.  One async memset on `stream`. */
+sml_status_t sml_rx_reset(uint64_t* d_state, uint64_t num_words, void* stream);
 
 /* ---- RDMA messages --------------------------------------
  * The RDMA backend's LTU is a message of msg_numel (1024) elements

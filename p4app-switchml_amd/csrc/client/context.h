@@ -69,6 +69,9 @@ class Context {
 
     // Worker-thread side (context.cc:174-197).
     bool GetJobSlice(WorkerTid worker_thread_id, JobSlice& job_slice);
+    // A job after the one with sched_seq `seq` is queued, so GetJobSlice will
+    // hand this worker thread its slice without blocking on an empty queue.
+    bool HasJobAfter(uint64_t seq) const { return scheduler_ && scheduler_->EnqueuedCount() > seq; }
     void NotifyJobSliceCompletion(WorkerTid worker_thread_id, const JobSlice& job_slice, bool ok = true);
 
     int device() const { return device_; }

@@ -48,11 +48,13 @@ bool FifoScheduler::EnqueueJob(std::shared_ptr<Job> job) {
         return false;
     }
     job->SetJobStatus(QUEUED);
+    job->sched_seq.store(enqueued_.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
     finished_job_slices_[job->id_] = 0;
     dispatched_job_slices_[job->id_] = 0;
     undispatched_job_slices_[job->id_] = config_.general_.num_worker_threads;
     queue_.push(job);
     queue_size_.store(queue_.size(), std::memory_order_release);
+    enqueued_.fetch_add(1, std::memory_order_release);
     job_submitted_event_.notify_all();
     return true;
 }

@@ -51,6 +51,11 @@ class FifoScheduler {
     // or after Stop() every slice that had been handed out.  Only then may
     // the caller publish the job's final status (its buffers are released).
     bool NotifyJobSliceCompletion(WorkerTid worker_thread_id, const JobSlice& job_slice);
+    // Jobs enqueued so far (a job's sched_seq is its position in this count).
+    // A worker thread that has taken the slice of job `seq` will find the next
+    // job without blocking iff EnqueuedCount() > seq: all worker threads take
+    // the slices of the same job between two barriers, in FIFO order.
+    uint64_t EnqueuedCount() const { return enqueued_.load(std::memory_order_acquire); }
     // Fail every queued job and wake all waiting worker threads.  A queued
     // job none of whose slices is running is published FAILED here; one with
     // running slices is marked failed and published by its last slice.
@@ -70,6 +75,7 @@ class FifoScheduler {
     // a worker sleeps on job_submitted_event_
     std::atomic<bool> stopped_flag_{false};
     std::atomic<size_t> queue_size_{0};
+    std::atomic<uint64_t> enqueued_{0};
 };
 
 }  // namespace switchml

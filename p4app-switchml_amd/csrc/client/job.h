@@ -39,6 +39,10 @@ class Job {
     static std::atomic<JobId> next_id_;
     std::atomic<JobStatus> job_status_;
     std::atomic<bool> failed_{false};
+
+  public:
+    // Position in the scheduler's FIFO (1, 2, ...), set when it is enqueued.
+    std::atomic<uint64_t> sched_seq{0};
     std::mutex access_mutex_;
     std::condition_variable job_finished_event_;
 };

@@ -8,6 +8,8 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <vector>
 #include <cstdio>
 #include <memory>
 #include <string>
@@ -137,15 +139,22 @@ uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, J
     hipStream_t st = ppp->stream();
     Tensor& t = js.slice;
     const size_t bytes = t.numel * DataTypeSize(t.data_type);
-    const bool in_dev = IsDevicePointer(t.in_ptr);
-    const bool out_dev = IsDevicePointer(t.out_ptr);
+    // Device tensors are used in place; pinned host tensors too, through
+    // their device mapping (the kernels read and write them over PCIe, both
+    // directions at once — "zero-copy"); pageable host tensors are
+    // staged through HBM with copies on the worker's stream.
+    void* in_d = DeviceAddress(t.in_ptr);
+    void* out_d = (t.out_ptr == t.in_ptr) ? in_d : DeviceAddress(t.out_ptr);
 
     JobSlice staged = js;
-    if (!in_dev) {
+    if (in_d) {
+        staged.slice.in_ptr = in_d;
+    } else {
         staged.slice.in_ptr = ws.in.get(bytes);
         hip_ok(hipMemcpyAsync(staged.slice.in_ptr, t.in_ptr, bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync H2D");
     }
-    if (!out_dev) staged.slice.out_ptr = (t.out_ptr == t.in_ptr) ? staged.slice.in_ptr : ws.out.get(bytes);
+    if (out_d) staged.slice.out_ptr = out_d;
+    else staged.slice.out_ptr = (t.out_ptr == t.in_ptr) ? staged.slice.in_ptr : ws.out.get(bytes);
 
     const uint64_t B = ppp->SetupJobSlice(&staged);
     const uint64_t P = ppp->ltu_numel();
@@ -169,14 +178,38 @@ uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, J
             sml_ok(sml_loopback_aggregate(static_cast<int32_t*>(payload), B * P, W, 0, st), "sml_loopback_aggregate");
         ppp->PostprocessBulk(payload, exps, false);
     }
-    if (!out_dev)
+    if (!out_d)
         hip_ok(hipMemcpyAsync(t.out_ptr, staged.slice.out_ptr, bytes, hipMemcpyDeviceToHost, st), "hipMemcpyAsync D2H");
-    stream_wait(st);
+    // Everything is enqueued on the worker's stream (args captured at launch):
+    // the caller records an event and retires the slice when it completes.
     ppp->CleanupJobSlice();
     return packets;
 }
 
+// Wait for an event: poll for a short while (a slice's kernels usually finish
+// within it), then block.
+void event_wait(hipEvent_t ev) {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(SpinMicros());
+    do {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) hip_ok(q, "hipEventQuery");
+    } while (std::chrono::steady_clock::now() < until);
+    hip_ok(hipEventSynchronize(ev), "hipEventSynchronize");
+}
+
 }  // namespace
+
+void* DeviceAddress(void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged) return p;
+    if (a.type == hipMemoryTypeHost && a.devicePointer) return a.devicePointer;
+    return nullptr;
+}
 
 bool IsDevicePointer(const void* p) {
     hipPointerAttribute_t a;
@@ -218,10 +251,47 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
         setup_error = e.what();
         fprintf(stderr, "[switchml] worker thread %d: %s\n", tid, e.what());
     }
+    auto* hip_ppp = dynamic_cast<HipExponentQuantizerPPP*>(ppp.get());
+    const float bw = config_.backend_.dummy.bandwidth;
+    // Slices whose kernels are still running: the worker takes the next job's
+    // slice (when one is queued) while the GPU finishes the previous one, and
+    // publishes each slice's completion, in order, once its event has passed.
+    // Up to kMaxInFlight per worker; the simulated wire (bandwidth > 0) keeps
+    // the strict one-at-a-time loop of dummy_worker_thread.cc.
+    constexpr size_t kMaxInFlight = 4;
+    struct InFlight {
+        JobSlice js;
+        hipEvent_t ev;
+        uint64_t packets;
+    };
+    std::deque<InFlight> inflight;
+    std::vector<hipEvent_t> events;
+    auto retire = [&](bool wait) {
+        InFlight& f = inflight.front();
+        bool ok = true;
+        try {
+            if (wait) event_wait(f.ev);
+        } catch (const std::exception& e) {
+            fprintf(stderr, "[switchml] worker thread %d: job %llu failed: %s\n", tid,
+                    (unsigned long long)f.js.job->id_, e.what());
+            ok = false;
+        }
+        if (ok) context_.GetStats().AddSlice(tid, f.packets, f.js.slice.numel * DataTypeSize(f.js.slice.data_type));
+        context_.NotifyJobSliceCompletion(tid, f.js, ok);
+        events.push_back(f.ev);
+        inflight.pop_front();
+    };
     WorkerState ws;
     JobSlice js;
+    uint64_t last_seq = 0;  // sched_seq of the last job this thread took a slice of
     while (context_.GetContextState() == Context::RUNNING) {
+        while (!inflight.empty() && hipEventQuery(inflight.front().ev) != hipErrorNotReady) retire(true);
+        if (!inflight.empty() && (inflight.size() >= kMaxInFlight || !context_.HasJobAfter(last_seq))) {
+            retire(true);  // nothing to overlap with: finish the oldest slice first
+            continue;
+        }
         if (!context_.GetJobSlice(tid, js)) continue;
+        last_seq = js.job->sched_seq.load(std::memory_order_relaxed);
         // empty slices and instant_job_completion never touch the PPP
         // (dummy_worker_thread.cc:87-93)
         const bool work = js.slice.numel > 0 && !g.instant_job_completion;
@@ -231,12 +301,26 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
         if (ok && work) {
             try {
                 packets = run_slice(*ppp, config_, ws, js);
+                if (hip_ppp && bw <= 0) {
+                    if (events.empty()) {
+                        hipEvent_t ev;
+                        hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+                        events.push_back(ev);
+                    }
+                    hipEvent_t ev = events.back();
+                    hip_ok(hipEventRecord(ev, hip_ppp->stream()), "hipEventRecord");
+                    events.pop_back();
+                    inflight.push_back(InFlight{js, ev, packets});
+                    js = JobSlice();
+                    continue;
+                }
+                if (hip_ppp) stream_wait(hip_ppp->stream());
             } catch (const std::exception& e) {
                 fprintf(stderr, "[switchml] worker thread %d: job %llu failed: %s\n", tid,
                         (unsigned long long)js.job->id_, e.what());
+                if (hip_ppp) (void)hipStreamSynchronize(hip_ppp->stream());  // nothing may still touch the buffers
                 ok = false;
             }
-            const float bw = config_.backend_.dummy.bandwidth;
             if (ok && bw > 0) {  // the dummy backend's simulated wire time (dummy_backend.cc:124-133)
                 const double ns = 1000.0 * (double)packets * g.packet_numel * 4 * 8 * g.num_worker_threads / bw;
                 // interruptible: Stop() must not wait out a simulated wire
@@ -244,11 +328,15 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
                 wire_cv_.wait_for(lk, std::chrono::nanoseconds((int64_t)std::min(ns, 9.0e18)),
                                   [this] { return context_.GetContextState() != Context::RUNNING; });
             }
-            context_.GetStats().AddSlice(tid, packets, js.slice.numel * DataTypeSize(js.slice.data_type));
+            if (ok) context_.GetStats().AddSlice(tid, packets, js.slice.numel * DataTypeSize(js.slice.data_type));
         }
         context_.NotifyJobSliceCompletion(tid, js, ok);
         js = JobSlice();
     }
+    // stopping: the in-flight slices still own their buffers until their
+    // kernels finish; then they are published (FAILED: the context stopped)
+    while (!inflight.empty()) retire(true);
+    for (hipEvent_t ev : events) (void)hipEventDestroy(ev);
 }
 
 }  // namespace switchml

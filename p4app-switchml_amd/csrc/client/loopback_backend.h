@@ -8,8 +8,9 @@
 // host ring, this backend moves the whole slice through HBM planes
 // (backend.hip.mode = bulk | fused), or — for API parity — runs the
 // reference's per-packet call sequence over a device ring (mode = packet).
-// Host tensors are staged through device buffers (H2D / D2H on the worker's
-// stream); device tensors are used in place.
+// Device tensors are used in place, pinned host tensors through their device
+// mapping (zero-copy over PCIe); pageable host tensors are staged through
+// device buffers (H2D / D2H on the worker's stream).
 #ifndef SWITCHML_AMD_LOOPBACK_BACKEND_H_
 #define SWITCHML_AMD_LOOPBACK_BACKEND_H_
 
@@ -45,6 +46,9 @@ class LoopbackBackend {
 
 // True if p is HIP device (or managed) memory; false for host memory.
 bool IsDevicePointer(const void* p);
+// Address a kernel can use for p: p for device / managed memory, the device
+// mapping of pinned host memory, nullptr for pageable host memory.
+void* DeviceAddress(void* p);
 
 }  // namespace switchml
 

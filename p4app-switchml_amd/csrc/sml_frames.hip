@@ -252,8 +252,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
 // state[k] (low byte = exponent of block k, held by a winner of this call or
 // kRxDone), then gathers the winner's payload and writes out[k*P ..]
 // contiguously.  No header is read again; pkt_ids without a winner in this
-// call (not received, or received earlier) write nothing.  Pass 3 retires the
-// winners.
+// call (not received, or received earlier) write nothing; the same pass then
+// retires the winners.
 constexpr int kRxU = 4;                        // 16-B chunks per lane per iteration
 constexpr int kRxTileElems = kRxU * kWave * 4;
 
@@ -284,11 +284,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
         // The state words are read unconditionally (index clamped into the
         // slice) so that all of them are in flight at once: per-slice guarded
         // reads made hipcc wait for each one before issuing the next.
+        unsigned long long sw[kRxU], se[kRxU];
         if constexpr (kChunksPerFrame >= kWave) {
             // P >= 256: slice u of the tile lies in one block, so its state
             // words are wave-uniform: scalar loads
             const ConstU64* state = reinterpret_cast<const ConstU64*>(reinterpret_cast<uintptr_t>(a.state));
-            unsigned long long sw[kRxU], se[kRxU];
 #pragma unroll
             for (int u = 0; u < kRxU; u++) {
                 const uint64_t k = t * kBlocksPerTile + (u * kWave) / kChunksPerFrame;
@@ -303,7 +303,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
                 s[u] = lut[(uint32_t)se[u] & 0xffu];
             }
         } else {
-            unsigned long long sw[kRxU], se[kRxU];
 #pragma unroll
             for (int u = 0; u < kRxU; u++) {
                 const uint64_t k = t * kBlocksPerTile + (u * kWave + lane) / kChunksPerFrame;
@@ -353,22 +352,23 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o[u];
             else store4_guarded(p, o[u], 0, a.numel - off);
         }
-    }
-}
-
-// Pass 3, thread per pkt_id: the winners of this call retire their pkt_id
-// (state -> kRxDone, keeping the exponent byte) and publish the exponent to
-// exps[pkt_id] — one coalesced sweep instead of two scattered 1-8 byte
-// stores per frame inside pass 2 (partial-line stores from many waves).
-__global__ __launch_bounds__(kBlockThreads) void k_rx_commit(RxArgs a) {
-    const uint64_t n = a.nblocks + a.b;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
-    for (uint64_t k = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; k < n; k += stride) {
-        const unsigned long long st = a.state[k];
-        const uint32_t hi = (uint32_t)(st >> 32);
-        if (hi == 0u || hi == kRxDone) continue;
-        a.state[k] = ((unsigned long long)kRxDone << 32) | (st & 0xffull);
-        if (k < a.nblocks) a.exps[k] = (int8_t)(st & 0xffull);
+        // The commit, folded in (it was a third launch): the lane that owns
+        // block k retires this call's winner of pkt_id k + b (state -> kRxDone,
+        // exponent byte kept), publishes exps[k] once pkt_id k is received, and
+        // for k < b retires the extra-batch pkt_id k too.  Every pkt_id's high
+        // half is read and written by exactly one wave (its own); other waves
+        // read only the low byte, which the retirement keeps.
+#pragma unroll
+        for (int u = 0; u < kRxU; u++) {
+            const uint64_t k = t * kBlocksPerTile + (u * kWave + lane) / kChunksPerFrame;
+            if (((u * kWave + lane) % kChunksPerFrame) != 0 || k >= a.nblocks) continue;
+            const uint32_t hw = (uint32_t)(sw[u] >> 32), he = (uint32_t)(se[u] >> 32);
+            if (hw != 0u && hw != kRxDone)
+                a.state[k + a.b] = ((unsigned long long)kRxDone << 32) | (sw[u] & 0xffull);
+            if (he != 0u) a.exps[k] = (int8_t)(se[u] & 0xffull);
+            if (k < a.b && he != 0u && he != kRxDone)
+                a.state[k] = ((unsigned long long)kRxDone << 32) | (se[u] & 0xffull);
+        }
     }
 }
 
@@ -489,8 +489,13 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
     const uint64_t ntiles = (a.nblocks * P + kRxTileElems - 1) / kRxTileElems;
     if (ntiles) launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
-    k_rx_commit<<<grid_for_vec(a.nblocks + a.b), kBlockThreads, 0, st>>>(a);
     return launch_check();
+}
+
+sml_status_t sml_rx_reset(uint64_t* d_state, uint64_t num_words, void* stream) {
+    if (num_words == 0) return SML_OK;
+    if (!d_state || ((uintptr_t)d_state & 7u)) return SML_ERR_INVALID_ARG;
+    return hip_check(hipMemsetAsync(d_state, 0, num_words * 8, (hipStream_t)stream));
 }
 
 }  // extern "C"

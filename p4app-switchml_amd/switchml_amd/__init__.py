@@ -116,6 +116,8 @@ def lib():
     L.sml_set_xcd_chunk.argtypes = [u32]
     L.sml_dequantize_frames.restype = i32
     L.sml_dequantize_frames.argtypes = [vp, u64, u64, u64, u32, u16, u32, u64, vp, vp, vp, vp, vp]
+    L.sml_rx_reset.restype = i32
+    L.sml_rx_reset.argtypes = [vp, u64, vp]
     L.sml_switch_aggregate.restype = i32
     L.sml_switch_aggregate.argtypes = [vp, vp, u16, u64, u32, vp, vp, vp, u32, vp]
     L.sml_ipc_handle_bytes.restype = u32
@@ -382,6 +384,13 @@ class RxSlice:
         self.state = torch.zeros(max(1, B + min(B, batch_max)), dtype=torch.int64, device=device)
         self.counts = torch.zeros(2, dtype=torch.int64, device=device)
         self.out = out if out is not None else torch.zeros(numel, dtype=torch.float32, device=device)
+
+    def reset(self, stream=None):
+        """rte_bitmap_reset for a new job slice: zero the rx state (one async
+        memset, sml_rx_reset)."""
+        torch = _torch()
+        _check("sml_rx_reset", lib().sml_rx_reset(_dev(self.state, torch.int64, "state"), self.state.numel(),
+                                                  _stream(stream, self.state)))
 
 
 def dequantize_frames(frames, num_frames: int, rx: RxSlice, num_workers: int = 1, job_id: int = 0,

@@ -72,6 +72,28 @@ def test_packet_mode_ring_placements(C, ring, T, W, P, n):
     C.stop()
 
 
+@pytest.mark.parametrize("mode", ["bulk", "fused", "packet"])
+def test_allreduce_pinned_host_tensors(C, mode):
+    """Pinned (page-locked) host tensors go to the kernels through their
+    device mapping — zero-copy over PCIe, no staging copies; in place and
+    not, ragged T = 3 slices (misaligned slice starts), bit-exact."""
+    import torch
+    T, W, P = 3, 2, 256
+    n = 100_003 if mode != "packet" else 20_011
+    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, max_outstanding_packets=64 * T,
+                          mode=mode, bandwidth=0))
+    x = O.splitmix_normal(17, n)
+    ref = O.dummy_allreduce(x, P=P, max_outstanding_packets=64 * T, num_worker_threads=T, num_workers=W)
+    hx = torch.from_numpy(x.copy()).pin_memory()
+    ho = torch.empty_like(hx).pin_memory()
+    C.allreduce(hx, ho)
+    assert bits_equal(ho.numpy(), ref)
+    assert bits_equal(hx.numpy(), x)          # input untouched
+    C.allreduce(hx)                           # in place
+    assert bits_equal(hx.numpy(), ref)
+    C.stop()
+
+
 @pytest.mark.parametrize("mode", ["bulk", "fused"])
 def test_allreduce_device_tensors(C, mode):
     import torch

@@ -273,3 +273,61 @@ def test_p2p_shards_tile_the_blocks(B, world):
         nxt += n
         assert n <= -(-B // world)
     assert nxt == B
+
+
+def _nccl_p2p(rank, world, port, n, P, q):
+    """One GPU per rank, RCCL (backend "nccl"): the production shape of both
+    switches — device all_reduce / all_gather, K6 reading the peers' planes
+    over xGMI through hipIpc mappings."""
+    try:
+        import sys
+        for p in (ROOT, os.path.join(ROOT, "p4app-switchml_amd")):
+            if p not in sys.path:
+                sys.path.insert(0, p)
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dev = torch.device("cuda", rank)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        from switchml_amd.p2pswitch import PeerSwitchAllReduce
+        from switchml_amd.switchsim import SwitchSimAllReduce
+        xs = [worker_data(r, n) for r in range(world)]
+        g = O.switch_exps([O.exponents(xx, P) for xx in xs])
+        agg = O.switch_payload([O.quantize(xx, P, world, global_exps=g) for xx in xs])
+        ref = O.dequantize(agg, g, n, P, world)
+        x = torch.from_numpy(xs[rank]).to(dev)
+        ok = np.array_equal(SwitchSimAllReduce(n, P, dev)(x).cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        ar = PeerSwitchAllReduce(n, P, dev)
+        for _ in range(2):
+            out = ar(x)
+            ok = ok and np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        ar.close()
+        q.put((rank, ok, ""))
+        dist.destroy_process_group()
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, False, repr(ex)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,P", [(100_003, 256), (4 * 1024 * 1024 + 77, 64)])
+def test_p2p_switch_nccl_multi_gpu(cuda, n, P):
+    """the peer-to-peer switch's production path — RCCL with one
+    GPU per rank, K6 reading the other GPUs' HBM over xGMI — called twice,
+    bit-exact against the oracle switch (and the RCCL ring switch-sim
+    likewise).  Needs >= 2 visible GPUs; skipped on a 1-GPU box."""
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        pytest.skip("needs >= 2 GPUs (one per rank)")
+    world = min(ndev, 8)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_nccl_p2p, args=(r, world, port, n, P, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, err in res:
+        assert ok, (rank, err)

@@ -27,7 +27,7 @@ def main(N=64 * 2 ** 20, P=256, bm=64, reps=20):
     rx = sw.RxSlice(N, P, bm, device=dev)
     res = {}
     for name, fn in (("tx", lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=bm, frames=frames)),
-                     ("rx", lambda: (rx.state.zero_(), sw.dequantize_frames(frames, F, rx)))):
+                     ("rx", lambda: (rx.reset(), sw.dequantize_frames(frames, F, rx)))):
         fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
