@@ -29,7 +29,7 @@ def rows(path):
         return list(csv.DictReader(f))
 
 
-def main(tag="r01", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
+def main(tag="r02", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
@@ -61,6 +61,11 @@ def main(tag="r01", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
 
     fetch = pmc("pmc_fetch", "FETCH_SIZE")
     write = pmc("pmc_write", "WRITE_SIZE")
+    cold = None
+    if os.path.isdir(os.path.join(src, "cold_fetch")) and os.path.isdir(os.path.join(src, "cold_write")):
+        cf, cw = pmc("cold_fetch", "FETCH_SIZE"), pmc("cold_write", "WRITE_SIZE")
+        if cf and cw:
+            cold = 2 * 1024 * statistics.mean(cf) + 1024 * statistics.mean(cw)
     B = -(-numel // packet_numel)
     alg_read, alg_write = 4 * numel, 4 * numel + B
     fetch_b = 2 * 1024 * statistics.mean(fetch)
@@ -83,15 +88,21 @@ def main(tag="r01", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
         "hbm_write_bytes_per_launch (WRITE_SIZE x 1024)": write_b,
         "hbm_bytes_per_launch": fetch_b + write_b,
         "traffic_over_algorithmic": (fetch_b + write_b) / (alg_read + alg_write),
+        "cold_hbm_bytes_per_launch (4 distinct buckets cycled)": cold,
+        "cold_traffic_over_algorithmic": None if cold is None else cold / (alg_read + alg_write),
     }
     if os.path.isdir(os.path.join(src, "fr_kt")):
         summary["frames"] = frames_summary(src, dst, numel, packet_numel)
     with open(os.path.join(dst, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
+    traffic = {"source": f"profiles/{tag}/summary.json",
+               "quantize_pack": {"numel": numel, "packet_numel": packet_numel,
+                                 "hbm_bytes_per_launch": round(fetch_b + write_b)}}
+    if cold is not None:
+        traffic["quantize_pack_cold"] = {"numel": numel, "packet_numel": packet_numel,
+                                         "hbm_bytes_per_launch": round(cold)}
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
-        json.dump({"source": f"profiles/{tag}/summary.json",
-                   "quantize_pack": {"numel": numel, "packet_numel": packet_numel,
-                                     "hbm_bytes_per_launch": round(fetch_b + write_b)}}, f, indent=1)
+        json.dump(traffic, f, indent=1)
     print(json.dumps(summary, indent=1))
 
 
@@ -109,7 +120,7 @@ def frames_summary(src, dst, numel, packet_numel, batch_max=64):
     B = -(-numel // packet_numel)
     fbytes = (B + min(B, batch_max)) * (52 + 4 * packet_numel)
     alg = {"k_quantize_frames": (4 * numel, fbytes), "k_rx_apply": (fbytes, 4 * numel),
-           "k_rx_claim": (None, None)}
+           "k_rx_claim": (None, None)}   # k_rx_apply also retires the winners (the old commit pass)
 
     def pmc(sub, counter, key):
         rr = rows(os.path.join(src, sub, "pmc_counter_collection.csv"))
@@ -134,4 +145,4 @@ def frames_summary(src, dst, numel, packet_numel, batch_max=64):
 
 
 if __name__ == "__main__":
-    main(*(sys.argv[1:2] or ["r01"]))
+    main(*(sys.argv[1:2] or ["r02"]))
