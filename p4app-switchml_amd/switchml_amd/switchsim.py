@@ -60,10 +60,24 @@ class SwitchSimAllReduce:
         self.payload = torch.empty(self.B * packet_numel, dtype=torch.int32, device=dev)
 
     def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """All-reduce (SUM) of a FLOAT32 bucket (quantized, as the exponent
+        quantizer PPP does) or an INT32 bucket (the INT32 PPP only reorders
+        bytes, ppp.cc:158-190, 262-298: htonl, the switch's wrapping sum,
+        ntohl — the same words as a wrapping sum in host order)."""
         if x.numel() != self.numel:
             raise ValueError("bucket size changed; build a new SwitchSimAllReduce")
+        if x.dtype not in (torch.float32, torch.int32):
+            raise TypeError("FLOAT32 or INT32 buckets only (common.h:51-55)")
         if out is None:
             out = torch.empty_like(x)
+        if out.dtype != x.dtype:
+            raise TypeError("out must have the bucket's dtype")
+        if x.dtype == torch.int32:
+            plane = self.payload[:self.numel]
+            plane.copy_(x)
+            exchange_payload(plane, self.group)                              # switch: int32 sum
+            out.copy_(plane)
+            return out
         exponents(x, self.P, out=self.exps)                                  # K2
         exchange_exponents(self.exps, self.group)                            # switch: int8 max
         quantize_pack(x, self.P, self.W, global_exps=self.exps, payload=self.payload,

@@ -150,6 +150,7 @@ def _gpu_p2p_int32(rank, world, port, n, P, q):
     try:
         dist = _init(rank, world, port)
         from switchml_amd.p2pswitch import PeerSwitchAllReduce
+        from switchml_amd.switchsim import SwitchSimAllReduce
         dev = torch.device("cuda:0")
         xs = [np.random.default_rng(77 + r).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
               for r in range(world)]
@@ -159,6 +160,8 @@ def _gpu_p2p_int32(rank, world, port, n, P, q):
         out = ar(torch.from_numpy(xs[rank]).to(dev))
         ok = np.array_equal(out.cpu().numpy().view(np.uint32), ref)
         ar.close()
+        out2 = SwitchSimAllReduce(n, P, dev)(torch.from_numpy(xs[rank]).to(dev))
+        ok = ok and np.array_equal(out2.cpu().numpy().view(np.uint32), ref)
         q.put((rank, ok, ""))
         dist.destroy_process_group()
     except Exception as ex:  # pragma: no cover
@@ -168,7 +171,8 @@ def _gpu_p2p_int32(rank, world, port, n, P, q):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,n,P", [(2, 100_003, 256), (3, 4 * 1024 * 64 * 3, 64)])
 def test_p2p_switch_int32_ranks_one_gpu(cuda, world, n, P):
-    """INT32 buckets through the peer-to-peer switch: wrapping sum, bit-exact."""
+    """INT32 buckets through the peer-to-peer switch and the ring switch-sim:
+    wrapping sum, bit-exact."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
