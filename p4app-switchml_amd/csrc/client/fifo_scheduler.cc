@@ -13,8 +13,20 @@ bool Barrier::Wait() {
     if (++count_ == n_) {
         count_ = 0;
         generation_++;
+        generation_flag_.store(generation_, std::memory_order_release);
         cv_.notify_all();
         return true;
+    }
+    if (SpinMicros() > 0) {
+        // The worker threads of one job arrive within microseconds of each
+        // other: poll for a short while before sleeping (a futex wake-up per
+        // job costs about as much as a 25 MiB bucket's kernels).
+        lock.unlock();
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(SpinMicros());
+        while (generation_flag_.load(std::memory_order_acquire) == gen &&
+               !destroyed_flag_.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < until)
+            std::this_thread::yield();
+        lock.lock();
     }
     cv_.wait(lock, [&] { return generation_ != gen || destroyed_; });
     return !destroyed_ || generation_ != gen;
@@ -23,6 +35,7 @@ bool Barrier::Wait() {
 void Barrier::Destroy() {
     std::unique_lock<std::mutex> lock(m_);
     destroyed_ = true;
+    destroyed_flag_.store(true, std::memory_order_release);
     cv_.notify_all();
 }
 

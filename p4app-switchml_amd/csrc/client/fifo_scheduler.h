@@ -33,6 +33,9 @@ class Barrier {
     int count_ = 0;
     uint64_t generation_ = 0;
     bool destroyed_ = false;
+    // lock-free mirrors of generation_ / destroyed_ for the short poll before sleeping
+    std::atomic<uint64_t> generation_flag_{0};
+    std::atomic<bool> destroyed_flag_{false};
 };
 
 // Slice t of T of a job of numel elements (fifo_scheduler.cc:93-109): the
