@@ -63,6 +63,8 @@ def parse(argv=None):
                          "0 = --numel per GPU (weak scaling) at any N")
     ap.add_argument("--switch-numel", type=int, default=CFG3_JOB_NUMEL,
                     help="N > 1: fp32 elements per worker for the switchsim / p2p_switch fields (0 = skip them)")
+    ap.add_argument("--no-plugin", action="store_true",
+                    help="N > 1: skip the configs4_plugin field (ResNet-50 buckets through the CollNet table per rank)")
     ap.add_argument("--buckets", type=int, default=1,
                     help="distinct input buckets (and output planes) the timed steps cycle through: 1 = one "
                          "resident bucket (the headline); >= 4 streams past the 256 MiB Infinity Cache (cold HBM)")
@@ -338,6 +340,17 @@ def main():
             f = fields.get(k, {})
             if "error" in f or not f.get("verified", False):
                 failures.append(f"{k}: {f.get('error', 'not verified')}")
+    if world > 1 and not args.no_plugin:
+        # configs[4] on every GPU at once: each rank hands the ResNet-50 buckets
+        # to its own plugin instance (loopback backend: the ranks do not
+        # exchange — replicas, like the reference's dummy backend processes)
+        try:
+            fields["configs4_plugin"] = plugin_measure_ranks(torch, dist, dev, world)
+            if not fields["configs4_plugin"]["placements_agree_all_ranks"]:
+                failures.append("configs4_plugin: device and pinned-host results differ")
+        except Exception as e:  # noqa: BLE001
+            fields["configs4_plugin"] = {"error": repr(e)[:400]}
+            failures.append(f"configs4_plugin: {fields['configs4_plugin']['error']}")
     extra = {}
     if args.extra and rank == 0:
         extra.update(extra_measurements(sw, torch, torch.randn(args.numel, device=dev, generator=gen), P, stream))
@@ -648,6 +661,28 @@ def extra_measurements(sw, torch, x, P, stream, reps=20):
 
 
 RESNET50_BUCKETS = [6_553_600, 6_553_600, 6_553_600, 5_896_232]   # DDP 25 MiB buckets of 25,557,032 fp32
+
+
+def plugin_measure_ranks(torch, dist, dev, world):
+    """configs[4] at N GPUs: every rank runs plugin_buckets on its own GPU and
+    host buffers at the same time (each GPU has its own PCIe link); reported:
+    max-over-ranks ms per iteration and the aggregate elements/s."""
+    dist.barrier()
+    r = plugin_buckets(torch, dev)
+    t = torch.tensor([r["device"]["ms_per_iteration"], r["pinned_host"]["ms_per_iteration"],
+                      0.0 if r["placements_agree"] else 1.0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    out = {k: r[k] for k in ("buckets", "params", "num_workers", "num_worker_threads", "packet_numel", "mode")}
+    out["ranks"] = world
+    for i, name in enumerate(("device", "pinned_host")):
+        ms = float(t[i])
+        out[name] = {"ms_per_iteration_max_over_ranks": round(ms, 4),
+                     "aggregate_elements_per_s": round(world * r["params"] / (ms * 1e-3), 1),
+                     "aggregate_fp32_GBps": round(world * 4 * r["params"] / (ms * 1e-3) / 1e9, 2)}
+    out["placements_agree_all_ranks"] = float(t[2]) == 0.0
+    out["note"] = ("loopback backend per rank (the plugin does not reduce across ranks, INTEGRATION.md §3): "
+                   "N replicas streaming at once; pinned_host is the H<->D-inclusive rate")
+    return out
 
 
 def plugin_buckets(torch, dev, iters=10):
