@@ -153,6 +153,17 @@ sml_status_t sml_switch_aggregate(const int32_t* const* d_payloads, const int8_t
                                   int32_t* d_payload_out, int8_t* d_exps_out, float* d_out,
                                   uint32_t flags, void* stream);
 
+/* The switch's exponent half alone (p4/exponents.p4:48-54): d_exps_out[k] =
+ * max_w (int8) d_exps[w][k], k < num_blocks — W planes of num_blocks bytes
+ * (local or mapped peers' planes; HOST array of DEVICE pointers). */
+sml_status_t sml_switch_exps(const int8_t* const* d_exps, uint16_t num_workers, uint64_t num_blocks,
+                             int8_t* d_exps_out, void* stream);
+
+/* Copy num_words 32-bit words (any 4-byte alignment; either side may be a
+ * peer's mapped plane or pinned host memory): the all-gather step of the
+ * in-node switch backend.  16-B accesses, the streaming kernels' tile shape. */
+sml_status_t sml_copy_words(const void* d_src, void* d_dst, uint64_t num_words, void* stream);
+
 /* Plane sharing for the peer-to-peer switch: export the allocation holding
  * d_ptr as an IPC handle of sml_ipc_handle_bytes() bytes plus d_ptr's byte
  * offset inside it; open a peer's handle in this process (returns the

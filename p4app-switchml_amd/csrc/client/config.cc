@@ -73,6 +73,9 @@ bool Config::LoadFromString(const std::string& ini) {
         else if (full == "backend.dummy.process_packets") backend_.dummy.process_packets = parse_bool(val);
         else if (full == "backend.dummy.fail_worker_thread") backend_.dummy.fail_worker_thread = std::stoi(val);
         else if (full == "backend.hip.device") backend_.hip.device = std::stoi(val);
+        else if (full == "backend.xgmi.session") backend_.xgmi.session = val;
+        else if (full == "backend.xgmi.max_slice_numel") backend_.xgmi.max_slice_numel = parse_uint<uint64_t>(full, val, ~0ull);
+        else if (full == "backend.xgmi.timeout_ms") backend_.xgmi.timeout_ms = parse_uint<uint64_t>(full, val, ~0ull);
         else if (full == "backend.hip.mode") backend_.hip.mode = val;
         else if (full == "backend.hip.packet_ring") backend_.hip.packet_ring = val;
         else fprintf(stderr, "[switchml] ignoring config key '%s' (not used by this build)\n", full.c_str());
@@ -116,7 +119,19 @@ void Config::Validate() {
         g.max_outstanding_packets = (uint32_t)pick;
     }
     if (g.scheduler != "fifo") throw SwitchMLFatal("'" + g.scheduler + "' is not a valid scheduler");
-    if (g.backend != "dummy") throw SwitchMLFatal("'" + g.backend + "' is not a backend of this build (dummy only)");
+    if (g.backend != "dummy" && g.backend != "xgmi")
+        throw SwitchMLFatal("'" + g.backend + "' is not a backend of this build (dummy | xgmi)");
+    if (g.backend == "xgmi") {
+        const std::string& s = backend_.xgmi.session;
+        if (s.empty() || s.size() > 200 ||
+            s.find_first_not_of("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789-_.") != std::string::npos)
+            throw SwitchMLFatal("backend.xgmi.session must be a non-empty name of [A-Za-z0-9-_.]");
+        if (g.rank >= g.num_workers) throw SwitchMLFatal("general.rank must be < general.num_workers");
+        if (g.num_workers > 16 || g.num_worker_threads > 16)
+            throw SwitchMLFatal("the xgmi backend supports up to 16 workers and 16 worker threads");
+        if (g.prepostprocessor == "bypass") throw SwitchMLFatal("the xgmi backend needs the HIP pre/post-processor");
+        if (backend_.xgmi.max_slice_numel == 0) throw SwitchMLFatal("backend.xgmi.max_slice_numel must be >= 1");
+    }
     const std::string& m = backend_.hip.mode;
     if (m != "bulk" && m != "fused" && m != "packet") throw SwitchMLFatal("backend.hip.mode must be bulk|fused|packet");
     const std::string& r = backend_.hip.packet_ring;
@@ -138,7 +153,10 @@ std::string Config::ToString() const {
       << "\nprocess_packets = " << (backend_.dummy.process_packets ? "true" : "false")
       << "\nfail_worker_thread = " << backend_.dummy.fail_worker_thread
       << "\n\n[backend.hip]\ndevice = " << backend_.hip.device << "\nmode = " << backend_.hip.mode
-      << "\npacket_ring = " << backend_.hip.packet_ring << "\n";
+      << "\npacket_ring = " << backend_.hip.packet_ring
+      << "\n\n[backend.xgmi]\nsession = " << backend_.xgmi.session
+      << "\nmax_slice_numel = " << backend_.xgmi.max_slice_numel << "\ntimeout_ms = " << backend_.xgmi.timeout_ms
+      << "\n";
     return o.str();
 }
 

@@ -50,9 +50,19 @@ struct HipBackendConfig {
     std::string packet_ring = "device";
 };
 
+// The in-node switch (general.backend = "xgmi", xgmi_switch.h): W worker
+// processes of one node (general.rank, general.num_workers) exchange through
+// each other's HBM; `session` names their shared rendezvous segment.
+struct XgmiBackendConfig {
+    std::string session;
+    uint64_t max_slice_numel = 16ull << 20;   // exchange chunk (elements) and plane size per worker thread
+    uint64_t timeout_ms = 60000;              // a worker missing a barrier this long fails the slice
+};
+
 struct BackendConfig {
     DummyBackendConfig dummy;
     HipBackendConfig hip;
+    XgmiBackendConfig xgmi;
 };
 
 class Config {

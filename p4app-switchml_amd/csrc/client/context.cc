@@ -92,7 +92,17 @@ bool Context::Start(Config* config) {
     backend_.reset(new LoopbackBackend(*this, config_));
     number_of_current_jobs_ = 0;
     context_state_ = RUNNING;  // before the workers start, or they exit at once
-    backend_->SetupWorker();
+    try {
+        backend_->SetupWorker();
+    } catch (...) {
+        context_state_ = STOPPING;
+        scheduler_->Stop();
+        backend_->CleanupWorker();
+        backend_.reset();
+        scheduler_.reset();
+        context_state_ = CREATED;
+        throw;
+    }
     return true;
 }
 

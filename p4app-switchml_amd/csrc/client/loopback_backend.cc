@@ -18,6 +18,7 @@
 #include "hip_exponent_quantizer_ppp.h"
 #include "prepostprocessor.h"
 #include "switchml_hip.h"
+#include "xgmi_switch.h"
 
 namespace switchml {
 
@@ -129,7 +130,8 @@ void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerStat
     }
 }
 
-uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, JobSlice& js) {
+uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, JobSlice& js, XgmiSwitch* xs,
+                   WorkerTid tid) {
     auto* ppp = dynamic_cast<HipExponentQuantizerPPP*>(&base);
     if (!ppp) {  // bypass: count packets, move nothing (bypass_ppp.h)
         const uint64_t B = base.SetupJobSlice(&js);
@@ -163,7 +165,10 @@ uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, J
     const bool is_float = t.data_type == FLOAT32;
     uint64_t packets = B + (ppp->NeedsExtraBatch() ? ppp->batch_num_ltus() : 0);
 
-    if (mode == "packet") {
+    if (xs) {
+        // the in-node switch: this slice across the W workers (synchronous)
+        xs->AllReduceSlice(tid, staged.slice.in_ptr, staged.slice.out_ptr, t.numel, t.data_type, st);
+    } else if (mode == "packet") {
         run_packet_loop(*ppp, cfg, ws, ppp->NeedsExtraBatch());
     } else if (mode == "fused" && is_float && cfg.backend_.dummy.process_packets) {
         sml_ok(sml_roundtrip_loopback(static_cast<const float*>(staged.slice.in_ptr),
@@ -220,9 +225,12 @@ bool IsDevicePointer(const void* p) {
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+LoopbackBackend::LoopbackBackend(Context& context, Config& config) : context_(context), config_(config) {}
+
 LoopbackBackend::~LoopbackBackend() { CleanupWorker(); }
 
 void LoopbackBackend::SetupWorker() {
+    if (config_.general_.backend == "xgmi" && !xgmi_) xgmi_.reset(new XgmiSwitch(config_, context_.device()));
     for (int i = 0; i < config_.general_.num_worker_threads; i++)
         threads_.emplace_back(&LoopbackBackend::WorkerMain, this, (WorkerTid)i);
 }
@@ -235,6 +243,7 @@ void LoopbackBackend::CleanupWorker() {
     for (auto& t : threads_)
         if (t.joinable()) t.join();
     threads_.clear();
+    xgmi_.reset();   // leave the session (a barrier with the other workers)
 }
 
 void LoopbackBackend::WorkerMain(WorkerTid tid) {
@@ -300,7 +309,7 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
         uint64_t packets = 0;
         if (ok && work) {
             try {
-                packets = run_slice(*ppp, config_, ws, js);
+                packets = run_slice(*ppp, config_, ws, js, xgmi_.get(), tid);
                 if (hip_ppp && bw <= 0) {
                     if (events.empty()) {
                         hipEvent_t ev;

@@ -15,6 +15,7 @@
 #define SWITCHML_AMD_LOOPBACK_BACKEND_H_
 
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -26,13 +27,14 @@ namespace switchml {
 
 class Context;
 class PrePostProcessor;
+class XgmiSwitch;
 
 class LoopbackBackend {
   public:
-    LoopbackBackend(Context& context, Config& config) : context_(context), config_(config) {}
+    LoopbackBackend(Context& context, Config& config);
     ~LoopbackBackend();
-    void SetupWorker();    // start num_worker_threads worker threads
-    void CleanupWorker();  // join them
+    void SetupWorker();    // (xgmi: join the session) start num_worker_threads worker threads
+    void CleanupWorker();  // join them (xgmi: leave the session)
 
   private:
     void WorkerMain(WorkerTid tid);
@@ -42,6 +44,7 @@ class LoopbackBackend {
     std::vector<std::thread> threads_;
     std::mutex wire_mutex_;              // simulated wire time, cut short by Stop()
     std::condition_variable wire_cv_;
+    std::unique_ptr<XgmiSwitch> xgmi_;   // general.backend = "xgmi": the in-node switch
 };
 
 // True if p is HIP device (or managed) memory; false for host memory.

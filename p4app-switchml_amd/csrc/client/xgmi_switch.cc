@@ -1,0 +1,278 @@
+// xgmi_switch.cc — see xgmi_switch.h.
+#include "xgmi_switch.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "switchml_hip.h"
+
+namespace switchml {
+
+namespace {
+
+constexpr uint32_t kMagic = 0x534d4c58u;   // "SMLX"
+constexpr int kMaxW = SML_MAX_SWITCH_WORKERS;
+constexpr int kMaxT = 16;
+constexpr size_t kHandle = sizeof(hipIpcMemHandle_t);
+
+void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw SwitchMLFatal(std::string("xgmi switch: ") + what + ": " + hipGetErrorString(e));
+}
+
+void sml_ok(int s, const char* what) {
+    if (s != SML_OK)
+        throw SwitchMLFatal(std::string("xgmi switch: ") + what + ": " + sml_status_string((sml_status_t)s) + " " +
+                            sml_last_error());
+}
+
+}  // namespace
+
+// The session segment (zero-filled when created).
+struct alignas(64) ShmBarrier {
+    std::atomic<uint32_t> count;
+    std::atomic<uint32_t> gen;
+    char pad[56];
+};
+
+struct ShmPlanes {
+    unsigned char exps[kHandle], payload[kHandle], out[kHandle];
+    std::atomic<uint32_t> published;
+};
+
+struct XgmiShm {
+    std::atomic<uint32_t> magic;
+    uint32_t W, T, P;
+    uint64_t cap;
+    std::atomic<uint32_t> attached;
+    std::atomic<uint32_t> detached;
+    ShmBarrier bar[kMaxT + 1];             // [t]: worker thread t; [kMaxT]: setup / teardown
+    ShmPlanes planes[kMaxW][kMaxT];
+};
+
+static_assert(std::atomic<uint32_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
+
+XgmiSwitch::XgmiSwitch(const Config& config, int device) {
+    const GeneralConfig& g = config.general_;
+    rank_ = g.rank;
+    W_ = g.num_workers;
+    T_ = g.num_worker_threads;
+    P_ = (uint32_t)g.packet_numel;
+    cap_ = (config.backend_.xgmi.max_slice_numel + 1023) / 1024 * 1024;
+    timeout_ms_ = config.backend_.xgmi.timeout_ms;
+    if (W_ < 1 || W_ > kMaxW) throw SwitchMLFatal("xgmi switch: num_workers must be 1..16");
+    if (T_ < 1 || T_ > kMaxT) throw SwitchMLFatal("xgmi switch: num_worker_threads must be 1..16");
+    if (rank_ < 0 || rank_ >= W_) throw SwitchMLFatal("xgmi switch: general.rank must be < num_workers");
+    name_ = "/switchml-" + config.backend_.xgmi.session;
+
+    hip_ok(hipSetDevice(device), "hipSetDevice");
+    const int fd = shm_open(name_.c_str(), O_CREAT | O_RDWR, 0600);
+    if (fd < 0) throw SwitchMLFatal("xgmi switch: shm_open " + name_ + ": " + strerror(errno));
+    if (ftruncate(fd, sizeof(XgmiShm)) != 0) {
+        close(fd);
+        throw SwitchMLFatal("xgmi switch: ftruncate: " + std::string(strerror(errno)));
+    }
+    void* m = mmap(nullptr, sizeof(XgmiShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) throw SwitchMLFatal("xgmi switch: mmap: " + std::string(strerror(errno)));
+    shm_ = static_cast<XgmiShm*>(m);
+    // every worker writes the same geometry; a mismatch is caught after the
+    // setup barrier
+    uint32_t expected = 0;
+    if (shm_->magic.compare_exchange_strong(expected, kMagic)) {
+        shm_->W = (uint32_t)W_;
+        shm_->T = (uint32_t)T_;
+        shm_->P = P_;
+        shm_->cap = cap_;
+    } else if (expected != kMagic) {
+        throw SwitchMLFatal("xgmi switch: " + name_ + " is not a SwitchML session segment");
+    }
+    if (shm_->attached.fetch_add(1) >= (uint32_t)W_)
+        throw SwitchMLFatal("xgmi switch: session " + name_ + " already has num_workers workers (stale segment?)");
+
+    const uint64_t cap_b = (cap_ + 63) / 64 + 64;   // blocks at the smallest packet size, padded
+    planes_.resize(T_);
+    for (int t = 0; t < T_; t++) {
+        ThreadPlanes& tp = planes_[t];
+        hip_ok(hipMalloc(&tp.exps, cap_b), "hipMalloc");
+        hip_ok(hipMalloc(&tp.payload, cap_ * 4), "hipMalloc");
+        hip_ok(hipMalloc(&tp.out, cap_ * 4), "hipMalloc");
+        hip_ok(hipMalloc(&tp.gexp, cap_b), "hipMalloc");
+        ShmPlanes& sp = shm_->planes[rank_][t];
+        hipIpcMemHandle_t h;
+        hip_ok(hipIpcGetMemHandle(&h, tp.exps), "hipIpcGetMemHandle");
+        memcpy(sp.exps, &h, kHandle);
+        hip_ok(hipIpcGetMemHandle(&h, tp.payload), "hipIpcGetMemHandle");
+        memcpy(sp.payload, &h, kHandle);
+        hip_ok(hipIpcGetMemHandle(&h, tp.out), "hipIpcGetMemHandle");
+        memcpy(sp.out, &h, kHandle);
+        sp.published.store(1, std::memory_order_release);
+    }
+    Barrier(kMaxT);   // every worker's handles are published
+    if (shm_->W != (uint32_t)W_ || shm_->T != (uint32_t)T_ || shm_->P != P_ || shm_->cap != cap_)
+        throw SwitchMLFatal("xgmi switch: workers disagree on num_workers / num_worker_threads / packet_numel / "
+                            "max_slice_numel");
+    for (int t = 0; t < T_; t++) {
+        ThreadPlanes& tp = planes_[t];
+        tp.peer_exps.resize(W_);
+        tp.peer_payload.resize(W_);
+        tp.peer_out.resize(W_);
+        for (int w = 0; w < W_; w++) {
+            if (w == rank_) {
+                tp.peer_exps[w] = tp.exps;
+                tp.peer_payload[w] = tp.payload;
+                tp.peer_out[w] = tp.out;
+                continue;
+            }
+            const ShmPlanes& sp = shm_->planes[w][t];
+            if (!sp.published.load(std::memory_order_acquire)) throw SwitchMLFatal("xgmi switch: peer planes missing");
+            void* p;
+            hipIpcMemHandle_t h;
+            memcpy(&h, sp.exps, kHandle);
+            hip_ok(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+            opened_.push_back(p);
+            tp.peer_exps[w] = static_cast<const int8_t*>(p);
+            memcpy(&h, sp.payload, kHandle);
+            hip_ok(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+            opened_.push_back(p);
+            tp.peer_payload[w] = static_cast<const int32_t*>(p);
+            memcpy(&h, sp.out, kHandle);
+            hip_ok(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+            opened_.push_back(p);
+            tp.peer_out[w] = static_cast<const float*>(p);
+        }
+    }
+}
+
+XgmiSwitch::~XgmiSwitch() {
+    if (!shm_) return;
+    try {
+        Barrier(kMaxT);   // nobody reads a peer's planes any more
+    } catch (...) {
+    }
+    for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+    try {
+        Barrier(kMaxT);   // every mapping of our planes is closed
+    } catch (...) {
+    }
+    for (ThreadPlanes& tp : planes_) {
+        (void)hipFree(tp.exps);
+        (void)hipFree(tp.payload);
+        (void)hipFree(tp.out);
+        (void)hipFree(tp.gexp);
+    }
+    const bool last = shm_->detached.fetch_add(1) + 1 == (uint32_t)W_;
+    munmap(shm_, sizeof(XgmiShm));
+    if (last) shm_unlink(name_.c_str());
+}
+
+// Sense-reversing barrier over the W workers (one per worker thread, so the
+// T slices of a job are exchanged independently).  Polls; a worker that does
+// not arrive within backend.xgmi.timeout_ms fails the slice.
+void XgmiSwitch::Barrier(int index) {
+    ShmBarrier& b = shm_->bar[index];
+    const uint32_t g = b.gen.load(std::memory_order_acquire);
+    if (b.count.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)W_) {
+        b.count.store(0, std::memory_order_relaxed);
+        b.gen.store(g + 1, std::memory_order_release);
+        return;
+    }
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
+    uint32_t spins = 0;
+    while (b.gen.load(std::memory_order_acquire) == g) {
+        if (++spins > 256) {
+            std::this_thread::yield();
+            if ((spins & 1023) == 0 && std::chrono::steady_clock::now() > deadline)
+                throw SwitchMLFatal("xgmi switch: barrier timeout (a worker did not arrive)");
+        }
+    }
+}
+
+void XgmiSwitch::FloatChunk(int tid, const float* in, float* out, uint64_t n, hipStream_t st) {
+    ThreadPlanes& tp = planes_[tid];
+    const uint64_t B = sml_num_blocks(n, P_);
+    const uint64_t S = (B + W_ - 1) / W_;
+    // K2: this worker's exponents; the switch's int8 max over the W planes
+    sml_ok(sml_exponents(in, n, P_, tp.exps, st), "sml_exponents");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    Barrier(tid);
+    sml_ok(sml_switch_exps(tp.peer_exps.data(), (uint16_t)W_, B, tp.gexp, st), "sml_switch_exps");
+    // K3: quantize with the global exponents into the own BE payload plane
+    sml_ok(sml_quantize_pack(in, n, P_, (uint16_t)W_, tp.gexp, tp.payload, nullptr, 0, st), "sml_quantize_pack");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    Barrier(tid);
+    // K6: the wrapping sum of this worker's shard over the W planes, dequantized
+    const uint64_t blk0 = std::min<uint64_t>((uint64_t)rank_ * S, B);
+    const uint64_t nb = std::min<uint64_t>(S, B - blk0);
+    if (nb) {
+        const uint64_t n_el = std::min<uint64_t>(nb * P_, n - blk0 * P_);
+        const int32_t* planes[kMaxW];
+        const int8_t* exps[kMaxW];
+        for (int w = 0; w < W_; w++) {
+            planes[w] = tp.peer_payload[w] + blk0 * P_;
+            exps[w] = tp.gexp + blk0;
+        }
+        sml_ok(sml_switch_aggregate(planes, exps, (uint16_t)W_, n_el, P_, nullptr, nullptr, tp.out + blk0 * P_, 0, st),
+               "sml_switch_aggregate");
+    }
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    Barrier(tid);
+    // the multicast: every shard into this worker's tensor
+    for (int w = 0; w < W_; w++) {
+        const uint64_t b0 = std::min<uint64_t>((uint64_t)w * S, B);
+        const uint64_t nbw = std::min<uint64_t>(S, B - b0);
+        if (!nbw) continue;
+        const uint64_t n_el = std::min<uint64_t>(nbw * P_, n - b0 * P_);
+        sml_ok(sml_copy_words(tp.peer_out[w] + b0 * P_, out + b0 * P_, n_el, st), "sml_copy_words");
+    }
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    Barrier(tid);   // peers are done reading our planes before the next chunk
+}
+
+void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, hipStream_t st) {
+    ThreadPlanes& tp = planes_[tid];
+    const uint64_t B = sml_num_blocks(n, P_);
+    const uint64_t S = (B + W_ - 1) / W_;
+    sml_ok(sml_copy_words(in, tp.payload, n, st), "sml_copy_words");
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    Barrier(tid);
+    const uint64_t blk0 = std::min<uint64_t>((uint64_t)rank_ * S, B);
+    const uint64_t nb = std::min<uint64_t>(S, B - blk0);
+    if (nb) {
+        const int32_t* planes[kMaxW];
+        for (int w = 0; w < W_; w++) planes[w] = tp.peer_payload[w] + blk0 * P_;
+        int32_t* dst = reinterpret_cast<int32_t*>(tp.out) + blk0 * P_;
+        sml_ok(sml_switch_aggregate(planes, nullptr, (uint16_t)W_, nb * P_, P_, dst, nullptr, nullptr,
+                                    SML_FLAG_PAYLOAD_LE, st),
+               "sml_switch_aggregate");
+    }
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    Barrier(tid);
+    for (int w = 0; w < W_; w++) {
+        const uint64_t b0 = std::min<uint64_t>((uint64_t)w * S, B);
+        const uint64_t nbw = std::min<uint64_t>(S, B - b0);
+        if (!nbw) continue;
+        const uint64_t n_el = std::min<uint64_t>(nbw * P_, n - b0 * P_);
+        sml_ok(sml_copy_words(tp.peer_out[w] + b0 * P_, out + b0 * P_, n_el, st), "sml_copy_words");
+    }
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    Barrier(tid);
+}
+
+void XgmiSwitch::AllReduceSlice(int tid, const void* in, void* out, uint64_t numel, DataType type, hipStream_t st) {
+    if (tid < 0 || tid >= T_) throw SwitchMLFatal("xgmi switch: bad worker thread id");
+    for (uint64_t off = 0; off < numel; off += cap_) {
+        const uint64_t n = std::min<uint64_t>(cap_, numel - off);
+        if (type == FLOAT32)
+            FloatChunk(tid, static_cast<const float*>(in) + off, static_cast<float*>(out) + off, n, st);
+        else
+            IntChunk(tid, static_cast<const int32_t*>(in) + off, static_cast<int32_t*>(out) + off, n, st);
+    }
+}
+
+}  // namespace switchml

@@ -1,0 +1,90 @@
+// xgmi_switch.h — the in-node switch backend (general.backend = "xgmi").
+//
+// The reference's workers send every packet to a Tofino switch, which adds
+// the W workers' payload slots as wrapping bit<32> (p4/processor.p4:48-54),
+// takes the signed int8 max of their exponents (p4/exponents.p4:48-54) and
+// multicasts the result (the DPDK / RDMA backends, out of scope here).  On
+// one MI355X node the W workers are W processes, one GPU each, connected by
+// xGMI; this backend is their switch without a switch:
+//
+//   * rendezvous: a POSIX shared-memory segment named by
+//     backend.xgmi.session (the role of the controller's gRPC session setup,
+//     switchml.proto:21-91) holds every worker thread's plane IPC handles and
+//     one barrier per worker thread;
+//   * per FIFO slice (thread t of every worker, the same slice geometry on all
+//     workers, as the switch's slots are): K2 exponents into the own plane →
+//     barrier → the max over the W exponent planes (sml_switch_exps) → K3
+//     quantize with the global exponents into the own BE payload plane →
+//     barrier → K6 on this worker's shard of ceil(B / W) blocks, reading the W
+//     payload planes (W − 1 over xGMI) and writing the dequantized fp32 shard
+//     into the own output plane → barrier → every worker copies the W shards
+//     into its tensor (the multicast) → barrier;
+//   * INT32 slices: the words themselves are summed (the INT32 PPP only
+//     reorders bytes, ppp.cc:158-190, 262-298).
+// Results are bit-identical to the oracle's W-worker software switch
+// (orc_switch_exps / orc_switch_payload + dequantize), slice by slice.
+//
+// All workers must submit the same jobs (same sizes, same order) — the
+// contract the real switch imposes too.  Slices larger than
+// backend.xgmi.max_slice_numel are exchanged in chunks of that many elements
+// (a multiple of every packet size, so block boundaries do not move).
+#ifndef SWITCHML_AMD_XGMI_SWITCH_H_
+#define SWITCHML_AMD_XGMI_SWITCH_H_
+
+#include <hip/hip_runtime_api.h>
+
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "config.h"
+
+namespace switchml {
+
+struct XgmiShm;
+
+class XgmiSwitch {
+  public:
+    // Opens / creates the session segment, allocates this worker's planes for
+    // every worker thread, publishes their IPC handles and maps the peers'
+    // (a barrier over all W workers).  Throws SwitchMLFatal on failure.
+    XgmiSwitch(const Config& config, int device);
+    // Barrier with the other workers, unmap the peers' planes, barrier, free;
+    // the last worker removes the segment.
+    ~XgmiSwitch();
+    XgmiSwitch(const XgmiSwitch&) = delete;
+    XgmiSwitch& operator=(const XgmiSwitch&) = delete;
+
+    // All-reduce worker thread `tid`'s slice across the W workers.  in / out
+    // are device-accessible (HBM or pinned host), may alias; returns when the
+    // result is in `out` (the stream is synchronised).
+    void AllReduceSlice(int tid, const void* in, void* out, uint64_t numel, DataType type, hipStream_t stream);
+
+  private:
+    struct ThreadPlanes {
+        int8_t* exps = nullptr;        // own planes (IPC-exported)
+        int32_t* payload = nullptr;
+        float* out = nullptr;
+        int8_t* gexp = nullptr;        // local: the global exponents
+        std::vector<const int8_t*> peer_exps;      // [W], own included
+        std::vector<const int32_t*> peer_payload;  // [W]
+        std::vector<const float*> peer_out;        // [W]
+    };
+
+    void Barrier(int index);
+    void FloatChunk(int tid, const float* in, float* out, uint64_t n, hipStream_t st);
+    void IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, hipStream_t st);
+
+    int rank_, W_, T_;
+    uint32_t P_;
+    uint64_t cap_;          // elements per chunk (multiple of 1024)
+    uint64_t timeout_ms_;
+    std::string name_;
+    XgmiShm* shm_ = nullptr;
+    std::vector<ThreadPlanes> planes_;
+    std::vector<void*> opened_;  // peer mappings to close
+};
+
+}  // namespace switchml
+
+#endif  // SWITCHML_AMD_XGMI_SWITCH_H_

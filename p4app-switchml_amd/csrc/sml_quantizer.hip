@@ -286,35 +286,6 @@ struct BswapOp {
     __device__ __forceinline__ uint32_t operator()(uint32_t q) const { return bswap(q); }
 };
 
-template <class Op>
-__global__ __launch_bounds__(kBlockThreads) void k_words(const uint32_t* in, uint32_t* out, uint64_t n, uint32_t xcd,
-                                                         Op op) {
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t ntiles = (n + kTileElems - 1) / kTileElems;
-    for (uint64_t t = xcd_block(xcd) * kWavesPerBlock + wave_index(); t < ntiles; t += nwaves) {
-        const uint64_t base = t * kTileElems;
-        if (base + kTileElems <= n) {
-            u4a v[kU];
-#pragma unroll
-            for (int u = 0; u < kU; u++)
-                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(in + base + (u * kWave + lane) * 4));
-#pragma unroll
-            for (int u = 0; u < kU; u++)
-                *reinterpret_cast<u4a*>(out + base + (u * kWave + lane) * 4) =
-                    u4a{op(v[u].x), op(v[u].y), op(v[u].z), op(v[u].w)};
-        } else {
-#pragma unroll
-            for (int u = 0; u < kU; u++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4 + j;
-                    if (idx < n) out[idx] = op(in[idx]);
-                }
-        }
-    }
-}
-
 // Measurement probe (not on the hot path): the same 1024-element tiles and
 // the same access policy as the quantize kernel (non-temporal 16-B loads,
 // default-policy 16-B stores), no arithmetic — the practical HBM ceiling the

@@ -128,6 +128,45 @@ __global__ __launch_bounds__(kBlockThreads) void k_switch_aggregate(SwitchArgs a
     }
 }
 
+// Exponent max over W planes, 4 blocks per thread (one dword per plane when
+// every plane is 4-byte aligned, bytes otherwise).
+struct ExpsMaxArgs {
+    const int8_t* exps[SML_MAX_SWITCH_WORKERS];
+    int8_t* out;
+    uint64_t nblocks;
+    uint32_t nw;
+    uint32_t aligned;
+};
+
+__global__ __launch_bounds__(kBlockThreads) void k_switch_exps(ExpsMaxArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; 4 * i < a.nblocks; i += stride) {
+        const uint64_t k0 = 4 * i;
+        if (a.aligned && k0 + 4 <= a.nblocks) {
+            int m0 = -128, m1 = -128, m2 = -128, m3 = -128;
+            for (uint32_t w = 0; w < a.nw; w++) {
+                const uint32_t d = *reinterpret_cast<const uint32_t*>(a.exps[w] + k0);
+                const int e0 = (int8_t)(d & 0xff), e1 = (int8_t)((d >> 8) & 0xff);
+                const int e2 = (int8_t)((d >> 16) & 0xff), e3 = (int8_t)(d >> 24);
+                m0 = e0 > m0 ? e0 : m0; m1 = e1 > m1 ? e1 : m1; m2 = e2 > m2 ? e2 : m2; m3 = e3 > m3 ? e3 : m3;
+            }
+            *reinterpret_cast<uint32_t*>(a.out + k0) =
+                (uint32_t)(uint8_t)m0 | ((uint32_t)(uint8_t)m1 << 8) | ((uint32_t)(uint8_t)m2 << 16) |
+                ((uint32_t)(uint8_t)m3 << 24);
+        } else {
+            for (uint64_t k = k0; k < k0 + 4 && k < a.nblocks; k++) {
+                int m = -128;
+                for (uint32_t w = 0; w < a.nw; w++) m = a.exps[w][k] > m ? a.exps[w][k] : m;
+                a.out[k] = (int8_t)m;
+            }
+        }
+    }
+}
+
+struct CopyOp {
+    __device__ __forceinline__ uint32_t operator()(uint32_t q) const { return q; }
+};
+
 template <bool ALIGNED, bool BE, bool RCP, bool EXPS>
 static void launch_switch_p(uint32_t P, dim3 grid, hipStream_t st, const SwitchArgs& a) {
     switch (P) {
@@ -193,6 +232,35 @@ sml_status_t sml_switch_aggregate(const int32_t* const* d_payloads, const int8_t
               else launch_switch_m<true, false>(exps, rcp, packet_numel, grid, st, a); }
     else    { if (be) launch_switch_m<false, true>(exps, rcp, packet_numel, grid, st, a);
               else launch_switch_m<false, false>(exps, rcp, packet_numel, grid, st, a); }
+    return launch_check();
+}
+
+sml_status_t sml_switch_exps(const int8_t* const* d_exps, uint16_t num_workers, uint64_t num_blocks,
+                             int8_t* d_exps_out, void* stream) {
+    if (num_workers == 0 || !d_exps || !d_exps_out) return SML_ERR_INVALID_ARG;
+    if (num_workers > SML_MAX_SWITCH_WORKERS) return SML_ERR_UNSUPPORTED;
+    if (num_blocks == 0) return SML_OK;
+    ExpsMaxArgs a{};
+    a.aligned = aligned4(d_exps_out);
+    for (uint32_t w = 0; w < num_workers; w++) {
+        if (!d_exps[w]) return SML_ERR_INVALID_ARG;
+        a.exps[w] = d_exps[w];
+        if (!aligned4(d_exps[w])) a.aligned = 0;
+    }
+    a.out = d_exps_out;
+    a.nblocks = num_blocks;
+    a.nw = num_workers;
+    k_switch_exps<<<grid_for_vec((num_blocks + 3) / 4), kBlockThreads, 0, (hipStream_t)stream>>>(a);
+    return launch_check();
+}
+
+sml_status_t sml_copy_words(const void* d_src, void* d_dst, uint64_t num_words, void* stream) {
+    if (num_words == 0) return SML_OK;
+    if (!d_src || !d_dst || !aligned4(d_src) || !aligned4(d_dst)) return SML_ERR_INVALID_ARG;
+    const uint64_t ntiles = (num_words + kTileElems - 1) / kTileElems;
+    k_words<<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(
+        static_cast<const uint32_t*>(d_src), static_cast<uint32_t*>(d_dst), num_words,
+        g_xcd_chunk.load(std::memory_order_relaxed), CopyOp{});
     return launch_check();
 }
 

@@ -15,11 +15,11 @@
 //    reporting "not done");
 //  * ncclUint8 is widened to int32 on the host as in :318-337, for host
 //    buffers; device uint8 buffers are rejected (ncclInvalidArgument).
-//  * the only backend of this client is the loopback ("dummy"): it multiplies
-//    a rank's own buffer by num_workers instead of summing across ranks, so a
-//    CollNet all-reduce through it is NOT a cross-rank reduction.  init()
-//    therefore refuses (ncclInvalidUsage) unless SWITCHML_COLLNET_LOOPBACK=1
-//    says the caller wants exactly that (tests, single-rank benchmarks).
+//  * backend "xgmi" (the in-node switch, xgmi_switch.h) reduces across the
+//    ranks of one node; the loopback ("dummy") backend multiplies a rank's
+//    own buffer by num_workers instead, so with it init() refuses
+//    (ncclInvalidUsage) unless SWITCHML_COLLNET_LOOPBACK=1 says the caller
+//    wants exactly that (tests, single-rank benchmarks).
 // Configuration: SWITCHML_CONFIG_INI (INI text) or SWITCHML_CONFIG (path),
 // else the reference's search path (/etc/switchml.cfg, ./switchml.cfg, ...).
 //
@@ -84,14 +84,6 @@ int type_size(ncclDataType_t t) {
 
 ncclResult_t sml_init(ncclDebugLogger_t logger) {
     g_logger = logger;
-    const char* lb = getenv("SWITCHML_COLLNET_LOOPBACK");
-    if (!lb || strcmp(lb, "1") != 0) {
-        if (g_logger)
-            g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__,
-                     "SwitchML CollNet: the loopback backend does not reduce across ranks; "
-                     "set SWITCHML_COLLNET_LOOPBACK=1 to use it anyway");
-        return ncclInvalidUsage;
-    }
     try {
         switchml::Context& ctx = switchml::Context::GetInstance();
         if (ctx.GetContextState() == switchml::Context::RUNNING) return ncclSuccess;
@@ -102,6 +94,16 @@ ncclResult_t sml_init(ncclDebugLogger_t logger) {
         else have = cfg.LoadFromFile();
         if (!have) {
             log_info("SwitchML CollNet: no switchml.cfg found");
+            return ncclInvalidUsage;
+        }
+        // the loopback ("dummy") backend multiplies a rank's own buffer by
+        // num_workers instead of summing the ranks' buffers: opt-in only
+        const char* lb = getenv("SWITCHML_COLLNET_LOOPBACK");
+        if (cfg.general_.backend == "dummy" && (!lb || strcmp(lb, "1") != 0)) {
+            if (g_logger)
+                g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__,
+                         "SwitchML CollNet: the loopback backend does not reduce across ranks; use backend = xgmi, "
+                         "or set SWITCHML_COLLNET_LOOPBACK=1 to use it anyway");
             return ncclInvalidUsage;
         }
         return ctx.Start(&cfg) ? ncclSuccess : ncclInternalError;
@@ -146,6 +148,9 @@ ncclResult_t sml_connect(void* handles[], int nranks, int rank, void* listen_com
     (void)handles;
     (void)listen_comm;
     if (rank < 0 || rank >= nranks) return ncclInternalError;  // switchml_plugin.cc:210-213
+    // with the in-node switch the communicator must be the session's workers
+    const switchml::GeneralConfig& g = switchml::Context::GetInstance().GetConfig().general_;
+    if (g.backend == "xgmi" && (nranks != g.num_workers || rank != g.rank)) return ncclInvalidUsage;
     *coll_comm = new CollComm{nranks, rank};
     return ncclSuccess;
 }

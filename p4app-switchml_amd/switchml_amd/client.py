@@ -63,7 +63,8 @@ def make_config(**kw) -> str:
         "backend", "scheduler", "prepostprocessor", "instant_job_completion")}
     dummy = {k: v for k, v in kw.items() if k in ("bandwidth", "process_packets", "fail_worker_thread")}
     hip = {k: v for k, v in kw.items() if k in ("device", "mode", "packet_ring")}
-    unknown = set(kw) - set(general) - set(dummy) - set(hip)
+    xgmi = {k: v for k, v in kw.items() if k in ("session", "max_slice_numel", "timeout_ms")}
+    unknown = set(kw) - set(general) - set(dummy) - set(hip) - set(xgmi)
     if unknown:
         raise KeyError(f"unknown config keys {sorted(unknown)}")
 
@@ -72,6 +73,7 @@ def make_config(**kw) -> str:
     out = "[general]\n" + "".join(f"{k} = {fmt(v)}\n" for k, v in general.items())
     out += "[backend.dummy]\n" + "".join(f"{k} = {fmt(v)}\n" for k, v in dummy.items())
     out += "[backend.hip]\n" + "".join(f"{k} = {fmt(v)}\n" for k, v in hip.items())
+    out += "[backend.xgmi]\n" + "".join(f"{k} = {fmt(v)}\n" for k, v in xgmi.items())
     return out
 
 

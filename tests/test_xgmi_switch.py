@@ -1,0 +1,179 @@
+"""The in-node switch backend (general.backend = "xgmi",
+csrc/client/xgmi_switch.{h,cc}): W worker processes run the reference's
+client API (Context::AllReduce via include/switchml_client.h, and the CollNet
+plugin table) and reduce across each other through their planes' IPC
+mappings — the Tofino switch's int8 exponent max and wrapping int32 sum
+(p4/exponents.p4:48-54, p4/processor.p4:48-54), each FIFO slice
+(fifo_scheduler.cc:93-109) exchanged on its own, then dequantized
+(ppp.cc:194-251).  Checked bit for bit against the oracle's software switch
+over the same W workers.  Here the W processes share cuda:0 (IPC inside one
+device); on a node each worker has its own GPU and the mappings cross xGMI.
+
+CPU: configuration validation of the backend."""
+import os
+import uuid
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def oracle_switch_allreduce(xs, P, T):
+    """W workers' buckets through the reference's switch, slice by slice."""
+    W, n = len(xs), xs[0].size
+    out = np.empty(n, dtype=np.float32)
+    for t in range(T):
+        off, m = O.slice_geometry(n, T, t)
+        if m == 0:
+            continue
+        parts = [x[off:off + m] for x in xs]
+        g = O.switch_exps([O.exponents(p, P) for p in parts])
+        agg = O.switch_payload([O.quantize(p, P, W, global_exps=g) for p in parts])
+        out[off:off + m] = O.dequantize(agg, g, m, P, W)
+    return out
+
+
+def worker_bucket(rank, n, seed):
+    return O.splitmix_normal(seed * 31 + rank, n) * np.float32(2.0 ** (rank % 3 - 1))
+
+
+def _paths():
+    import sys
+    for p in (ROOT, os.path.join(ROOT, "p4app-switchml_amd"), os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _client_worker(rank, W, T, P, session, cap, q):
+    try:
+        _paths()
+        from switchml_amd import client as C
+        C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=T, packet_numel=P,
+                              max_outstanding_packets=64 * T, mode="bulk", bandwidth=0, device=0,
+                              session=session, max_slice_numel=cap))
+        res = []
+        sizes = [100_003, 1, 3 * cap + 517, 0, 4 * P * W + 5]
+        for i, n in enumerate(sizes):
+            where = ("device", "pageable", "pinned")[i % 3]
+            xs = [worker_bucket(r, n, i) for r in range(W)]
+            x = torch.from_numpy(xs[rank].copy())
+            if where == "device":
+                x = x.cuda()
+            elif where == "pinned":
+                x = x.pin_memory()
+            inplace = i % 2 == 0
+            out = x if inplace else torch.empty_like(x)
+            C.allreduce(x, out)
+            got = out.cpu().numpy() if out.is_cuda else out.numpy()
+            ref = oracle_switch_allreduce(xs, P, T)
+            res.append(bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32))))
+        # INT32: the words' wrapping sum over the workers
+        n = 50_021
+        xi = [np.random.default_rng(5 + r).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+              for r in range(W)]
+        t = torch.from_numpy(xi[rank].copy()).cuda()
+        C.allreduce(t)
+        ref = O.bswap32(O.switch_payload([O.bswap32(v) for v in xi]))
+        res.append(bool(np.array_equal(t.cpu().numpy().view(np.uint32), ref)))
+        # several jobs in flight at once, the same order on every worker
+        xs = [[worker_bucket(r, 70_001 + j, 100 + j) for r in range(W)] for j in range(4)]
+        ts = [torch.from_numpy(xs[j][rank].copy()).cuda() for j in range(4)]
+        jobs = [C.allreduce_async(tt) for tt in ts]
+        C.wait_for_all_jobs()
+        for j in range(4):
+            ref = oracle_switch_allreduce(xs[j], P, T)
+            res.append(jobs[j].status() == C.JOB_FINISHED and
+                       bool(np.array_equal(ts[j].cpu().numpy().view(np.uint32), ref.view(np.uint32))))
+        C.stop()
+        q.put((rank, res, ""))
+    except Exception as ex:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()[-2000:]))
+
+
+def _run(target, W, args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, W) + args + (q,)) for r in range(W)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,T,P", [(2, 1, 256), (3, 2, 64), (4, 4, 1024)])
+def test_xgmi_backend_allreduce_matches_oracle_switch(cuda, W, T, P):
+    """Context::AllReduce with backend = xgmi on W worker processes: FLOAT32
+    buckets (device, pageable and pinned host tensors; in place and not;
+    ragged sizes, one element, empty, and slices exchanged in several chunks of
+    max_slice_numel), INT32 buckets, and four jobs in flight — every result
+    bit-exact against the oracle switch over the same W workers."""
+    session = "test-" + uuid.uuid4().hex
+    cap = 8192 * (P // 64)
+    for rank, res, err in _run(_client_worker, W, (T, P, session, cap)):
+        assert res is not None, (rank, err)
+        assert all(res), (rank, res)
+
+
+def _plugin_worker(rank, W, session, q):
+    try:
+        _paths()
+        ini = ("[general]\nbackend = xgmi\nrank = %d\nnum_workers = %d\nnum_worker_threads = 2\npacket_numel = 256\n"
+               "max_outstanding_packets = 128\n[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = bulk\n"
+               "device = 0\n[backend.xgmi]\nsession = %s\n" % (rank, W, session))
+        os.environ["SWITCHML_CONFIG_INI"] = ini
+        os.environ.pop("SWITCHML_COLLNET_LOOPBACK", None)
+        from switchml_amd.collnet import CollNetComm, NCCL_FLOAT32, CollNetError
+        comm = CollNetComm(nranks=W, rank=rank)
+        sizes = [6_553_600, 5_896_232, 1000]     # ResNet-50 DDP buckets (two of them) + a small one
+        xs = [[worker_bucket(r, n, 7 + j) for r in range(W)] for j, n in enumerate(sizes)]
+        send = [torch.from_numpy(xs[j][rank].copy()).cuda() for j in range(len(sizes))]
+        recv = [torch.empty_like(s) for s in send]
+        comm.allreduce_buckets([(s.data_ptr(), r.data_ptr(), s.numel()) for s, r in zip(send, recv)], NCCL_FLOAT32)
+        ok = [bool(np.array_equal(recv[j].cpu().numpy().view(np.uint32),
+                                  oracle_switch_allreduce(xs[j], 256, 2).view(np.uint32))) for j in range(len(sizes))]
+        # a communicator that is not the session's workers is refused
+        try:
+            CollNetComm(nranks=W + 1, rank=rank)
+            ok.append(False)
+        except CollNetError:
+            ok.append(True)
+        comm.close()
+        from switchml_amd import client as C
+        C.stop()
+        q.put((rank, ok, ""))
+    except Exception as ex:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()[-2000:]))
+
+
+@pytest.mark.gpu
+def test_collnet_plugin_over_xgmi_backend(cuda):
+    """The CollNet table (iallreduce / test, switchml_plugin.cc:293-387) on a
+    2-rank communicator with the in-node switch behind it: a real cross-rank
+    SwitchML all-reduce of configs[4]-sized buckets, no loopback opt-in."""
+    session = "plug-" + uuid.uuid4().hex
+    for rank, res, err in _run(_plugin_worker, 2, (session,)):
+        assert res is not None, (rank, err)
+        assert all(res), (rank, res)
+
+
+def test_xgmi_config_validation():
+    from switchml_amd import client as C
+    bad = [dict(backend="xgmi", prepostprocessor="hip_exponent_quantizer"),                 # no session
+           dict(backend="xgmi", session="a b"),                                             # bad name
+           dict(backend="xgmi", session="ok", rank=2, num_workers=2),                       # rank >= W
+           dict(backend="xgmi", session="ok", num_workers=17),
+           dict(backend="xgmi", session="ok", prepostprocessor="bypass")]
+    for kw in bad:
+        with pytest.raises(C.ContextError):
+            C.start(C.make_config(bandwidth=0, **kw))
+        assert C.state() != C.RUNNING
