@@ -19,9 +19,14 @@ switch simulation with W = N real workers (each holding its own 1 GiB bucket):
   switchsim   K2 -> RCCL int8 MAX -> K3 -> RCCL int32 SUM -> K4 (ring, xGMI)
   p2p_switch  K2 -> RCCL int8 MAX -> K3 -> K6 over the peers' HBM (hipIpc,
               xGMI) on this rank's block shard -> RCCL all_gather (fp32)
+  xgmi_switch the client's Context::AllReduce with backend = xgmi (the
+              native in-node switch: shm rendezvous, exponent max over the
+              peers' planes, K3, K6 on this rank's shard, gather)
 each checked (bit-equal to each other, and within the quantization bound of
-an fp32 all-reduce of the same buckets) and set against its xGMI bound.  A
-failed check or an exception exits non-zero.
+an fp32 all-reduce of the same buckets) and set against its xGMI bound; and
+configs4_plugin: the ResNet-50 buckets through the CollNet plugin table on an
+N-rank communicator over the xgmi backend (device and pinned host buffers).
+A failed check or an exception exits non-zero.
 
 Units: value / roofline.achieved = ALGORITHMIC bytes per second: 4N read
 (fp32 in) + 4N written (int32 payload) + B written (int8 exponents),
@@ -336,7 +341,7 @@ def main():
             fields = exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev)
         except Exception as e:  # noqa: BLE001 - recorded, then the run fails
             fields = {"switchsim": {"error": repr(e)[:400]}}
-        for k in ("switchsim", "p2p_switch"):
+        for k in ("switchsim", "p2p_switch", "xgmi_switch"):
             f = fields.get(k, {})
             if "error" in f or not f.get("verified", False):
                 failures.append(f"{k}: {f.get('error', 'not verified')}")
@@ -497,6 +502,8 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
                   host-order int32 payload (SUM, wrapping)
       p2p_switch  the payload summed at the reader from the peers' planes
                   mapped over xGMI (K6), fp32 shards all-gathered
+      xgmi_switch the same switch natively in the client runtime
+                  (Context::AllReduce, backend = xgmi)
     Verified: the two outputs are bit-identical, and both are within the
     quantization bound of an fp32 all-reduce of the same buckets.  Timed:
     max over ranks of the mean of `reps` calls.  xGMI bound: each GPU moves
@@ -559,15 +566,59 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
             del err
         except Exception as e:  # noqa: BLE001
             res[name] = {"error": repr(e)[:400], "pipeline": pipe}
-    same = None
-    if "switchsim" in outs and "p2p_switch" in outs:
-        eq = torch.tensor([int(torch.equal(outs["switchsim"], outs["p2p_switch"]))], dtype=torch.int32, device=dev)
+    # the native in-node switch: the client's Context with backend = xgmi
+    # (C++ runtime, no torch.distributed in the data path)
+    pipe = ("Context::AllReduce, backend xgmi: K2 -> int8 max over the peers' exponent planes -> K3 BE -> K6 on "
+            "this worker's shard over the peers' planes (hipIpc, xGMI) -> gather of the W shards")
+    try:
+        from switchml_amd import client as C
+        session = [f"bench-xgmi-{os.getpid()}-{int(time.time() * 1e3)}" if rank == 0 else None]
+        dist.broadcast_object_list(session, src=0)
+        if C.state() == C.RUNNING:
+            C.stop()
+        C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=1, packet_numel=P,
+                              max_outstanding_packets=256, mode="bulk", bandwidth=0, device=dev.index,
+                              session=session[0], max_slice_numel=64 << 20))
+        out = torch.empty_like(x)
+        C.allreduce(x, out)
+        torch.cuda.synchronize()
+        err = (out - ref).abs()
+        within = bool((err <= tol).all().item())
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            C.allreduce(x, out)
+        torch.cuda.synchronize()
+        tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt[0])
+        C.stop()
+        ok_t = torch.tensor([int(within)], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        outs["xgmi_switch"] = out
+        res["xgmi_switch"] = {"workers": W, "numel_per_worker": n, "packet_numel": P,
+                              "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * n / t / 1e9, 2),
+                              "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
+                              "xgmi_bound_ms": round(bound_s * 1e3, 3), "frac_of_xgmi_bound": round(bound_s / t, 4),
+                              "within_quantization_bound": bool(ok_t.item()),
+                              "max_abs_err_vs_fp32_allreduce": float(err.max().item()), "pipeline": pipe}
+        del err
+    except Exception as e:  # noqa: BLE001
+        res["xgmi_switch"] = {"error": repr(e)[:400], "pipeline": pipe}
+    # the three paths compute the same switch: bit-equal outputs
+    names = [k for k in ("switchsim", "p2p_switch", "xgmi_switch") if k in outs]
+    eqs = {}
+    for k in names:
+        if k == "switchsim" or "switchsim" not in outs:
+            continue
+        eq = torch.tensor([int(torch.equal(outs["switchsim"], outs[k]))], dtype=torch.int32, device=dev)
         dist.all_reduce(eq, op=dist.ReduceOp.MIN)
-        same = bool(eq.item())
-    for name in ("switchsim", "p2p_switch"):
+        eqs[k] = bool(eq.item())
+    for name in ("switchsim", "p2p_switch", "xgmi_switch"):
         r = res[name]
         if "error" not in r:
-            r["bit_equal_to_other_path"] = same
+            same = all(eqs.values()) if name == "switchsim" else eqs.get(name)
+            r["bit_equal_to_switchsim" if name != "switchsim" else "bit_equal_to_other_paths"] = same
             r["verified"] = bool(r["within_quantization_bound"] and same)
         r["xgmi_link_GBps_assumed"] = XGMI_LINK_GBPS
     res["p2p_switch"]["status"] = "experimental (first cross-GPU run is the driver's multi-GPU bench)"
@@ -664,15 +715,24 @@ RESNET50_BUCKETS = [6_553_600, 6_553_600, 6_553_600, 5_896_232]   # DDP 25 MiB b
 
 
 def plugin_measure_ranks(torch, dist, dev, world):
-    """configs[4] at N GPUs: every rank runs plugin_buckets on its own GPU and
-    host buffers at the same time (each GPU has its own PCIe link); reported:
-    max-over-ranks ms per iteration and the aggregate elements/s."""
+    """configs[4] at N GPUs: every rank hands the ResNet-50 buckets to its
+    CollNet plugin instance at once, on an N-rank communicator whose backend
+    is the in-node switch (general.backend = xgmi): a real SwitchML
+    all-reduce across the N GPUs over xGMI.  Reported: max-over-ranks ms per
+    iteration, device and pinned host buffers (the H<->D-inclusive rate), and
+    aggregate elements/s = N x params / t."""
+    rank = dist.get_rank()
+    session = [f"bench-cfg4-{os.getpid()}-{int(time.time() * 1e3)}" if rank == 0 else None]
+    dist.broadcast_object_list(session, src=0)
+    ini = ("[general]\nbackend = xgmi\nrank = %d\nnum_workers = %d\nnum_worker_threads = 4\npacket_numel = 256\n"
+           "max_outstanding_packets = 256\n[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = bulk\ndevice = %d\n"
+           "[backend.xgmi]\nsession = %s\n" % (rank, world, dev.index, session[0]))
     dist.barrier()
-    r = plugin_buckets(torch, dev)
+    r = plugin_buckets(torch, dev, ini=ini, nranks=world, rank=rank)
     t = torch.tensor([r["device"]["ms_per_iteration"], r["pinned_host"]["ms_per_iteration"],
                       0.0 if r["placements_agree"] else 1.0], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    out = {k: r[k] for k in ("buckets", "params", "num_workers", "num_worker_threads", "packet_numel", "mode")}
+    out = {k: r[k] for k in ("buckets", "params", "num_workers", "num_worker_threads", "packet_numel", "backend")}
     out["ranks"] = world
     for i, name in enumerate(("device", "pinned_host")):
         ms = float(t[i])
@@ -680,35 +740,44 @@ def plugin_measure_ranks(torch, dist, dev, world):
                      "aggregate_elements_per_s": round(world * r["params"] / (ms * 1e-3), 1),
                      "aggregate_fp32_GBps": round(world * 4 * r["params"] / (ms * 1e-3) / 1e9, 2)}
     out["placements_agree_all_ranks"] = float(t[2]) == 0.0
-    out["note"] = ("loopback backend per rank (the plugin does not reduce across ranks, INTEGRATION.md §3): "
-                   "N replicas streaming at once; pinned_host is the H<->D-inclusive rate")
+    out["note"] = ("CollNet iallreduce/test on an N-rank communicator, backend xgmi (the in-node switch: "
+                   "exponent max, K3, K6 over the peers' planes, gather); pinned_host = H<->D-inclusive rate")
     return out
 
 
-def plugin_buckets(torch, dev, iters=10):
+def plugin_buckets(torch, dev, iters=10, ini=None, nranks=1, rank=0):
     """configs[4]: ResNet-50-sized gradient buckets handed to the RCCL CollNet
     plugin's iallreduce and polled with test() (switchml_plugin.cc:293-387),
     all four buckets in flight per iteration, as RCCL's proxy posts them.
     Placements: device buffers (ptrSupport CUDA: the HIP quantizer works in
     place in HBM) and pinned host buffers (what the reference's HOST-only
-    plugin is handed: staged H2D -> kernels -> D2H by the worker threads).
-    Backend: the loopback (W = 8, T = 4, fused round trip)."""
+    plugin is handed; read and written by the kernels over PCIe).
+    Backend: the loopback (W = 8, T = 4, fused round trip) unless `ini`
+    names another (the in-node switch at N > 1)."""
     import numpy as np
-    os.environ["SWITCHML_CONFIG_INI"] = (
-        "[general]\nnum_workers = 8\nnum_worker_threads = 4\npacket_numel = 256\nmax_outstanding_packets = 256\n"
-        "[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = fused\n")
-    os.environ["SWITCHML_COLLNET_LOOPBACK"] = "1"
+    if ini is None:
+        ini = ("[general]\nnum_workers = 8\nnum_worker_threads = 4\npacket_numel = 256\nmax_outstanding_packets = 256\n"
+               "[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = fused\n")
+        os.environ["SWITCHML_COLLNET_LOOPBACK"] = "1"
+    os.environ["SWITCHML_CONFIG_INI"] = ini
+    from switchml_amd import client as C
     from switchml_amd.collnet import CollNetComm, NCCL_FLOAT32
-    comm = CollNetComm()
+    if C.state() == C.RUNNING:
+        C.stop()
+    comm = CollNetComm(nranks=nranks, rank=rank)
     g = torch.Generator(device=dev)
-    g.manual_seed(7)
+    g.manual_seed(7 + rank)
     dsend = [torch.randn(n, device=dev, generator=g) * 1e-3 for n in RESNET50_BUCKETS]
     drecv = [torch.empty_like(d) for d in dsend]
     hsend = [d.cpu().pin_memory() for d in dsend]
     hrecv = [torch.empty_like(h).pin_memory() for h in hsend]
     total = sum(RESNET50_BUCKETS)
-    res = {"buckets": RESNET50_BUCKETS, "params": total, "num_workers": 8, "num_worker_threads": 4,
-           "packet_numel": 256, "mode": "fused"}
+    cfg = C.config_text()
+    res = {"buckets": RESNET50_BUCKETS, "params": total,
+           "num_workers": int(cfg.split("num_workers = ")[1].split()[0]),
+           "num_worker_threads": int(cfg.split("num_worker_threads = ")[1].split()[0]),
+           "packet_numel": 256, "backend": cfg.split("backend = ")[1].split()[0],
+           "mode": cfg.split("mode = ")[1].split()[0]}
     for name, snd, rcv in (("device", dsend, drecv), ("pinned_host", hsend, hrecv)):
         jobs = [(s.data_ptr(), r.data_ptr(), s.numel()) for s, r in zip(snd, rcv)]
         comm.allreduce_buckets(jobs, NCCL_FLOAT32)
@@ -722,6 +791,7 @@ def plugin_buckets(torch, dev, iters=10):
                      "fp32_GBps": round(4 * total / t / 1e9, 2)}
     res["placements_agree"] = all(bool(torch.equal(r.cpu(), h)) for r, h in zip(drecv, hrecv))
     comm.close()
+    C.stop()
     return res
 
 

@@ -1,0 +1,8 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/r02o
+mkdir -p $OUT
+SML_BENCH_REHEARSE=1 timeout -k 10 400 python bench.py --gpus 2 --switch-numel 4194304 --steps 20 --warmup 20 > $OUT/bench2.json 2> $OUT/bench2.err
+echo "rc=$?" >> $OUT/bench2.err
+SML_BENCH_REHEARSE=1 timeout -k 10 400 python bench.py --gpus 3 --switch-numel 1048583 --steps 20 --warmup 20 > $OUT/bench3.json 2> $OUT/bench3.err
+echo "rc=$?" >> $OUT/bench3.err
