@@ -146,7 +146,10 @@ uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, J
     // directions at once — "zero-copy"); pageable host tensors are
     // staged through HBM with copies on the worker's stream.
     void* in_d = DeviceAddress(t.in_ptr);
-    void* out_d = (t.out_ptr == t.in_ptr) ? in_d : DeviceAddress(t.out_ptr);
+    // the in-node switch reads its input twice (exponents, then quantize):
+    // a host input is copied into HBM once instead of crossing PCIe twice
+    if (xs && in_d && !IsDevicePointer(t.in_ptr)) in_d = nullptr;
+    void* out_d = DeviceAddress(t.out_ptr);
 
     JobSlice staged = js;
     if (in_d) {
