@@ -35,8 +35,10 @@ def switch_return(sent, stride, P, W):
     return f
 
 
-def rx_stream(x, P, W, batch_max, job_id, seed, n_dups=3, n_wrong=2, bad_pid=True):
-    """(frames [F, stride] uint8 in rx order, number of frames that must be discarded)."""
+def rx_stream(x, P, W, batch_max, job_id, seed, n_dups=3, n_wrong=2, bad_pid=True, shuffle=True):
+    """(frames [F, stride] uint8 in rx order, number of frames that must be discarded).
+    shuffle=False keeps the switch's return order (frame f carries pkt_id f)
+    before the anomalies are inserted."""
     stride = 52 + 4 * P
     sent = O.build_frames(x, _params(job_id), P=P, num_workers=W, batch_max=batch_max)
     ret = switch_return(sent, stride, P, W)
@@ -46,7 +48,8 @@ def rx_stream(x, P, W, batch_max, job_id, seed, n_dups=3, n_wrong=2, bad_pid=Tru
     order = []
     for w0 in range(0, B + b, b):
         win = list(range(w0, min(w0 + b, B + b)))
-        rng.shuffle(win)
+        if shuffle:
+            rng.shuffle(win)
         order += win
     rows = [ret[i] for i in order]
     discard = 0
@@ -240,5 +243,118 @@ def test_rx_frames_random_streams(cuda):
         assert np.array_equal(out.view(np.uint32), ref.out.view(np.uint32))
         assert np.array_equal(exps, ref.exps)
         assert cnt == ref.counts
+
+    check()
+
+
+# ------------------------------------------------------ in-order streams --
+# The switch's return order (frame f carries pkt_id p0 + f), split into rx
+# bursts, with and without one anomaly deep inside a later burst: the common
+# case of the receive loop, and the edge cases an in-order fast path would
+# have to get right (one was tried and measured slower).
+
+def _in_order_case(torch, sw, n, P, W, bm, job, cuts, edit=None, where="device"):
+    x = O.splitmix_normal(n + 7 * P + W, n)
+    frames, _ = rx_stream(x, P, W, bm, job_id=job, seed=n, n_dups=0, n_wrong=0, bad_pid=False, shuffle=False)
+    if edit is not None:
+        frames = edit(frames)
+    F = frames.shape[0]
+    cuts = [0] + [c for c in cuts if 0 < c < F] + [F]
+    ref = O.RxState(n, P, bm)
+    for a, c in zip(cuts[:-1], cuts[1:]):
+        O.dequantize_frames(frames[a:c], int(c - a), frames.shape[1], ref, W, job_id=job)
+    dev = torch.device("cuda:0")
+    stride = frames.shape[1]
+    t = torch.from_numpy(frames.reshape(-1).copy())
+    t = t.to(dev) if where == "device" else t.pin_memory()
+    rx = sw.RxSlice(n, P, bm, device=dev)
+    for a, c in zip(cuts[:-1], cuts[1:]):
+        sw.dequantize_frames(t[a * stride:c * stride], int(c - a), rx, num_workers=W, job_id=job, stride=stride)
+    torch.cuda.synchronize()
+    assert np.array_equal(rx.out.cpu().numpy().view(np.uint32), ref.out.view(np.uint32))
+    assert np.array_equal(rx.exps.cpu().numpy(), ref.exps)
+    assert [int(v) for v in rx.counts.cpu()] == ref.counts
+    return ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [64, 128, 256, 512, 1024])
+@pytest.mark.parametrize("where", ["device", "pinned"])
+def test_rx_in_order_bursts(cuda, P, where):
+    """In-order bursts of one slice (p0 > 0 after the first), counters included."""
+    import torch
+    import switchml_amd as sw
+    n = 200_000 + P + 3
+    ref = _in_order_case(torch, sw, n, P, 3, 16, 0x21, cuts=[1, 40, 1000, 1001, 2500], where=where)
+    assert ref.counts[1] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [64, 256, 1024])
+@pytest.mark.parametrize("kind", ["wrong_job", "dup_of_earlier_call", "swap", "bad_pid", "dup_in_call"])
+def test_rx_in_order_then_miss(cuda, P, kind):
+    """An in-order stream with one anomaly deep inside a later call: the
+    result equals the oracle loop's."""
+    import torch
+    import switchml_amd as sw
+    n, bm = 150_000 + 5, 8
+
+    def edit(fr):
+        fr = fr.copy()
+        i = fr.shape[0] * 2 // 3
+        if kind == "wrong_job":
+            fr[i, 43] ^= 0x01
+        elif kind == "dup_of_earlier_call":         # a copy of frame 3 (first call) inside the second call
+            fr = np.concatenate([fr[:i], fr[3:4], fr[i:]])
+        elif kind == "swap":
+            fr[[i, i + 1]] = fr[[i + 1, i]]
+        elif kind == "bad_pid":
+            fr[i, 44:48] = np.frombuffer(np.uint32(0xFFFFFF00).tobytes(), dtype=np.uint8)
+        else:                                     # garbage second copy of frame i, right after it
+            d = fr[i].copy()
+            d[52:] ^= 0xA5
+            fr = np.concatenate([fr[:i + 1], d[None], fr[i + 1:]])
+        return fr
+    B = O.num_blocks(n, P)
+    _in_order_case(torch, sw, n, P, 2, bm, 0x5A, cuts=[(B + bm) // 3], edit=edit)
+
+
+@pytest.mark.gpu
+def test_rx_in_order_random(cuda):
+    """Hypothesis (derandomized): in-order streams split into random bursts,
+    with 0-2 anomalies (swap, duplicate of an earlier frame, wrong job, bad
+    pkt_id) at random places, vs the oracle loop."""
+    pytest.importorskip("hypothesis")
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+    import torch
+    import switchml_amd as sw
+
+    @settings(max_examples=60, deadline=None, derandomize=True, suppress_health_check=list(HealthCheck))
+    @given(n=st.integers(1, 30_000), P=st.sampled_from([64, 128, 256, 512, 1024]), W=st.sampled_from([1, 2, 3, 8]),
+           bm=st.integers(1, 70), job=st.integers(0, 255), calls=st.integers(1, 5), seed=st.integers(0, 2 ** 31),
+           anomalies=st.lists(st.tuples(st.sampled_from(["swap", "dup", "job", "pid"]), st.floats(0, 1)),
+                              max_size=2))
+    def check(n, P, W, bm, job, calls, seed, anomalies):
+        rng = np.random.default_rng(seed)
+
+        def edit(fr):
+            fr = fr.copy()
+            for kind, at in anomalies:
+                i = min(int(at * fr.shape[0]), fr.shape[0] - 1)
+                if kind == "swap" and i + 1 < fr.shape[0]:
+                    fr[[i, i + 1]] = fr[[i + 1, i]]
+                elif kind == "dup":
+                    j = int(rng.integers(0, i + 1))
+                    fr = np.concatenate([fr[:i + 1], fr[j:j + 1], fr[i + 1:]])
+                elif kind == "job":
+                    fr[i, 43] ^= 0x80
+                elif kind == "pid":
+                    fr[i, 44:48] = np.frombuffer(np.uint32(int(rng.integers(0, 2 ** 32))).tobytes(), dtype=np.uint8)
+            return fr
+        B = O.num_blocks(n, P)
+        F = B + min(B, bm)
+        cuts = sorted(int(c) for c in rng.integers(1, F + 2, calls - 1)) if calls > 1 else []
+        _in_order_case(torch, sw, n, P, W, bm, job, cuts=cuts, edit=edit)
 
     check()
