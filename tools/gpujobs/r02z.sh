@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/r02z
+mkdir -p $OUT
+timeout -k 10 300 python tools/zero_copy_rt.py > $OUT/zc.json 2> $OUT/zc.err
