@@ -132,6 +132,23 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
                                     int32_t* d_payload, int8_t* d_exps_out,
                                     uint32_t flags, void* stream);
 
+/* The fused round trip over a batch of job slices in ONE launch (the
+ * client's worker submits every slice of the jobs queued so far together):
+ * slice i is exactly sml_roundtrip_loopback(in, out, numel, ...) — its blocks
+ * start at its own first element (FIFO slices, fifo_scheduler.cc:93-109) — and
+ * no payload / exponent planes are written.  Any 4-byte alignment; slices
+ * must not overlap each other (a slice's in == out is fine); numel == 0
+ * slices are skipped.  Flags: SML_FLAG_ROUND_RNE (the payload byte order is
+ * not observable here). */
+#define SML_MAX_BATCH_SLICES 64
+typedef struct sml_slice {
+    const float* in;
+    float* out;
+    uint64_t numel;
+} sml_slice;
+sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_slices, uint32_t packet_numel,
+                                          uint16_t num_workers, uint32_t flags, void* stream);
+
 /* ---- The switch's aggregation ---------------------------
  * K6: what the Tofino pipeline does to W workers' packets for one slot, over
  * whole planes, fused with the worker's dequantize:

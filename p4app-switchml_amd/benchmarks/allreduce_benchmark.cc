@@ -60,7 +60,7 @@ void usage() {
                  "  --seed arg (=0)                    Random seed (0 = time).\n"
                  "  --dump-stats arg (=0)              Print and clear the switchml statistics after each sync?\n"
                  "  --config arg                       switchml.cfg to use (MI355X build)\n"
-                 "  --mode / --num-workers / --num-worker-threads / --packet-numel / --bandwidth\n"
+                 "  --mode / --num-workers / --num-worker-threads / --packet-numel / --bandwidth / --batch-jobs\n"
                  "                                     config overrides (MI355X build)\n";
 }
 
@@ -104,6 +104,7 @@ Opts parse(int argc, char** argv) {
         else if (a == "--num-worker-threads") o.overrides["general.num_worker_threads"] = v;
         else if (a == "--packet-numel") o.overrides["general.packet_numel"] = v;
         else if (a == "--bandwidth") o.overrides["backend.dummy.bandwidth"] = v;
+        else if (a == "--batch-jobs") o.overrides["backend.hip.batch_jobs"] = v;
         else {
             std::cerr << "unrecognised option '" << a << "'\n";
             exit(EXIT_FAILURE);

@@ -48,6 +48,13 @@ struct HipBackendConfig {
     // "pinned" (page-locked host memory, a NIC's DMA buffers) or "pageable"
     // (plain malloc) — the per-LTU calls handle all three (staged or direct).
     std::string packet_ring = "device";
+    // mode = fused, loopback switch, no simulated wire: ONE worker thread
+    // takes every slice of up to batch_jobs queued jobs (at most
+    // SML_MAX_BATCH_SLICES slices) and runs them in one kernel launch
+    // (sml_roundtrip_loopback_batch) — same FIFO slice geometry and results,
+    // one launch instead of num_worker_threads per job.  0: every worker
+    // thread launches its own slice (the reference's threading).
+    uint32_t batch_jobs = 16;
 };
 
 // The in-node switch (general.backend = "xgmi", xgmi_switch.h): W worker

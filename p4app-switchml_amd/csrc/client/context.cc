@@ -163,6 +163,11 @@ bool Context::GetJobSlice(WorkerTid tid, JobSlice& job_slice) {
     return scheduler_->GetJobSlice(tid, job_slice);
 }
 
+bool Context::GetJobs(size_t max_jobs, std::vector<std::shared_ptr<Job>>& jobs) {
+    if (context_state_ != RUNNING) return false;
+    return scheduler_->GetJobs(max_jobs, jobs);
+}
+
 void Context::NotifyJobSliceCompletion(WorkerTid tid, const JobSlice& job_slice, bool ok) {
     if (!ok) job_slice.job->MarkFailed();
     if (!scheduler_->NotifyJobSliceCompletion(tid, job_slice)) return;

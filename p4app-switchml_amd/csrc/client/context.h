@@ -69,6 +69,8 @@ class Context {
 
     // Worker-thread side (context.cc:174-197).
     bool GetJobSlice(WorkerTid worker_thread_id, JobSlice& job_slice);
+    // Batched dispatch (FifoScheduler::GetJobs): up to max_jobs whole jobs.
+    bool GetJobs(size_t max_jobs, std::vector<std::shared_ptr<Job>>& jobs);
     // A job after the one with sched_seq `seq` is queued, so GetJobSlice will
     // hand this worker thread its slice without blocking on an empty queue.
     bool HasJobAfter(uint64_t seq) const { return scheduler_ && scheduler_->EnqueuedCount() > seq; }

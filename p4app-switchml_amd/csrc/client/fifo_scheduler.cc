@@ -112,6 +112,31 @@ bool FifoScheduler::GetJobSlice(WorkerTid tid, JobSlice& job_slice) {
     return true;
 }
 
+bool FifoScheduler::GetJobs(size_t max_jobs, std::vector<std::shared_ptr<Job>>& jobs) {
+    std::unique_lock<std::mutex> lock(access_mutex_);
+    if (!stopped_ && queue_.empty() && SpinMicros() > 0) {
+        lock.unlock();
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(SpinMicros());
+        while (!stopped_flag_.load(std::memory_order_acquire) && queue_size_.load(std::memory_order_acquire) == 0 &&
+               std::chrono::steady_clock::now() < until)
+            std::this_thread::yield();
+        lock.lock();
+    }
+    job_submitted_event_.wait(lock, [this] { return stopped_ || !queue_.empty(); });
+    if (stopped_) return false;
+    const int T = config_.general_.num_worker_threads;
+    while (!queue_.empty() && jobs.size() < max_jobs) {
+        std::shared_ptr<Job> job = queue_.front();
+        queue_.pop();
+        dispatched_job_slices_.at(job->id_) = T;
+        undispatched_job_slices_.erase(job->id_);
+        job->SetJobStatus(RUNNING);
+        jobs.push_back(std::move(job));
+    }
+    queue_size_.store(queue_.size(), std::memory_order_release);
+    return true;
+}
+
 bool FifoScheduler::NotifyJobSliceCompletion(WorkerTid, const JobSlice& job_slice) {
     std::unique_lock<std::mutex> lock(access_mutex_);
     const JobId id = job_slice.job->id_;

@@ -11,6 +11,7 @@
 #include <atomic>
 #include <mutex>
 #include <queue>
+#include <vector>
 
 #include "config.h"
 #include "job.h"
@@ -50,6 +51,12 @@ class FifoScheduler {
     // Blocks (after a barrier with the other worker threads) until a job is
     // queued or the scheduler stops; false when stopped.
     bool GetJobSlice(WorkerTid worker_thread_id, JobSlice& job_slice);
+    // Batched dispatch (one worker thread runs every slice): blocks until a
+    // job is queued, then hands out up to max_jobs queued jobs whole (all
+    // num_worker_threads slices of each dispatched at once; the caller cuts
+    // them with FifoSliceGeometry and reports every slice's completion).
+    // No barrier.  False when stopped.
+    bool GetJobs(size_t max_jobs, std::vector<std::shared_ptr<Job>>& jobs);
     // True when this completed the job's last RUNNING slice: all T slices,
     // or after Stop() every slice that had been handed out.  Only then may
     // the caller publish the job's final status (its buffers are released).

@@ -234,8 +234,183 @@ LoopbackBackend::~LoopbackBackend() { CleanupWorker(); }
 
 void LoopbackBackend::SetupWorker() {
     if (config_.general_.backend == "xgmi" && !xgmi_) xgmi_.reset(new XgmiSwitch(config_, context_.device()));
+    if (BatchEligible()) {
+        threads_.emplace_back(&LoopbackBackend::BatchMain, this);
+        return;
+    }
     for (int i = 0; i < config_.general_.num_worker_threads; i++)
         threads_.emplace_back(&LoopbackBackend::WorkerMain, this, (WorkerTid)i);
+}
+
+bool LoopbackBackend::BatchEligible() const {
+    const GeneralConfig& g = config_.general_;
+    return config_.backend_.hip.batch_jobs > 0 && config_.backend_.hip.mode == "fused" && g.backend == "dummy" &&
+           g.prepostprocessor != "bypass" && config_.backend_.dummy.process_packets &&
+           config_.backend_.dummy.bandwidth <= 0;
+}
+
+// Batched dispatch.  The reference's worker threads each run their FIFO slice
+// of every job (dummy_worker_thread.cc:73-177) because a CPU core is the unit
+// of parallelism; on the GPU one launch already fills the chip, so here ONE
+// thread takes the queued jobs whole and runs every slice of up to
+// batch_jobs of them in one sml_roundtrip_loopback_batch launch — the same
+// slice geometry (so the same bits) with one launch and one event per batch
+// instead of num_worker_threads per job.  Jobs whose buffers overlap an
+// earlier job of the batch start a new launch (stream order keeps them in
+// FIFO order); INT32 and pageable-host jobs run slice by slice through
+// run_slice on the same stream.  Completion of every slice is reported under
+// its own worker thread id, so the scheduler, Stats and failure semantics are
+// those of the threaded path.
+void LoopbackBackend::BatchMain() {
+    const GeneralConfig& g = config_.general_;
+    const int T = g.num_worker_threads;
+    std::shared_ptr<PrePostProcessor> ppp;
+    try {
+        hip_ok(hipSetDevice(context_.device()), "hipSetDevice");
+        ppp = PrePostProcessor::CreateInstance(config_, 0, g.packet_numel * 4, g.max_outstanding_packets / T);
+    } catch (const std::exception& e) {
+        fprintf(stderr, "[switchml] batch worker: %s\n", e.what());
+    }
+    auto* hip_ppp = dynamic_cast<HipExponentQuantizerPPP*>(ppp.get());
+    const uint64_t P = g.packet_numel;
+    const uint64_t bmax = g.max_outstanding_packets / T;
+    const size_t max_jobs = std::max<size_t>(1, std::min<size_t>(config_.backend_.hip.batch_jobs,
+                                                                  SML_MAX_BATCH_SLICES / std::max(1, T)));
+    struct Piece {
+        JobSlice js;
+        WorkerTid tid;
+        uint64_t packets;
+        bool ok;
+    };
+    struct Batch {
+        std::vector<Piece> pieces;
+        hipEvent_t ev = nullptr;
+    };
+    constexpr size_t kMaxInFlight = 4;
+    std::deque<Batch> inflight;
+    std::vector<hipEvent_t> events;
+    auto publish = [&](std::vector<Piece>& pieces, bool ok) {
+        for (Piece& pc : pieces) {
+            const bool good = ok && pc.ok;
+            if (good) context_.GetStats().AddSlice(pc.tid, pc.packets, pc.js.slice.numel * DataTypeSize(pc.js.slice.data_type));
+            context_.NotifyJobSliceCompletion(pc.tid, pc.js, good);
+        }
+    };
+    auto retire = [&]() {
+        Batch& b = inflight.front();
+        bool ok = true;
+        try {
+            event_wait(b.ev);
+        } catch (const std::exception& e) {
+            fprintf(stderr, "[switchml] batch worker: %s\n", e.what());
+            ok = false;
+        }
+        publish(b.pieces, ok);
+        events.push_back(b.ev);
+        inflight.pop_front();
+    };
+    WorkerState ws;
+    std::vector<std::shared_ptr<Job>> jobs;
+    uint64_t last_seq = 0;
+    while (context_.GetContextState() == Context::RUNNING) {
+        while (!inflight.empty() && hipEventQuery(inflight.front().ev) != hipErrorNotReady) retire();
+        if (!inflight.empty() && (inflight.size() >= kMaxInFlight || !context_.HasJobAfter(last_seq))) {
+            retire();  // nothing to overlap with: finish the oldest batch first
+            continue;
+        }
+        jobs.clear();
+        if (!context_.GetJobs(max_jobs, jobs)) continue;
+        last_seq = jobs.back()->sched_seq.load(std::memory_order_relaxed);
+
+        Batch cur;
+        std::vector<sml_slice> segs;
+        std::vector<std::pair<uintptr_t, uintptr_t>> reads, writes;   // kernel address ranges in the batch
+        // Enqueue what `cur` holds (a batch launch if it has segments) and put
+        // it in flight behind an event; a failure fails its slices.
+        auto submit = [&]() {
+            if (cur.pieces.empty()) return;
+            try {
+                if (!hip_ppp) throw SwitchMLFatal("no pre/post-processor");
+                if (!segs.empty())
+                    sml_ok(sml_roundtrip_loopback_batch(segs.data(), (uint32_t)segs.size(), (uint32_t)P,
+                                                        g.num_workers, 0, hip_ppp->stream()),
+                           "sml_roundtrip_loopback_batch");
+                if (events.empty()) {
+                    hipEvent_t ev;
+                    hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+                    events.push_back(ev);
+                }
+                cur.ev = events.back();
+                hip_ok(hipEventRecord(cur.ev, hip_ppp->stream()), "hipEventRecord");
+                events.pop_back();
+                inflight.push_back(std::move(cur));
+            } catch (const std::exception& e) {
+                fprintf(stderr, "[switchml] batch worker: %s\n", e.what());
+                if (hip_ppp) (void)hipStreamSynchronize(hip_ppp->stream());   // nothing may still touch the buffers
+                while (!inflight.empty()) retire();
+                publish(cur.pieces, false);
+            }
+            cur = Batch();
+            segs.clear();
+            reads.clear();
+            writes.clear();
+        };
+        auto overlaps = [](const std::vector<std::pair<uintptr_t, uintptr_t>>& v, uintptr_t a, uintptr_t b) {
+            for (const auto& r : v)
+                if (a < r.second && r.first < b) return true;
+            return false;
+        };
+        for (auto& job : jobs) {
+            const Tensor& t = job->tensor_;
+            const size_t esz = DataTypeSize(t.data_type);
+            const bool work = t.numel > 0 && !g.instant_job_completion && hip_ppp;
+            void* in_d = work ? DeviceAddress(t.in_ptr) : nullptr;
+            void* out_d = work ? DeviceAddress(t.out_ptr) : nullptr;
+            const bool batched = work && t.data_type == FLOAT32 && in_d && out_d;
+            if (batched) {
+                const uintptr_t i0 = (uintptr_t)in_d, i1 = i0 + t.numel * esz;
+                const uintptr_t o0 = (uintptr_t)out_d, o1 = o0 + t.numel * esz;
+                if (overlaps(writes, i0, i1) || overlaps(writes, o0, o1) || overlaps(reads, o0, o1)) submit();
+                reads.emplace_back(i0, i1);
+                writes.emplace_back(o0, o1);
+            } else if (work) {
+                submit();   // keep FIFO order on the stream
+            }
+            for (int tid = 0; tid < T; tid++) {
+                Piece pc{JobSlice(), (WorkerTid)tid, 0, true};
+                pc.js.job = job;
+                pc.js.slice = t;
+                Numel off, n;
+                FifoSliceGeometry(t.numel, T, tid, &off, &n);
+                pc.js.slice.numel = n;
+                pc.js.slice.OffsetPtrs(off);
+                if (!work || n == 0) {
+                    pc.ok = work || t.numel == 0 || g.instant_job_completion;   // no pre/post-processor: failed
+                } else if (tid == config_.backend_.dummy.fail_worker_thread) {
+                    pc.ok = false;   // injected fault: this slice's buffers are not touched
+                } else if (batched) {
+                    const uint64_t B = n / P + (n % P != 0);
+                    pc.packets = B + std::min<uint64_t>(B, bmax);
+                    segs.push_back(sml_slice{static_cast<const float*>(in_d) + off, static_cast<float*>(out_d) + off, n});
+                } else {
+                    try {
+                        pc.packets = run_slice(*ppp, config_, ws, pc.js, nullptr, (WorkerTid)tid);
+                    } catch (const std::exception& e) {
+                        fprintf(stderr, "[switchml] batch worker: job %llu failed: %s\n",
+                                (unsigned long long)job->id_, e.what());
+                        (void)hipStreamSynchronize(hip_ppp->stream());
+                        pc.ok = false;
+                    }
+                }
+                cur.pieces.push_back(std::move(pc));
+            }
+            if (!batched && work) submit();
+        }
+        submit();
+    }
+    // stopping: batches in flight own their buffers until their kernels finish
+    while (!inflight.empty()) retire();
+    for (hipEvent_t ev : events) (void)hipEventDestroy(ev);
 }
 
 void LoopbackBackend::CleanupWorker() {

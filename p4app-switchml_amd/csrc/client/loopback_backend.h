@@ -38,6 +38,10 @@ class LoopbackBackend {
 
   private:
     void WorkerMain(WorkerTid tid);
+    // backend.hip.batch_jobs > 0, mode = fused, loopback switch, no simulated
+    // wire, HIP pre/post-processor: one thread, batched launches (BatchMain).
+    bool BatchEligible() const;
+    void BatchMain();
 
     Context& context_;
     Config& config_;

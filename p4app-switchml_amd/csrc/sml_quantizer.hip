@@ -202,71 +202,121 @@ struct RoundTripArgs {
 };
 
 // Fused dummy-backend round trip: PreprocessSingle -> ProcessPacket (x W) ->
-// PostprocessSingle for every packet of the slice in one HBM pass.
+// PostprocessSingle for every packet of the slice in one HBM pass.  One tile
+// of one slice (blocks restart at the slice start, as in the reference).
+template <int P, bool ALIGNED, bool BE, bool RNE>
+__device__ __forceinline__ void roundtrip_tile(const RoundTripArgs& a, uint64_t t, const float* lut, int lane) {
+    const bool pow2 = (a.W & (a.W - 1)) == 0;
+    const uint32_t log2W = 31 - __builtin_clz(a.W);
+    const uint64_t padded = a.nblocks * P;
+    const uint64_t base = t * kTileElems;
+    const bool full = base + kTileElems <= a.numel;
+    f4 v[kU];
+    if (full) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
+    } else {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            v[u] = load4_guarded(a.in + idx, idx, a.numel);
+        }
+    }
+    int e[kU];
+    tile_exponents<P>(v, e);
+    if (a.exps_out) {
+        constexpr int kPk = kTileElems / P;
+        if (((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= padded)
+            store_tile_exponents<P>(a.exps_out + base / P, lane, e);
+        else
+            store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+        const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+        if (idx >= padded) continue;
+        const float s = lut[(uint8_t)e[u]];
+        uint64_t body = 0;
+        if constexpr (RNE) {
+            const uint64_t blk0 = idx / P * P;
+            const uint64_t n = a.numel - blk0 < (uint64_t)P ? a.numel - blk0 : (uint64_t)P;
+            body = blk0 + (n - n % 16);
+        }
+        const u4 qv = quantize4<RNE>(v[u], s, idx, body);
+        const uint32_t q[4] = {qv.x, qv.y, qv.z, qv.w};
+        if (a.payload) {
+            u4 wq = BE ? mku4(bswap(q[0]), bswap(q[1]), bswap(q[2]), bswap(q[3]))
+                          : mku4(q[0], q[1], q[2], q[3]);
+            store_payload(a.payload + idx / 4, wq);
+        }
+        // DummyBackend::ProcessPacket: int32 wrap multiply by W; then the
+        // dequantize (exact reciprocal multiply for power-of-two W, as K4).
+        f4 o;
+        if (pow2) {
+            const float r = rcp_scale_pow2(log2W, e[u]);
+            o = mkf4((float)(int32_t)(q[0] * a.W) * r, (float)(int32_t)(q[1] * a.W) * r,
+                     (float)(int32_t)(q[2] * a.W) * r, (float)(int32_t)(q[3] * a.W) * r);
+        } else {
+            o = mkf4(dequantize1(q[0] * a.W, s), dequantize1(q[1] * a.W, s), dequantize1(q[2] * a.W, s),
+                     dequantize1(q[3] * a.W, s));
+        }
+        if (full) store4<ALIGNED>(a.out + idx, o);
+        else if (idx < a.numel) store4_guarded(a.out + idx, o, idx, a.numel);
+    }
+}
+
 template <int P, bool ALIGNED, bool BE, bool RNE>
 __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
     __shared__ float lut[256];
     build_lut(lut, a.W);
-    const bool pow2 = (a.W & (a.W - 1)) == 0;
-    const uint32_t log2W = 31 - __builtin_clz(a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t padded = a.nblocks * P;
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
-        const uint64_t base = t * kTileElems;
-        const bool full = base + kTileElems <= a.numel;
-        f4 v[kU];
-        if (full) {
-#pragma unroll
-            for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
-        } else {
-#pragma unroll
-            for (int u = 0; u < kU; u++) {
-                uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-                v[u] = load4_guarded(a.in + idx, idx, a.numel);
-            }
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves)
+        roundtrip_tile<P, ALIGNED, BE, RNE>(a, t, lut, lane);
+}
+
+// The fused round trip over a batch of slices (of one or several jobs) in ONE
+// launch: the slices' tiles are numbered consecutively (tile_end[s] = tiles of
+// slices 0..s), each wave finds its slice by a binary search over that
+// wave-uniform table (kernel arguments, scalar loads) and runs the slice's
+// own block geometry.  Slices start at any 4-byte offset (FIFO slices,
+// pinned host tensors): the unaligned form, which streams at the aligned rate.
+struct RoundTripBatchArgs {
+    const float* in[SML_MAX_BATCH_SLICES];
+    float* out[SML_MAX_BATCH_SLICES];
+    uint64_t numel[SML_MAX_BATCH_SLICES];
+    uint32_t tile_end[SML_MAX_BATCH_SLICES];
+    uint32_t nslices;
+    uint32_t W;
+    uint32_t xcd;
+};
+
+template <int P, bool RNE>
+__global__ __launch_bounds__(kBlockThreads) void k_roundtrip_batch(RoundTripBatchArgs a) {
+    __shared__ float lut[256];
+    build_lut(lut, a.W);
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t nwaves = gridDim.x * kWavesPerBlock;
+    const uint32_t ntiles = a.tile_end[a.nslices - 1];
+    for (uint32_t t = (uint32_t)xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < ntiles; t += nwaves) {
+        uint32_t lo = 0, hi = a.nslices - 1;             // first s with tile_end[s] > t
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (a.tile_end[mid] > t) hi = mid;
+            else lo = mid + 1;
         }
-        int e[kU];
-        tile_exponents<P>(v, e);
-        if (a.exps_out) {
-            constexpr int kPk = kTileElems / P;
-            if (((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= padded)
-                store_tile_exponents<P>(a.exps_out + base / P, lane, e);
-            else
-                store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
-        }
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-            if (idx >= padded) continue;
-            const float s = lut[(uint8_t)e[u]];
-            uint64_t body = 0;
-            if constexpr (RNE) {
-                const uint64_t blk0 = idx / P * P;
-                const uint64_t n = a.numel - blk0 < (uint64_t)P ? a.numel - blk0 : (uint64_t)P;
-                body = blk0 + (n - n % 16);
-            }
-            const u4 qv = quantize4<RNE>(v[u], s, idx, body);
-            const uint32_t q[4] = {qv.x, qv.y, qv.z, qv.w};
-            if (a.payload) {
-                u4 wq = BE ? mku4(bswap(q[0]), bswap(q[1]), bswap(q[2]), bswap(q[3]))
-                              : mku4(q[0], q[1], q[2], q[3]);
-                store_payload(a.payload + idx / 4, wq);
-            }
-            // DummyBackend::ProcessPacket: int32 wrap multiply by W; then the
-            // dequantize (exact reciprocal multiply for power-of-two W, as K4).
-            f4 o;
-            if (pow2) {
-                const float r = rcp_scale_pow2(log2W, e[u]);
-                o = mkf4((float)(int32_t)(q[0] * a.W) * r, (float)(int32_t)(q[1] * a.W) * r,
-                         (float)(int32_t)(q[2] * a.W) * r, (float)(int32_t)(q[3] * a.W) * r);
-            } else {
-                o = mkf4(dequantize1(q[0] * a.W, s), dequantize1(q[1] * a.W, s), dequantize1(q[2] * a.W, s),
-                         dequantize1(q[3] * a.W, s));
-            }
-            if (full) store4<ALIGNED>(a.out + idx, o);
-            else if (idx < a.numel) store4_guarded(a.out + idx, o, idx, a.numel);
-        }
+        const uint32_t t0 = lo ? a.tile_end[lo - 1] : 0u;
+        RoundTripArgs r;
+        r.in = a.in[lo];
+        r.out = a.out[lo];
+        r.numel = a.numel[lo];
+        r.nblocks = r.numel / P + (r.numel % P != 0);
+        r.ntiles = a.tile_end[lo] - t0;
+        r.payload = nullptr;
+        r.exps_out = nullptr;
+        r.W = a.W;
+        r.xcd = a.xcd;
+        roundtrip_tile<P, false, true, RNE>(r, t - t0, lut, lane);
     }
 }
 
@@ -380,6 +430,17 @@ static void launch_rt_p(uint32_t P, dim3 grid, hipStream_t st, const RoundTripAr
         case 256:  k_roundtrip<256, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
         case 512:  k_roundtrip<512, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
         default:   k_roundtrip<1024, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
+}
+
+template <bool RNE>
+static void launch_rtb_p(uint32_t P, dim3 grid, hipStream_t st, const RoundTripBatchArgs& a) {
+    switch (P) {
+        case 64:   k_roundtrip_batch<64, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_roundtrip_batch<128, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_roundtrip_batch<256, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_roundtrip_batch<512, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_roundtrip_batch<1024, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
     }
 }
 
@@ -542,6 +603,35 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
     const bool be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
     if (al) launch_rt_a<true>(be, rne, packet_numel, grid, st, a);
     else launch_rt_a<false>(be, rne, packet_numel, grid, st, a);
+    return launch_check();
+}
+
+sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_slices, uint32_t packet_numel,
+                                          uint16_t num_workers, uint32_t flags, void* stream) {
+    if (!valid_packet(packet_numel)) return SML_ERR_UNSUPPORTED;
+    if (num_workers == 0 || num_slices > SML_MAX_BATCH_SLICES || (num_slices && !slices)) return SML_ERR_INVALID_ARG;
+    RoundTripBatchArgs a;
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    a.W = num_workers;
+    a.nslices = 0;
+    uint64_t tiles = 0;
+    for (uint32_t i = 0; i < num_slices; i++) {
+        const sml_slice& sl = slices[i];
+        if (sl.numel == 0) continue;                      // empty slices touch nothing
+        if (!sl.in || !sl.out || !aligned4(sl.in) || !aligned4(sl.out)) return SML_ERR_INVALID_ARG;
+        tiles += (sml_num_blocks(sl.numel, packet_numel) * packet_numel + kTileElems - 1) / kTileElems;
+        if (tiles > 0xFFFFFFFFull) return SML_ERR_UNSUPPORTED;
+        a.in[a.nslices] = sl.in;
+        a.out[a.nslices] = sl.out;
+        a.numel[a.nslices] = sl.numel;
+        a.tile_end[a.nslices] = (uint32_t)tiles;
+        a.nslices++;
+    }
+    if (a.nslices == 0) return SML_OK;
+    const dim3 grid(grid_for_tiles(tiles));
+    hipStream_t st = (hipStream_t)stream;
+    if (flags & SML_FLAG_ROUND_RNE) launch_rtb_p<true>(packet_numel, grid, st, a);
+    else launch_rtb_p<false>(packet_numel, grid, st, a);
     return launch_check();
 }
 

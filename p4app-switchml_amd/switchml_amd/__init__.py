@@ -100,6 +100,8 @@ def lib():
     L.sml_loopback_aggregate.argtypes = [vp, u64, u16, u32, vp]
     L.sml_roundtrip_loopback.restype = i32
     L.sml_roundtrip_loopback.argtypes = [vp, vp, u64, u32, u16, vp, vp, u32, vp]
+    L.sml_roundtrip_loopback_batch.restype = i32
+    L.sml_roundtrip_loopback_batch.argtypes = [vp, u32, u32, u16, u32, vp]
     L.sml_set_grid_limit.restype = u32
     L.sml_set_grid_limit.argtypes = [u32]
     L.sml_stream_copy.restype = i32
@@ -294,6 +296,31 @@ def roundtrip_loopback(x, packet_numel: int = 256, num_workers: int = 1, out=Non
         _dev(x, torch.float32, "x"), _dev(out, torch.float32, "out"), x.numel(), packet_numel,
         num_workers, p, e, flags, _stream(stream, x)))
     return out
+
+
+class Slice(ctypes.Structure):
+    """sml_slice: one job slice of a batched round trip."""
+    _fields_ = [("in_", ctypes.c_void_p), ("out", ctypes.c_void_p), ("numel", ctypes.c_uint64)]
+
+
+MAX_BATCH_SLICES = 64
+
+
+def roundtrip_loopback_batch(slices, packet_numel: int = 256, num_workers: int = 1, flags: int = 0, stream=None):
+    """The fused round trip over several slices in one launch
+    (sml_roundtrip_loopback_batch): `slices` is a list of (x, out) fp32
+    device (or pinned host) tensors; slice i gets exactly
+    roundtrip_loopback(x_i, out=out_i) — its blocks start at its own first
+    element."""
+    torch = _torch()
+    arr = (Slice * max(1, len(slices)))()
+    for i, (x, o) in enumerate(slices):
+        if x.numel() != o.numel():
+            raise ValueError("slice in/out sizes differ")
+        arr[i] = Slice(_dev(x, torch.float32, "x").value, _dev(o, torch.float32, "out").value, x.numel())
+    st = _stream(stream, slices[0][0]) if slices else None
+    _check("sml_roundtrip_loopback_batch", lib().sml_roundtrip_loopback_batch(
+        arr, len(slices), packet_numel, num_workers, flags, st))
 
 
 MAX_SWITCH_WORKERS = 16

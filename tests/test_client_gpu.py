@@ -29,12 +29,17 @@ def bits_equal(a, b):
     return np.array_equal(np.asarray(a).view(np.uint32), np.asarray(b).view(np.uint32))
 
 
-@pytest.mark.parametrize("mode", ["bulk", "fused", "packet"])
+def _mode(mode):
+    """'fused-threads': mode fused with batched dispatch off (batch_jobs = 0)."""
+    return dict(mode="fused", batch_jobs=0) if mode == "fused-threads" else dict(mode=mode)
+
+
+@pytest.mark.parametrize("mode", ["bulk", "fused", "fused-threads", "packet"])
 @pytest.mark.parametrize("T,W,P", [(1, 1, 256), (4, 2, 256), (3, 3, 64), (2, 8, 1024)])
 def test_allreduce_float_host_tensors(C, mode, T, W, P):
     n = 100_003 if mode != "packet" else 20_011
     C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, max_outstanding_packets=64 * T,
-                          mode=mode, bandwidth=0))
+                          bandwidth=0, **_mode(mode)))
     x = O.splitmix_normal(T * 100 + W, n)
     ref = O.dummy_allreduce(x, P=P, max_outstanding_packets=64 * T, num_worker_threads=T, num_workers=W)
     out = np.empty_like(x)
@@ -72,7 +77,7 @@ def test_packet_mode_ring_placements(C, ring, T, W, P, n):
     C.stop()
 
 
-@pytest.mark.parametrize("mode", ["bulk", "fused", "packet"])
+@pytest.mark.parametrize("mode", ["bulk", "fused", "fused-threads", "packet"])
 def test_allreduce_pinned_host_tensors(C, mode):
     """Pinned (page-locked) host tensors go to the kernels through their
     device mapping — zero-copy over PCIe, no staging copies; in place and
@@ -81,7 +86,7 @@ def test_allreduce_pinned_host_tensors(C, mode):
     T, W, P = 3, 2, 256
     n = 100_003 if mode != "packet" else 20_011
     C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, max_outstanding_packets=64 * T,
-                          mode=mode, bandwidth=0))
+                          bandwidth=0, **_mode(mode)))
     x = O.splitmix_normal(17, n)
     ref = O.dummy_allreduce(x, P=P, max_outstanding_packets=64 * T, num_worker_threads=T, num_workers=W)
     hx = torch.from_numpy(x.copy()).pin_memory()
@@ -94,11 +99,11 @@ def test_allreduce_pinned_host_tensors(C, mode):
     C.stop()
 
 
-@pytest.mark.parametrize("mode", ["bulk", "fused"])
+@pytest.mark.parametrize("mode", ["bulk", "fused", "fused-threads"])
 def test_allreduce_device_tensors(C, mode):
     import torch
     T, W, P, n = 4, 2, 256, 1_000_003
-    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, mode=mode, bandwidth=0))
+    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, bandwidth=0, **_mode(mode)))
     x = O.splitmix_normal(5, n)
     xd = torch.from_numpy(x).cuda()
     outd = torch.empty_like(xd)
