@@ -336,6 +336,8 @@ def main():
     if world == 1 and not args.no_side:
         side["cold_hbm"] = cold_measure(sw, torch, args.numel, P, stream)
         side["configs3_1gpu"] = job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev)
+    if world > 1 and not args.no_side:
+        side["weak_256MiB_per_gpu"] = weak_measure(sw, torch, dist, args.numel, P, stream, dev, world)
     if world > 1 and args.switch_numel:
         try:
             fields = exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev)
@@ -493,6 +495,38 @@ def job_measure(sw, torch, job_numel, P, stream, dev, reps=50):
     alg = 8 * job_numel + B
     return {"job_numel": job_numel, "kernel_ms": round(t * 1e3, 4), "value_GBps": round(alg / t / 1e9, 1),
             "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}
+
+
+def weak_measure(sw, torch, dist, N, P, stream, dev, world, reps=200):
+    """Weak scaling beside the strong-scaling headline at N > 1: every rank
+    runs K1 over its own resident N-element bucket (the metric's 256 MiB per
+    GPU, as at N = 1), launches bracketed by a barrier and a device sync;
+    aggregate = world x (8N + B) / max-over-ranks time per step."""
+    B = sw.num_blocks(N, P)
+    g = torch.Generator(device=dev)
+    g.manual_seed(4343 + dist.get_rank())
+    x = torch.randn(N, device=dev, generator=g)
+    pl = torch.empty(B * P, dtype=torch.int32, device=dev)
+    ex = torch.empty(B, dtype=torch.int8, device=dev)
+    fn = lambda: sw.quantize_pack(x, P, 1, payload=pl, exps_out=ex, stream=stream)  # noqa: E731
+    settle(fn, 30.0)
+    for _ in range(20):
+        fn()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = float(t[0])
+    alg = 8 * N + B
+    return {"numel_per_gpu": N, "ms_per_step": round(t * 1e3, 5), "value_GBps": round(world * alg / t / 1e9, 1),
+            "per_gpu_GBps": round(alg / t / 1e9, 1), "frac_per_gpu": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
+            "note": "every GPU quantizes its own resident 256 MiB bucket (weak scaling); the headline "
+                    "shards one 1 GiB job (strong scaling, configs[3])"}
 
 
 def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):

@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/r02ad
+mkdir -p $OUT
+SML_BENCH_REHEARSE=1 timeout -k 10 400 python bench.py --gpus 2 --switch-numel 4194304 --steps 20 --warmup 20 > $OUT/bench2.json 2> $OUT/bench2.err
