@@ -628,6 +628,9 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
         a.nslices++;
     }
     if (a.nslices == 0) return SML_OK;
+    if (a.nslices == 1)   // one slice: the single-slice kernel (aligned form when the slice allows it)
+        return sml_roundtrip_loopback(a.in[0], a.out[0], a.numel[0], packet_numel, num_workers, nullptr, nullptr,
+                                      flags & SML_FLAG_ROUND_RNE, stream);
     const dim3 grid(grid_for_tiles(tiles));
     hipStream_t st = (hipStream_t)stream;
     if (flags & SML_FLAG_ROUND_RNE) launch_rtb_p<true>(packet_numel, grid, st, a);

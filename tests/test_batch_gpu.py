@@ -152,3 +152,45 @@ def test_client_batch_mode_fault_and_stop(C):
     jobs = [C.allreduce_async(big) for _ in range(40)]
     C.stop()
     assert all(j.status() in (C.JOB_FINISHED, C.JOB_FAILED) for j in jobs)
+
+
+def test_batch_kernel_random_slice_tables(cuda):
+    """Hypothesis (derandomized): random batches — 1-8 jobs of 0-40 000
+    elements at random element offsets of one buffer (any 4-byte
+    alignment), T = 1-8 FIFO slices each, P, W, RNE — one batched launch ==
+    one sml_roundtrip_loopback per slice, bit for bit."""
+    pytest.importorskip("hypothesis")
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+    import torch
+    import switchml_amd as sw
+    dev = torch.device("cuda:0")
+    pool = torch.from_numpy(O.splitmix_normal(99, 400_000)).to(dev)
+
+    @settings(max_examples=60, deadline=None, derandomize=True, suppress_health_check=list(HealthCheck))
+    @given(jobs=st.lists(st.tuples(st.integers(0, 40_000), st.integers(1, 8)), min_size=1, max_size=8),
+           P=st.sampled_from([64, 128, 256, 512, 1024]), W=st.sampled_from([1, 2, 3, 8, 255]),
+           rne=st.booleans(), seed=st.integers(0, 2 ** 31))
+    def check(jobs, P, W, rne, seed):
+        rng = np.random.default_rng(seed)
+        flags = sw.FLAG_ROUND_RNE if rne else 0
+        out = torch.full_like(pool, float("nan"))
+        ref = torch.full_like(pool, float("nan"))
+        batch, pos = [], 0
+        for n, T in jobs:
+            pos += int(rng.integers(0, 9))              # gaps: any element offset
+            if pos + n > pool.numel():
+                break
+            for off, m in fifo_slices(n, T):
+                if len(batch) == sw.MAX_BATCH_SLICES:
+                    break
+                a = pos + off
+                batch.append((pool[a:a + m], out[a:a + m]))
+                if m:
+                    sw.roundtrip_loopback(pool[a:a + m], P, W, out=ref[a:a + m], flags=flags)
+            pos += n
+        sw.roundtrip_loopback_batch(batch, P, W, flags=flags)
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+
+    check()
