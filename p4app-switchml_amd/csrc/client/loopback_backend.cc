@@ -206,6 +206,22 @@ void event_wait(hipEvent_t ev) {
     hip_ok(hipEventSynchronize(ev), "hipEventSynchronize");
 }
 
+// The oldest in-flight slice's event, while no later job is queued yet: poll
+// for either its completion or a new job (a framework posts its buckets one
+// call at a time — blocking on the event would serialize the next job behind
+// this one's kernels), for SpinMicros(); then block on the event.  True: the
+// event completed (or failed: the caller's retire reports it); false: a job
+// arrived first, go and overlap it.
+template <class HasJob>
+bool event_or_job(hipEvent_t ev, HasJob has_job) {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(SpinMicros());
+    do {
+        if (hipEventQuery(ev) != hipErrorNotReady) return true;
+        if (has_job()) return false;
+    } while (std::chrono::steady_clock::now() < until);
+    return true;
+}
+
 }  // namespace
 
 void* DeviceAddress(void* p) {
@@ -315,7 +331,12 @@ void LoopbackBackend::BatchMain() {
     while (context_.GetContextState() == Context::RUNNING) {
         while (!inflight.empty() && hipEventQuery(inflight.front().ev) != hipErrorNotReady) retire();
         if (!inflight.empty() && (inflight.size() >= kMaxInFlight || !context_.HasJobAfter(last_seq))) {
-            retire();  // nothing to overlap with: finish the oldest batch first
+            // nothing to overlap with: finish the oldest batch first.  (Unlike the
+            // threaded path this does not poll for a new job meanwhile: jobs that
+            // arrive while the batch runs join the next launch — for zero-copy
+            // host buckets larger launches move more bytes per second over PCIe;
+            // measured: configs[4] pinned 2.95 ms this way, 3.23 ms polling.)
+            retire();
             continue;
         }
         jobs.clear();
@@ -474,7 +495,10 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
     while (context_.GetContextState() == Context::RUNNING) {
         while (!inflight.empty() && hipEventQuery(inflight.front().ev) != hipErrorNotReady) retire(true);
         if (!inflight.empty() && (inflight.size() >= kMaxInFlight || !context_.HasJobAfter(last_seq))) {
-            retire(true);  // nothing to overlap with: finish the oldest slice first
+            // nothing to overlap with (yet): finish the oldest slice, unless a job arrives first
+            if (inflight.size() >= kMaxInFlight ||
+                event_or_job(inflight.front().ev, [&] { return context_.HasJobAfter(last_seq); }))
+                retire(true);
             continue;
         }
         if (!context_.GetJobSlice(tid, js)) continue;
