@@ -40,6 +40,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -68,6 +69,9 @@ def parse(argv=None):
                          "0 = --numel per GPU (weak scaling) at any N")
     ap.add_argument("--switch-numel", type=int, default=CFG3_JOB_NUMEL,
                     help="N > 1: fp32 elements per worker for the switchsim / p2p_switch fields (0 = skip them)")
+    ap.add_argument("--exchange-timeout", type=float, default=300.0,
+                    help="N > 1: seconds the switch / plugin phase may take before the run reports what it has "
+                         "measured, with a failure, and exits 1 (a hang would otherwise print nothing)")
     ap.add_argument("--no-plugin", action="store_true",
                     help="N > 1: skip the configs4_plugin field (ResNet-50 buckets through the CollNet table per rank)")
     ap.add_argument("--buckets", type=int, default=1,
@@ -332,37 +336,12 @@ def main():
     del xs, pls, exs, x, payload, exps
 
     failures = [] if ok else ["self_check: K1 exponent plane != K2 exponents"]
-    side, fields = {}, {}
-    if world == 1 and not args.no_side:
-        side["cold_hbm"] = cold_measure(sw, torch, args.numel, P, stream)
-        side["configs3_1gpu"] = job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev)
-    if world > 1 and not args.no_side:
-        side["weak_256MiB_per_gpu"] = weak_measure(sw, torch, dist, args.numel, P, stream, dev, world)
-    if world > 1 and args.switch_numel:
-        try:
-            fields = exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev)
-        except Exception as e:  # noqa: BLE001 - recorded, then the run fails
-            fields = {"switchsim": {"error": repr(e)[:400]}}
-        for k in ("switchsim", "p2p_switch", "xgmi_switch"):
-            f = fields.get(k, {})
-            if "error" in f or not f.get("verified", False):
-                failures.append(f"{k}: {f.get('error', 'not verified')}")
-    if world > 1 and not args.no_plugin:
-        # configs[4] on every GPU at once: each rank hands the ResNet-50 buckets
-        # to its own plugin instance (loopback backend: the ranks do not
-        # exchange — replicas, like the reference's dummy backend processes)
-        try:
-            fields["configs4_plugin"] = plugin_measure_ranks(torch, dist, dev, world)
-            if not fields["configs4_plugin"]["placements_agree_all_ranks"]:
-                failures.append("configs4_plugin: device and pinned-host results differ")
-        except Exception as e:  # noqa: BLE001
-            fields["configs4_plugin"] = {"error": repr(e)[:400]}
-            failures.append(f"configs4_plugin: {fields['configs4_plugin']['error']}")
-    extra = {}
-    if args.extra and rank == 0:
-        extra.update(extra_measurements(sw, torch, torch.randn(args.numel, device=dev, generator=gen), P, stream))
+    side, fields, extra = {}, {}, {}
 
-    if rank == 0:
+    def emit():
+        """Rank 0's one JSON line, from whatever has been measured so far."""
+        if rank != 0:
+            return
         ms_per_step = elapsed * 1e3 / args.steps
         value = total_alg / (elapsed / args.steps) / 1e9
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
@@ -421,11 +400,59 @@ def main():
             line["side"] = side
         if extra:
             line["extra"] = extra
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(N, P, args.cpu_seconds)
+        if "cpu_baseline" in side_cpu:
+            line["cpu_baseline"] = side_cpu["cpu_baseline"]
         if failures:
             line["failures"] = failures
         print(json.dumps(line), flush=True)
+
+    side_cpu = {}
+    if world == 1 and not args.no_side:
+        side["cold_hbm"] = cold_measure(sw, torch, args.numel, P, stream)
+        side["configs3_1gpu"] = job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev)
+    if world > 1 and not args.no_side:
+        side["weak_256MiB_per_gpu"] = weak_measure(sw, torch, dist, args.numel, P, stream, dev, world)
+    watchdog = None
+    if world > 1:
+        # The multi-GPU exchange phase (switch paths, plugin over the in-node
+        # switch) is where a hang could happen; past the deadline the run
+        # reports what it has, with the failure, and every rank exits 1.
+        def on_timeout():
+            failures.append(f"timeout: the switch / plugin phase exceeded {args.exchange_timeout:g} s")
+            try:
+                emit()
+            finally:
+                os._exit(1)
+        watchdog = threading.Timer(args.exchange_timeout, on_timeout)
+        watchdog.daemon = True
+        watchdog.start()
+    if world > 1 and args.switch_numel:
+        try:
+            fields.update(exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev))
+        except Exception as e:  # noqa: BLE001 - recorded, then the run fails
+            fields["switchsim"] = {"error": repr(e)[:400]}
+        for k in ("switchsim", "p2p_switch", "xgmi_switch"):
+            f = fields.get(k, {})
+            if "error" in f or not f.get("verified", False):
+                failures.append(f"{k}: {f.get('error', 'not verified')}")
+    if world > 1 and not args.no_plugin:
+        # configs[4] on every GPU at once: each rank hands the ResNet-50 buckets
+        # to its own plugin instance, on an N-rank communicator whose backend
+        # is the in-node switch (a real cross-rank SwitchML all-reduce)
+        try:
+            fields["configs4_plugin"] = plugin_measure_ranks(torch, dist, dev, world)
+            if not fields["configs4_plugin"]["placements_agree_all_ranks"]:
+                failures.append("configs4_plugin: device and pinned-host results differ")
+        except Exception as e:  # noqa: BLE001
+            fields["configs4_plugin"] = {"error": repr(e)[:400]}
+            failures.append(f"configs4_plugin: {fields['configs4_plugin']['error']}")
+    if watchdog is not None:
+        watchdog.cancel()
+    if args.extra and rank == 0:
+        extra.update(extra_measurements(sw, torch, torch.randn(args.numel, device=dev, generator=gen), P, stream))
+    if world == 1 and not args.no_cpu_baseline:
+        side_cpu["cpu_baseline"] = cpu_baseline(N, P, args.cpu_seconds)
+    emit()
     if world > 1:
         dist.destroy_process_group()
     if failures:
