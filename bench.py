@@ -412,6 +412,12 @@ def main():
         side["configs3_1gpu"] = job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev)
     if world > 1 and not args.no_side:
         side["weak_256MiB_per_gpu"] = weak_measure(sw, torch, dist, args.numel, P, stream, dev, world)
+        if rank == 0:
+            # what the peer-to-peer paths rely on: every pair of the node's GPUs can map each other
+            side["topology"] = {
+                "devices": ndev, "name": torch.cuda.get_device_name(dev),
+                "peer_access": [[i == j or torch.cuda.can_device_access_peer(i, j) for j in range(ndev)]
+                                for i in range(ndev)]}
     watchdog = None
     if world > 1:
         # The multi-GPU exchange phase (switch paths, plugin over the in-node
