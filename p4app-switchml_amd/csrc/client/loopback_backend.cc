@@ -343,38 +343,32 @@ void LoopbackBackend::BatchMain() {
         if (!context_.GetJobs(max_jobs, jobs)) continue;
         last_seq = jobs.back()->sched_seq.load(std::memory_order_relaxed);
 
+        // Every job taken here shares ONE completion event, recorded after
+        // the last launch: jobs that must be split into several launches (a
+        // buffer shared with an earlier job of the batch: stream order keeps
+        // FIFO order) do not pay an event between kernels each.
         Batch cur;
         std::vector<sml_slice> segs;
-        std::vector<std::pair<uintptr_t, uintptr_t>> reads, writes;   // kernel address ranges in the batch
-        // Enqueue what `cur` holds (a batch launch if it has segments) and put
-        // it in flight behind an event; a failure fails its slices.
-        auto submit = [&]() {
-            if (cur.pieces.empty()) return;
-            try {
-                if (!hip_ppp) throw SwitchMLFatal("no pre/post-processor");
-                if (!segs.empty())
+        size_t seg_first = 0;                                   // first piece of the pending launch
+        std::vector<std::pair<uintptr_t, uintptr_t>> reads, writes;   // kernel address ranges of the pending launch
+        // Launch the pending slices (one sml_roundtrip_loopback_batch); a
+        // failure fails exactly those slices.
+        auto launch = [&]() {
+            if (!segs.empty()) {
+                try {
                     sml_ok(sml_roundtrip_loopback_batch(segs.data(), (uint32_t)segs.size(), (uint32_t)P,
                                                         g.num_workers, 0, hip_ppp->stream()),
                            "sml_roundtrip_loopback_batch");
-                if (events.empty()) {
-                    hipEvent_t ev;
-                    hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-                    events.push_back(ev);
+                } catch (const std::exception& e) {
+                    fprintf(stderr, "[switchml] batch worker: %s\n", e.what());
+                    (void)hipStreamSynchronize(hip_ppp->stream());
+                    for (size_t i = seg_first; i < cur.pieces.size(); i++) cur.pieces[i].ok = false;
                 }
-                cur.ev = events.back();
-                hip_ok(hipEventRecord(cur.ev, hip_ppp->stream()), "hipEventRecord");
-                events.pop_back();
-                inflight.push_back(std::move(cur));
-            } catch (const std::exception& e) {
-                fprintf(stderr, "[switchml] batch worker: %s\n", e.what());
-                if (hip_ppp) (void)hipStreamSynchronize(hip_ppp->stream());   // nothing may still touch the buffers
-                while (!inflight.empty()) retire();
-                publish(cur.pieces, false);
             }
-            cur = Batch();
             segs.clear();
             reads.clear();
             writes.clear();
+            seg_first = cur.pieces.size();
         };
         auto overlaps = [](const std::vector<std::pair<uintptr_t, uintptr_t>>& v, uintptr_t a, uintptr_t b) {
             for (const auto& r : v)
@@ -391,11 +385,11 @@ void LoopbackBackend::BatchMain() {
             if (batched) {
                 const uintptr_t i0 = (uintptr_t)in_d, i1 = i0 + t.numel * esz;
                 const uintptr_t o0 = (uintptr_t)out_d, o1 = o0 + t.numel * esz;
-                if (overlaps(writes, i0, i1) || overlaps(writes, o0, o1) || overlaps(reads, o0, o1)) submit();
+                if (overlaps(writes, i0, i1) || overlaps(writes, o0, o1) || overlaps(reads, o0, o1)) launch();
                 reads.emplace_back(i0, i1);
                 writes.emplace_back(o0, o1);
             } else if (work) {
-                submit();   // keep FIFO order on the stream
+                launch();   // keep FIFO order on the stream
             }
             for (int tid = 0; tid < T; tid++) {
                 Piece pc{JobSlice(), (WorkerTid)tid, 0, true};
@@ -425,9 +419,27 @@ void LoopbackBackend::BatchMain() {
                 }
                 cur.pieces.push_back(std::move(pc));
             }
-            if (!batched && work) submit();
+            if (!batched) seg_first = cur.pieces.size();   // its slices are not part of a pending launch
         }
-        submit();
+        if (hip_ppp) launch();
+        // one event for everything taken in this round
+        try {
+            if (!hip_ppp) throw SwitchMLFatal("no pre/post-processor");
+            if (events.empty()) {
+                hipEvent_t ev;
+                hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+                events.push_back(ev);
+            }
+            cur.ev = events.back();
+            hip_ok(hipEventRecord(cur.ev, hip_ppp->stream()), "hipEventRecord");
+            events.pop_back();
+            inflight.push_back(std::move(cur));
+        } catch (const std::exception& e) {
+            fprintf(stderr, "[switchml] batch worker: %s\n", e.what());
+            if (hip_ppp) (void)hipStreamSynchronize(hip_ppp->stream());   // nothing may still touch the buffers
+            while (!inflight.empty()) retire();
+            publish(cur.pieces, false);
+        }
     }
     // stopping: batches in flight own their buffers until their kernels finish
     while (!inflight.empty()) retire();
