@@ -47,7 +47,20 @@ def test_planes_and_dequantize_past_4GiB(cuda):
         assert np.array_equal(payload[lo:lo + P].cpu().numpy().view(np.uint32), qb), k
         want = O.dequantize(qb, eb, hi - lo, P, W)
         assert np.array_equal(out[lo:hi].cpu().numpy().view(np.uint32), want.view(np.uint32)), k
-    del payload, exps, out
+    # K3 with global exponents (the switch's max of one worker = its own) and
+    # K6 over two planes of the worker: the same bytes past 4 GiB
+    p3, _ = sw.quantize_pack(x, P, W, global_exps=exps)
+    assert torch.equal(p3, payload)
+    del p3, out
+    s_out = sw.switch_aggregate([payload, payload], [exps, exps], N, P, out=torch.empty_like(x))
+    torch.cuda.synchronize()
+    for k in _sample(B, np.random.default_rng(3))[::4]:
+        lo, hi = k * P, min((k + 1) * P, N)
+        xb = x[lo:hi].cpu().numpy()
+        qb, eb = O.quantize(xb, P, W), O.exponents(xb, P)
+        want = O.dequantize(O.switch_payload([qb, qb]), O.switch_exps([eb, eb]), hi - lo, P, 2)
+        assert np.array_equal(s_out[lo:hi].cpu().numpy().view(np.uint32), want.view(np.uint32)), k
+    del payload, exps, s_out
     rt = sw.roundtrip_loopback(x, P, W)                # fused round trip over the same 5 GiB
     torch.cuda.synchronize()
     for k in _sample(B, np.random.default_rng(2)):
