@@ -108,3 +108,31 @@ def test_batch_kernel_past_4GiB(cuda):
         sw.roundtrip_loopback(x[a:a + m], P, W, out=ref[a:a + m])
     torch.cuda.synchronize()
     assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+
+
+@pytest.mark.parametrize("mode", ["fused", "bulk"])
+def test_client_allreduce_past_4GiB(cuda, mode):
+    """Context::AllReduce of a 5 GiB device tensor, T = 4 FIFO slices (batched
+    launch in fused mode, K1 -> K5 -> K4 per slice in bulk mode): equal to
+    one fused round trip per FIFO slice."""
+    import torch
+    import switchml_amd as sw
+    from switchml_amd import client as C
+    dev = torch.device("cuda:0")
+    T, Wc = 4, 2
+    x = _x(torch, dev)
+    out = torch.empty_like(x)
+    C.start(C.make_config(num_workers=Wc, num_worker_threads=T, packet_numel=P, max_outstanding_packets=64 * T,
+                          mode=mode, bandwidth=0))
+    try:
+        C.allreduce(x, out)
+    finally:
+        C.stop()
+    ref = torch.empty_like(x)
+    for t in range(T):
+        q, r = divmod(N, T)
+        m = q + (t < r)
+        off = t * m if t < r else t * m + r
+        sw.roundtrip_loopback(x[off:off + m], P, Wc, out=ref[off:off + m])
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
