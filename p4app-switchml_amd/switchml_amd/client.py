@@ -129,8 +129,23 @@ class Job:
             self._h = None
 
 
+def _ready(*tensors):
+    """The Context takes plain pointers and runs on its own non-blocking HIP
+    streams, so — like the reference's ProcessGroupSML, which synchronizes
+    the producing stream before AllReduceAsync (ProcessGroupSML.cpp:137-151)
+    — device (or pinned host) torch tensors are made ready first: the
+    current stream's pending kernels may still write the input, or read a
+    freed block the caching allocator has handed out again as the output."""
+    for t in tensors:
+        if getattr(t, "is_cuda", False) or (hasattr(t, "is_pinned") and t.is_pinned()):
+            import torch
+            torch.cuda.current_stream(t.device if t.is_cuda else None).synchronize()
+            return
+
+
 def allreduce_async(inp, out=None, numel: int | None = None) -> Job:
     out = inp if out is None else out
+    _ready(inp, out)
     n = inp.numel() if numel is None and hasattr(inp, "numel") and callable(inp.numel) else (
         inp.size if numel is None else numel)
     h = ctypes.c_void_p()

@@ -114,7 +114,10 @@ class CollNetComm:
 
     def allreduce_buckets(self, buckets, dtype: int = NCCL_FLOAT32, mhs=None) -> list[int]:
         """Post every bucket's iallreduce, then poll them (RCCL's proxy keeps
-        several requests in flight); buckets = [(send_ptr, recv_ptr, count)]."""
+        several requests in flight); buckets = [(send_ptr, recv_ptr, count)].
+        As with RCCL's proxy, the buffers must be ready when posted (their
+        producing stream synchronized): the plugin's worker streams do not
+        order after the caller's."""
         reqs = [self.iallreduce(s, r, c, dtype, None if mhs is None else mhs[i])
                 for i, (s, r, c) in enumerate(buckets)]
         return [self.wait(q) for q in reqs]

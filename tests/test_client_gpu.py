@@ -209,3 +209,44 @@ def test_dnn_benchmark_example_model_device(C):
         del jobs
     torch.cuda.synchronize()
     assert bits_equal(xd.cpu().numpy(), ref)
+
+
+def _busy(torch):
+    """Keep torch's current stream busy for a while (so the kernels queued
+    after this still wait when the next host call runs)."""
+    a = torch.randn(2048, 2048, device="cuda")
+    for _ in range(40):
+        a = a @ a
+        a = a / a.abs().max()
+    return a
+
+
+@pytest.mark.parametrize("mode", ["fused", "bulk"])
+def test_allreduce_waits_for_the_producing_stream(C, mode):
+    """Device tensors still being produced on torch's stream when the job is
+    submitted: the Python client makes them ready first (the reference's
+    ProcessGroupSML synchronizes its stream before AllReduceAsync,
+    ProcessGroupSML.cpp:137-151).  Without that the worker stream reads the
+    input before the producing kernel wrote it, and writes an output block
+    the caching allocator has just recycled from a tensor a queued kernel
+    still reads (what made a 5 GiB test fail inside the full suite)."""
+    import torch
+    n, W, T = 1 << 22, 2, 4
+    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=256, max_outstanding_packets=64 * T,
+                          bandwidth=0, mode=mode))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    src = torch.randn(n, device="cuda", generator=g)
+    torch.cuda.synchronize()
+    want_in = src * 3.0
+    _busy(torch)                        # queued ahead of the producer below
+    t = src.clone()
+    x = t * 3.0                         # producer, queued behind the busy work
+    del t                               # its block may come back as `out`
+    out = torch.empty_like(x)
+    C.allreduce(x, out)
+    torch.cuda.synchronize()
+    assert torch.equal(x, want_in)
+    ref = O.dummy_allreduce(want_in.cpu().numpy(), P=256, max_outstanding_packets=64 * T, num_worker_threads=T,
+                            num_workers=W)
+    assert bits_equal(out.cpu().numpy(), ref)

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Build frames-tx (k_quantize_frames) variants of the kernel library into
+tools/ab/ (sources copied and patched there; tools/ab/ is git-ignored):
+  tx_base   the product source
+  tx_bf     payload stores of a full tile in a branch-free loop, the four
+            slices' scales read from the LDS table before any store
+  tx_nohdr  DIAGNOSTIC ONLY (frames wrong): no lane-parallel header stores —
+            what do the headers cost?
+Timed by tools/ab_frames.py on the GPU (AB_NOCHECK=1 when tx_nohdr is in)."""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "p4app-switchml_amd")
+AB = os.path.join(ROOT, "tools", "ab")
+
+PAYLOAD = """        // payloads
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            if (idx >= padded) continue;"""
+PAYLOAD_BF = """        // payloads
+        if (base + kTileElems <= padded) {
+            float s[kU];
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                int e = eloc[u];
+                if constexpr (GLOBAL) e = a.gexp[(base + (uint64_t)(u * kWave + lane) * 4) / P];
+                s[u] = lut[(uint8_t)e];
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+                const uint64_t k = idx / P;
+                const u4 q = quantize4<false>(v[u], s[u], idx, 0);
+                uint32_t* dst = reinterpret_cast<uint32_t*>(a.frames + (k + a.b) * a.stride + 52) + (idx - k * P);
+                *reinterpret_cast<u4a*>(dst) = u4a{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)};
+            }
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
+            if (idx >= padded) continue;"""
+HDR = """            if (lane < 48) {
+                if (j < kPk && pk0 + j < a.nblocks) {"""
+NOHDR = """            if (lane < 48) {
+                if (j < kPk && pk0 + j < a.nblocks && a.W == 0xffffu) {"""
+
+
+def build(name, patches=()):
+    d = os.path.join(AB, name)
+    if os.path.isdir(d):
+        shutil.rmtree(d)
+    shutil.copytree(os.path.join(PKG, "csrc"), os.path.join(d, "csrc"))
+    f = os.path.join(d, "csrc", "sml_frames.hip")
+    s = open(f).read()
+    for old, new in patches:
+        assert s.count(old) == 1, old
+        s = s.replace(old, new)
+    open(f, "w").write(s)
+    objs = []
+    for k in ("sml_quantizer", "sml_frames", "sml_switch"):
+        o = os.path.join(d, k + ".o")
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
+                        "-I" + os.path.join(ROOT, "include"), "-fno-gpu-rdc", "-c", "-o", o,
+                        os.path.join(d, "csrc", k + ".hip")], check=True)
+        objs.append(o)
+    out = os.path.join(AB, name + ".so")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-shared", "--offload-arch=gfx950", "-fno-gpu-rdc", "-o", out] + objs,
+                   check=True)
+    shutil.rmtree(d)
+    print(out)
+
+
+VARIANTS = {"tx_base": (), "tx_bf": ((PAYLOAD, PAYLOAD_BF),), "tx_nohdr": ((HDR, NOHDR),)}
+
+if __name__ == "__main__":
+    os.makedirs(AB, exist_ok=True)
+    for name in sys.argv[1:] or list(VARIANTS):
+        build(name, VARIANTS[name])
