@@ -289,9 +289,12 @@ uint32_t sml_set_grid_limit(uint32_t max_workgroups);
  * 64; 0 = plain blockIdx order).  Process-wide; returns the previous value. */
 uint32_t sml_set_xcd_chunk(uint32_t chunk);
 
-/* Experiment knob: tiles (1024 elements) per wave per loop iteration of the
- * quantize kernel, 1 (default) or 2.  Returns the previous value. */
-uint32_t sml_set_tiles_per_wave(uint32_t tiles);
+/* Tuning knob: slices of 256 elements per wave tile in sml_exponents /
+ * sml_quantize_pack (K1/K2/K3): 4 (the default; 0 or any other value
+ * restores it), 2 or 1 — never below P / 256.  Results are identical for
+ * every size; smaller tiles measured slower.  Returns the
+ * previous value. */
+uint32_t sml_set_quantize_tile_slices(uint32_t slices);
 
 #ifdef __cplusplus
 }

@@ -79,6 +79,7 @@ bool Config::LoadFromString(const std::string& ini) {
         else if (full == "backend.hip.mode") backend_.hip.mode = val;
         else if (full == "backend.hip.packet_ring") backend_.hip.packet_ring = val;
         else if (full == "backend.hip.batch_jobs") backend_.hip.batch_jobs = parse_uint<uint32_t>(full, val, 0xffffffffull);
+        else if (full == "backend.hip.coalesce_us") backend_.hip.coalesce_us = parse_uint<uint32_t>(full, val, 1000000ull);
         else fprintf(stderr, "[switchml] ignoring config key '%s' (not used by this build)\n", full.c_str());
     }
     return true;
@@ -155,6 +156,7 @@ std::string Config::ToString() const {
       << "\nfail_worker_thread = " << backend_.dummy.fail_worker_thread
       << "\n\n[backend.hip]\ndevice = " << backend_.hip.device << "\nmode = " << backend_.hip.mode
       << "\npacket_ring = " << backend_.hip.packet_ring << "\nbatch_jobs = " << backend_.hip.batch_jobs
+      << "\ncoalesce_us = " << backend_.hip.coalesce_us
       << "\n\n[backend.xgmi]\nsession = " << backend_.xgmi.session
       << "\nmax_slice_numel = " << backend_.xgmi.max_slice_numel << "\ntimeout_ms = " << backend_.xgmi.timeout_ms
       << "\n";

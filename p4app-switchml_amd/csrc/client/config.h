@@ -55,6 +55,10 @@ struct HipBackendConfig {
     // one launch instead of num_worker_threads per job.  0: every worker
     // thread launches its own slice (the reference's threading).
     uint32_t batch_jobs = 16;
+    // Batched dispatch with a zero-copy (pinned host) job in the round: jobs
+    // that arrive within coalesce_us of the previous one join the same
+    // launch (PCIe moves more bytes per second in larger launches); 0 = off.
+    uint32_t coalesce_us = 20;
 };
 
 // The in-node switch (general.backend = "xgmi", xgmi_switch.h): W worker

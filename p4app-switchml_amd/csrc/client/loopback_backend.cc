@@ -235,6 +235,15 @@ void* DeviceAddress(void* p) {
     return nullptr;
 }
 
+bool IsHostMapped(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && a.devicePointer;
+}
+
 bool IsDevicePointer(const void* p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -292,6 +301,7 @@ void LoopbackBackend::BatchMain() {
     const uint64_t bmax = g.max_outstanding_packets / T;
     const size_t max_jobs = std::max<size_t>(1, std::min<size_t>(config_.backend_.hip.batch_jobs,
                                                                   SML_MAX_BATCH_SLICES / std::max(1, T)));
+    const uint32_t coalesce_us = config_.backend_.hip.coalesce_us;
     struct Piece {
         JobSlice js;
         WorkerTid tid;
@@ -342,6 +352,26 @@ void LoopbackBackend::BatchMain() {
         jobs.clear();
         if (!context_.GetJobs(max_jobs, jobs)) continue;
         last_seq = jobs.back()->sched_seq.load(std::memory_order_relaxed);
+        // Zero-copy host buckets: a framework posts its buckets one call at a
+        // time, so the first one would otherwise go alone into a small launch;
+        // PCIe moves 31 GB/s each way in a 26 MB launch but 37-42 in 100 MB+
+        // ones (profiles/r02/zero_copy_probes.json).  While the next job
+        // follows within coalesce_us of the last, it joins this launch.
+        if (coalesce_us > 0 && jobs.size() < max_jobs) {
+            bool host = false;
+            for (const auto& j : jobs) host = host || (j->tensor_.numel > 0 && IsHostMapped(j->tensor_.in_ptr));
+            auto last = std::chrono::steady_clock::now();
+            while (host && jobs.size() < max_jobs && context_.GetContextState() == Context::RUNNING) {
+                if (context_.HasJobAfter(last_seq)) {
+                    if (!context_.GetJobs(max_jobs, jobs)) break;
+                    last_seq = jobs.back()->sched_seq.load(std::memory_order_relaxed);
+                    last = std::chrono::steady_clock::now();
+                    continue;
+                }
+                if (std::chrono::steady_clock::now() - last > std::chrono::microseconds(coalesce_us)) break;
+                std::this_thread::yield();
+            }
+        }
 
         // Every job taken here shares ONE completion event, recorded after
         // the last launch: jobs that must be split into several launches (a

@@ -59,6 +59,9 @@ constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlock = kBlockThreads / kWave;
 constexpr int kU = 4;                          // f4 slices per lane per tile
 constexpr int kTileElems = kWave * 4 * kU;     // 1024
+// Elements of a tile of U slices (K1/K2/K3 take U = 1, 2 or 4: DESIGN §4).
+template <int U>
+constexpr int tile_elems() { return kWave * 4 * U; }
 
 // ----------------------------------------------------------------- numerics
 
@@ -213,35 +216,39 @@ __device__ __forceinline__ uint32_t max4(f4 v) {
     return a > c ? a : c;
 }
 
-// Exponents e[u] of the packet each lane's slice u belongs to.
-template <int P>
-__device__ __forceinline__ void tile_exponents(const f4 (&v)[kU], int (&e)[kU]) {
-    uint32_t m[kU];
+// Exponents e[u] of the packet each lane's slice u belongs to (a tile of U
+// slices; a packet of P > 256 elements is P / 256 consecutive slices).
+template <int P, int U>
+__device__ __forceinline__ void tile_exponents(const f4 (&v)[U], int (&e)[U]) {
+    static_assert(P == 64 || P == 128 || P == 256 || P == 512 || P == 1024,
+                  "packet_numel must be 64..1024, power of two");
+    static_assert(P <= 256 * U, "a packet must lie inside one tile");
+    uint32_t m[U];
 #pragma unroll
-    for (int u = 0; u < kU; u++) m[u] = max4(v[u]);
+    for (int u = 0; u < U; u++) m[u] = max4(v[u]);
     if constexpr (P <= 256) {
 #pragma unroll
-        for (int u = 0; u < kU; u++) e[u] = exponent_of(group_max<P>(m[u]));
-    } else if constexpr (P == 512) {
-        uint32_t a = group_max<256>(m[0] > m[1] ? m[0] : m[1]);
-        uint32_t b = group_max<256>(m[2] > m[3] ? m[2] : m[3]);
-        e[0] = e[1] = exponent_of(a);
-        e[2] = e[3] = exponent_of(b);
+        for (int u = 0; u < U; u++) e[u] = exponent_of(group_max<P>(m[u]));
     } else {
-        static_assert(P == 1024, "packet_numel must be 64..1024, power of two");
-        uint32_t a = m[0] > m[1] ? m[0] : m[1];
-        uint32_t b = m[2] > m[3] ? m[2] : m[3];
-        uint32_t t = group_max<256>(a > b ? a : b);
-        e[0] = e[1] = e[2] = e[3] = exponent_of(t);
+        constexpr int G = P / 256;             // slices per packet
+#pragma unroll
+        for (int g = 0; g < U; g += G) {
+            uint32_t t = m[g];
+#pragma unroll
+            for (int i = 1; i < G; i++) t = t > m[g + i] ? t : m[g + i];
+            const int x = exponent_of(group_max<256>(t));
+#pragma unroll
+            for (int i = 0; i < G; i++) e[g + i] = x;
+        }
     }
 }
 
 // The lane that owns packet `pkt` of slice u writes its exponent byte.
-template <int P>
+template <int P, int U>
 __device__ __forceinline__ void store_exponents(int8_t* exps_out, uint64_t tile_base, int lane,
-                                                const int (&e)[kU], uint64_t nblocks) {
+                                                const int (&e)[U], uint64_t nblocks) {
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
+    for (int u = 0; u < U; u++) {
         bool leader;
         if constexpr (P <= 256) leader = (lane % (P / 4)) == 0;
         else leader = lane == 0 && (u % (P / 256)) == 0;
@@ -250,13 +257,13 @@ __device__ __forceinline__ void store_exponents(int8_t* exps_out, uint64_t tile_
     }
 }
 
-// A full tile's kPk = 1024 / P exponent bytes are contiguous in exps_out:
+// A full tile's kPk = 256 U / P exponent bytes are contiguous in exps_out:
 // lane 0 gathers them (v_readlane of each packet's first lane) and writes them
 // with one 1/2/4/8/16-byte store — per-packet byte stores cost ~10 % on the
 // 256 MiB bucket (partial-line writes).  dst must be kPk-byte aligned.
-template <int P>
-__device__ __forceinline__ void store_tile_exponents(int8_t* dst, int lane, const int (&e)[kU]) {
-    constexpr int kPk = kTileElems / P;
+template <int P, int U>
+__device__ __forceinline__ void store_tile_exponents(int8_t* dst, int lane, const int (&e)[U]) {
+    constexpr int kPk = tile_elems<U>() / P;
     constexpr int kLanesPerPk = P / 4 < kWave ? P / 4 : kWave;
     constexpr int kWords = (kPk + 3) / 4;
     uint32_t w[kWords];
@@ -267,7 +274,7 @@ __device__ __forceinline__ void store_tile_exponents(int8_t* dst, int lane, cons
         const int u = (j * P) / 256;
         uint32_t ej = 0;
 #pragma unroll
-        for (int uu = 0; uu < kU; uu++)
+        for (int uu = 0; uu < U; uu++)
             if (uu == u) ej = (uint32_t)__builtin_amdgcn_readlane(e[uu], (j * kLanesPerPk) % kWave);
         w[j / 4] |= (ej & 0xffu) << (8 * (j % 4));
     }
@@ -364,7 +371,7 @@ struct QuantArgs {
     const float* in;
     uint64_t numel;
     uint64_t nblocks;       // B
-    uint64_t ntiles;        // ceil(B*P / 1024)
+    uint64_t ntiles;        // ceil(B*P / tile_elems<U>())
     const int8_t* gexp;     // global exponents (K3) or nullptr (K1)
     u4* payload;          // B*P words, 16-B aligned (nullptr: exponents only)
     int8_t* exps_out;       // nullable
@@ -372,14 +379,14 @@ struct QuantArgs {
     uint32_t xcd;           // xcd_block chunk (0 = plain order)
 };
 
-template <bool ALIGNED>
-__device__ __forceinline__ void load_tile(const QuantArgs& a, uint64_t base, int lane, f4 (&v)[kU]) {
-    if (base + kTileElems <= a.numel) {
+template <bool ALIGNED, int U>
+__device__ __forceinline__ void load_tile(const QuantArgs& a, uint64_t base, int lane, f4 (&v)[U]) {
+    if (base + tile_elems<U>() <= a.numel) {
 #pragma unroll
-        for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
+        for (int u = 0; u < U; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
     } else {
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
+        for (int u = 0; u < U; u++) {
             uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
             v[u] = load4_guarded(a.in + idx, idx, a.numel);
         }

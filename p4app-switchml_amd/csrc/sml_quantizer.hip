@@ -17,14 +17,14 @@ std::atomic<uint32_t> g_xcd_chunk{64};
 // -------------------------------------------------------------- kernels
 
 // K3: the tile's global exponents (one scalar load per slice when aligned).
-template <int P>
-__device__ __forceinline__ void global_tile_exponents(const QuantArgs& a, uint64_t base, int lane, int (&e)[kU]) {
-    if (base + kTileElems <= a.nblocks * P && slice_exps_scalar_ok<P>(a.gexp)) {
+template <int P, int U>
+__device__ __forceinline__ void global_tile_exponents(const QuantArgs& a, uint64_t base, int lane, int (&e)[U]) {
+    if (base + tile_elems<U>() <= a.nblocks * P && slice_exps_scalar_ok<P>(a.gexp)) {
 #pragma unroll
-        for (int u = 0; u < kU; u++) e[u] = (int)(int8_t)slice_exponent_byte<P>(a.gexp, base, u, lane);
+        for (int u = 0; u < U; u++) e[u] = (int)(int8_t)slice_exponent_byte<P>(a.gexp, base, u, lane);
     } else {
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
+        for (int u = 0; u < U; u++) {
             uint64_t pkt = (base + (uint64_t)(u * kWave + lane) * 4) / P;
             e[u] = pkt < a.nblocks ? (int)a.gexp[pkt] : 0;
         }
@@ -50,15 +50,16 @@ __device__ __forceinline__ void quant_slice(const QuantArgs& a, uint64_t idx, f4
 
 // Exponents, quantize and pack of one loaded tile (K3: `e` holds the global
 // exponents already).
-template <int P, bool GLOBAL, bool BE, bool RNE>
-__device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, int lane, const f4 (&v)[kU],
-                                           const float* lut, int (&e)[kU]) {
+template <int P, bool GLOBAL, bool BE, bool RNE, int U>
+__device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, int lane, const f4 (&v)[U],
+                                           const float* lut, int (&e)[U]) {
     const uint64_t padded = a.nblocks * P;
+    constexpr int kElems = tile_elems<U>();
     if constexpr (!GLOBAL) {
         tile_exponents<P>(v, e);
         if (a.exps_out) {
-            constexpr int kPk = kTileElems / P;   // packets per tile
-            if (((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= padded) {
+            constexpr int kPk = kElems / P;       // packets per tile
+            if (((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kElems <= padded) {
                 store_tile_exponents<P>(a.exps_out + base / P, lane, e);
             } else {
                 store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
@@ -73,44 +74,38 @@ __device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, in
     // loaded data is inside this loop) 3 % against K1 (whose exponent reduce
     // consumes all four slices first): profiles/r02/k1_vs_k3_counters.json,
     // ab_k3_waitcnt.json.
-    if (base + kTileElems <= padded) {
+    if (base + kElems <= padded) {
 #pragma unroll
-        for (int u = 0; u < kU; u++) quant_slice<P, BE, RNE>(a, base + (uint64_t)(u * kWave + lane) * 4, v[u], lut, e[u]);
+        for (int u = 0; u < U; u++) quant_slice<P, BE, RNE>(a, base + (uint64_t)(u * kWave + lane) * 4, v[u], lut, e[u]);
         return;
     }
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
+    for (int u = 0; u < U; u++) {
         const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
         if (idx < padded) quant_slice<P, BE, RNE>(a, idx, v[u], lut, e[u]);
     }
 }
 
 // K1 (fused exponent + quantize + pack), K2 (exponents only: payload == nullptr)
-// and K3 (given global exponents: GLOBAL = true).  TPW consecutive tiles per
-// wave per iteration: all their loads are issued before any arithmetic.
-template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE, int TPW>
+// and K3 (given global exponents: GLOBAL = true).  A wave's tile is U slices
+// of 256 elements (one 16-B load per lane per slice, all issued before any
+// arithmetic); U = 4 by default — four loads in flight per lane keep the
+// stream at the copy rate, smaller tiles measured slower.
+template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE, int U>
 __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
     __shared__ float lut[256];
     if (a.payload) build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
-    const uint64_t wave = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
-    for (uint64_t t = wave * TPW; t < a.ntiles; t += nwaves * TPW) {
-        f4 v[TPW][kU];
-        int e[TPW][kU];
-#pragma unroll
-        for (int k = 0; k < TPW; k++)
-            if (k == 0 || t + k < a.ntiles) load_tile<ALIGNED>(a, (t + k) * kTileElems, lane, v[k]);
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
+        const uint64_t base = t * tile_elems<U>();
+        f4 v[U];
+        int e[U];
+        load_tile<ALIGNED>(a, base, lane, v);
         // K3: the exponent dword is read after the data loads are in flight
         // (read first, the compiler waits on it before issuing them: asm)
-        if constexpr (GLOBAL) {
-#pragma unroll
-            for (int k = 0; k < TPW; k++)
-                if (k == 0 || t + k < a.ntiles) global_tile_exponents<P>(a, (t + k) * kTileElems, lane, e[k]);
-        }
-#pragma unroll
-        for (int k = 0; k < TPW; k++)
-            if (k == 0 || t + k < a.ntiles) quant_tile<P, GLOBAL, BE, RNE>(a, (t + k) * kTileElems, lane, v[k], lut, e[k]);
+        if constexpr (GLOBAL) global_tile_exponents<P>(a, base, lane, e);
+        quant_tile<P, GLOBAL, BE, RNE>(a, base, lane, v, lut, e);
     }
 }
 
@@ -369,40 +364,53 @@ __global__ void k_scale_lut(float* lut, uint32_t W) {
 
 // ------------------------------------------------------------ host side
 
-// Dispatch tables: runtime (P, alignment, mode) -> template instance.
-template <bool ALIGNED, bool GLOBAL, bool BE, bool RNE, int TPW>
-static void launch_quant_t(uint32_t P, dim3 grid, hipStream_t st, const QuantArgs& a) {
+// Dispatch tables: runtime (P, tile slices U, alignment, mode) -> template
+// instance.  U is 1, 2 or 4 and at least P / 256 (quantize_common).
+template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
+static void launch_quant_u(uint32_t U, dim3 grid, hipStream_t st, const QuantArgs& a) {
+    if constexpr (P <= 256) {
+        if (U == 1) { k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 1><<<grid, kBlockThreads, 0, st>>>(a); return; }
+    }
+    if constexpr (P <= 512) {
+        if (U == 2) { k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 2><<<grid, kBlockThreads, 0, st>>>(a); return; }
+    }
+    k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 4><<<grid, kBlockThreads, 0, st>>>(a);
+}
+
+template <bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
+static void launch_quant_p(uint32_t P, uint32_t U, dim3 grid, hipStream_t st, const QuantArgs& a) {
     switch (P) {
-        case 64:   k_quantize_pack<64, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_quantize_pack<128, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_quantize_pack<256, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_quantize_pack<512, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_quantize_pack<1024, ALIGNED, GLOBAL, BE, RNE, TPW><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   launch_quant_u<64, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
+        case 128:  launch_quant_u<128, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
+        case 256:  launch_quant_u<256, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
+        case 512:  launch_quant_u<512, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
+        default:   launch_quant_u<1024, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
     }
 }
 
-static std::atomic<uint32_t> g_tiles_per_wave{1};
+// Slices per K1/K2/K3 tile: 4 (1024-element tiles, the default), 2 or 1
+// (never below P / 256).  sml_set_quantize_tile_slices.  Measured
+// (profiles/r02/sweep_tile_slices_p*.json): 1-slice tiles lose 15 % resident
+// and 4 % cold (one 1 KiB load in flight per wave is latency-bound; K2 -35 %),
+// 2-slice tiles are level on cold HBM and lose up to 11 % resident.
+static std::atomic<uint32_t> g_quant_slices{4};
 
-template <bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
-static void launch_quant_p(uint32_t P, dim3 grid, hipStream_t st, const QuantArgs& a) {
-    if (g_tiles_per_wave == 2) {
-        dim3 g2((grid.x + 1) / 2);
-        launch_quant_t<ALIGNED, GLOBAL, BE, RNE, 2>(P, g2, st, a);
-    } else {
-        launch_quant_t<ALIGNED, GLOBAL, BE, RNE, 1>(P, grid, st, a);
-    }
+static uint32_t quant_slices(uint32_t P) {
+    const uint32_t need = P > 256 ? P / 256 : 1;
+    const uint32_t want = g_quant_slices.load(std::memory_order_relaxed);
+    return want > need ? want : need;
 }
 
 template <bool ALIGNED, bool GLOBAL, bool BE>
-static void launch_quant_r(bool rne, uint32_t P, dim3 g, hipStream_t st, const QuantArgs& a) {
-    if (rne) launch_quant_p<ALIGNED, GLOBAL, BE, true>(P, g, st, a);
-    else launch_quant_p<ALIGNED, GLOBAL, BE, false>(P, g, st, a);
+static void launch_quant_r(bool rne, uint32_t P, uint32_t U, dim3 g, hipStream_t st, const QuantArgs& a) {
+    if (rne) launch_quant_p<ALIGNED, GLOBAL, BE, true>(P, U, g, st, a);
+    else launch_quant_p<ALIGNED, GLOBAL, BE, false>(P, U, g, st, a);
 }
 
 template <bool ALIGNED, bool GLOBAL>
-static void launch_quant_b(bool be, bool rne, uint32_t P, dim3 g, hipStream_t st, const QuantArgs& a) {
-    if (be) launch_quant_r<ALIGNED, GLOBAL, true>(rne, P, g, st, a);
-    else launch_quant_r<ALIGNED, GLOBAL, false>(rne, P, g, st, a);
+static void launch_quant_b(bool be, bool rne, uint32_t P, uint32_t U, dim3 g, hipStream_t st, const QuantArgs& a) {
+    if (be) launch_quant_r<ALIGNED, GLOBAL, true>(rne, P, U, g, st, a);
+    else launch_quant_r<ALIGNED, GLOBAL, false>(rne, P, U, g, st, a);
 }
 
 template <bool ALIGNED, bool BE, bool RCP>
@@ -479,8 +487,8 @@ uint32_t sml_set_xcd_chunk(uint32_t chunk) {
     return g_xcd_chunk.exchange(chunk);
 }
 
-uint32_t sml_set_tiles_per_wave(uint32_t tpw) {
-    return g_tiles_per_wave.exchange(tpw == 2 ? 2u : 1u);
+uint32_t sml_set_quantize_tile_slices(uint32_t slices) {
+    return g_quant_slices.exchange(slices == 1 || slices == 2 ? slices : 4u);
 }
 
 uint64_t sml_num_blocks(uint64_t numel, uint32_t packet_numel) {
@@ -513,11 +521,14 @@ static sml_status_t quantize_common(const float* d_in, uint64_t numel, uint32_t 
     if (!d_in || !aligned4(d_in)) return SML_ERR_INVALID_ARG;
     if (d_payload && !aligned16(d_payload)) return SML_ERR_ALIGNMENT;
     QuantArgs a;
-    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    const uint32_t U = quant_slices(P);
+    // XCD runs keep their byte length (C workgroups of 4 U-slice tiles)
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);
     a.in = d_in;
     a.numel = numel;
     a.nblocks = sml_num_blocks(numel, P);
-    a.ntiles = (a.nblocks * P + kTileElems - 1) / kTileElems;
+    const uint64_t te = 256ull * U;
+    a.ntiles = (a.nblocks * P + te - 1) / te;
     a.gexp = d_gexp;
     a.payload = reinterpret_cast<u4*>(d_payload);
     a.exps_out = d_gexp ? nullptr : d_exps_out;
@@ -526,11 +537,11 @@ static sml_status_t quantize_common(const float* d_in, uint64_t numel, uint32_t 
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_in), be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
     if (d_gexp) {
-        if (al) launch_quant_b<true, true>(be, rne, P, grid, st, a);
-        else launch_quant_b<false, true>(be, rne, P, grid, st, a);
+        if (al) launch_quant_b<true, true>(be, rne, P, U, grid, st, a);
+        else launch_quant_b<false, true>(be, rne, P, U, grid, st, a);
     } else {
-        if (al) launch_quant_b<true, false>(be, rne, P, grid, st, a);
-        else launch_quant_b<false, false>(be, rne, P, grid, st, a);
+        if (al) launch_quant_b<true, false>(be, rne, P, U, grid, st, a);
+        else launch_quant_b<false, false>(be, rne, P, U, grid, st, a);
     }
     return launch_check();
 }

@@ -112,8 +112,8 @@ def lib():
     L.sml_frame_bytes.argtypes = [u32]
     L.sml_quantize_pack_frames.restype = i32
     L.sml_quantize_pack_frames.argtypes = [vp, u64, u32, u16, vp, u32, ctypes.POINTER(FrameParams), vp, u64, vp]
-    L.sml_set_tiles_per_wave.restype = u32
-    L.sml_set_tiles_per_wave.argtypes = [u32]
+    L.sml_set_quantize_tile_slices.restype = u32
+    L.sml_set_quantize_tile_slices.argtypes = [u32]
     L.sml_set_xcd_chunk.restype = u32
     L.sml_set_xcd_chunk.argtypes = [u32]
     L.sml_dequantize_frames.restype = i32
@@ -179,8 +179,10 @@ def set_grid_limit(max_workgroups: int) -> int:
     return int(lib().sml_set_grid_limit(max_workgroups))
 
 
-def set_tiles_per_wave(tiles: int) -> int:
-    return int(lib().sml_set_tiles_per_wave(tiles))
+def set_quantize_tile_slices(slices: int) -> int:
+    """Slices of 256 elements per K1/K2/K3 wave tile: 4 (default; 0
+    restores it), 2 or 1, never below P/256; returns the previous setting."""
+    return int(lib().sml_set_quantize_tile_slices(slices))
 
 
 def set_xcd_chunk(chunk: int) -> int:

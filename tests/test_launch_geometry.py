@@ -91,3 +91,38 @@ def test_misaligned_slice_geometry_invariant(sw):
             sw.set_xcd_chunk(chunk)
             payload, _ = sw.quantize_pack(xs, P, W)
             assert np.array_equal(payload.cpu().numpy().view(np.uint32), want), (off, cap, chunk)
+
+
+@pytest.mark.parametrize("P", [64, 128, 256, 512, 1024])
+def test_quantize_tile_slices_invariant(sw, P):
+    """K1 / K2 / K3 with every wave-tile size (sml_set_quantize_tile_slices:
+    4 = default, 1, 2 slices of 256 elements, never below P / 256) under capped grids
+    and XCD orders, aligned and 4-byte-offset slices, RNE and LE flags: the
+    same bytes as the oracle."""
+    import torch
+    W, n = 3, 200_003
+    x_np = O.splitmix_normal(P + 5, n + 1)
+    xd = torch.from_numpy(x_np).cuda()
+    try:
+        for off in (0, 1):
+            xs, xn = xd[off:off + n], x_np[off:off + n]
+            want_q, want_e = O.quantize(xn, P, W), O.exponents(xn, P)
+            want_rne = O.quantize(xn, P, W, rounding=O.RNE_VCL)
+            for sl in (0, 1, 2, 4):
+                sw.set_quantize_tile_slices(sl)
+                for cap, chunk in GEOMETRIES[:3] + GEOMETRIES[6:8]:
+                    sw.set_grid_limit(cap)
+                    sw.set_xcd_chunk(chunk)
+                    payload, exps = sw.quantize_pack(xs, P, W)
+                    e_only = sw.exponents(xs, P)
+                    k3, _ = sw.quantize_pack(xs, P, W, global_exps=exps, flags=sw.FLAG_PAYLOAD_LE)
+                    rne, _ = sw.quantize_pack(xs, P, W, flags=sw.FLAG_ROUND_RNE)
+                    torch.cuda.synchronize()
+                    tag = (off, sl, cap, chunk)
+                    assert np.array_equal(payload.cpu().numpy().view(np.uint32), want_q), tag
+                    assert np.array_equal(exps.cpu().numpy(), want_e), tag
+                    assert np.array_equal(e_only.cpu().numpy(), want_e), tag
+                    assert np.array_equal(k3.cpu().numpy().view(np.uint32), want_q.byteswap()), tag
+                    assert np.array_equal(rne.cpu().numpy().view(np.uint32), want_rne), tag
+    finally:
+        sw.set_quantize_tile_slices(0)

@@ -28,8 +28,8 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=9, reps=20):
         L.sml_quantize_pack.argtypes = [vp, u64, u32, u16, vp, vp, vp, u32, vp]
         L.sml_dequantize.restype = ctypes.c_int
         L.sml_dequantize.argtypes = [vp, vp, u64, u32, u16, vp, u32, vp]
-        L.sml_set_tiles_per_wave.restype = u32
-        L.sml_set_tiles_per_wave.argtypes = [u32]
+        L.sml_set_quantize_tile_slices.restype = u32
+        L.sml_set_quantize_tile_slices.argtypes = [u32]
         libs[p] = L
     L0 = libs[paths[0]]
     assert L0.sml_quantize_pack(x.data_ptr(), N, P, 1, None, payload.data_ptr(), exps.data_ptr(), 0, st.cuda_stream) == 0
@@ -47,7 +47,7 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=9, reps=20):
     def k4(L):
         return L.sml_dequantize(ref.data_ptr(), exps.data_ptr(), N, P, 1, out.data_ptr(), 0, st.cuda_stream)
 
-    tpws = (1, 2) if "--tpw2" in sys.argv else (1,)
+    tpws = (4, 2) if "--slices2" in sys.argv else (4,)   # tile slices per wave
     arms = []
     for p in paths:
         for tpw in tpws:
@@ -56,14 +56,14 @@ def main(paths, N=64 * 1024 * 1024, P=256, rounds=9, reps=20):
         arms.append((f"{p.split('/')[-1]} K4", libs[p], k4, 1))
     eq = {}
     for name, L, fn, tpw in arms:
-        L.sml_set_tiles_per_wave(tpw)
+        L.sml_set_quantize_tile_slices(tpw)
         assert fn(L) == 0
         torch.cuda.synchronize()
         eq[name] = bool(torch.equal(payload, ref)) if fn is not k4 else None
     times = {a[0]: [] for a in arms}
     for _ in range(rounds):
         for name, L, fn, tpw in arms:
-            L.sml_set_tiles_per_wave(tpw)
+            L.sml_set_quantize_tile_slices(tpw)
             for _ in range(5):
                 fn(L)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -180,17 +180,35 @@ int main(int argc, char** argv) {
     [=](hipStream_t s) { unsigned long long g = nvec / (WG * U); k_read<WG, U, LN><<<g, WG, 0, s>>>(in, sink); }, {}})
 #define WRITE(WG, U, SN) vs.push_back({"write wg" #WG " u" #U " stnt" #SN, 16.0, \
     [=](hipStream_t s) { unsigned long long g = nvec / (WG * U); k_write<WG, U, SN><<<g, WG, 0, s>>>(out); }, {}})
-    COPY(256, 4, 1, 0, 64);  // == K1 now
 #define MULTI(IT, C) vs.push_back({"copy multi iter" #IT " xcd" #C, 32.0, \
     [=](hipStream_t s) { k_copy_multi<IT, C><<<nvec / (1024 * IT), 256, 0, s>>>(in, out); }, {}})
-    MULTI(1, 64);
-    MULTI(2, 32);
-    MULTI(4, 16);
-    MULTI(8, 8);
-    MULTI(16, 4);
-    MULTI(2, 64);
-    MULTI(4, 64);
-    READ(256, 4, 1);
+    const char* set = getenv("PROBE_SET");
+    if (set && std::string(set) == "tiles") {
+        // tile size (U f4 per lane) x workgroup size x XCD run length
+        COPY(256, 4, 1, 0, 64);  // == K1 now
+        COPY(256, 4, 1, 0, 32);
+        COPY(128, 4, 1, 0, 128);
+        COPY(256, 2, 1, 0, 64);
+        COPY(256, 2, 1, 0, 128);
+        COPY(128, 2, 1, 0, 128);
+        COPY(128, 2, 1, 0, 256);
+        COPY(64, 2, 1, 0, 256);
+        COPY(64, 2, 1, 0, 512);
+        COPY(64, 4, 1, 0, 256);
+        COPY(256, 1, 1, 0, 256);
+        READ(256, 4, 1);
+        WRITE(256, 4, 0);
+    } else {
+        COPY(256, 4, 1, 0, 64);  // == K1 now
+        MULTI(1, 64);
+        MULTI(2, 32);
+        MULTI(4, 16);
+        MULTI(8, 8);
+        MULTI(16, 4);
+        MULTI(2, 64);
+        MULTI(4, 64);
+        READ(256, 4, 1);
+    }
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));

@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
-"""K1 launch-shape sweep on COLD HBM: the steps cycle 4 distinct 256 MiB
-buckets + planes (2 GiB, past the 256 MiB Infinity Cache), so the shape
-that wins on the resident bucket (round 1's sweeps) is re-checked where the
-stream really comes from HBM.  Knobs: XCD run length, tiles per wave,
-workgroup cap (grid-stride).  Interleaved rounds, medians."""
+"""K1 / K3 / K2 launch-shape sweep, resident and on COLD HBM.  Resident: one
+256 MiB bucket re-read every step (the bench headline).  Cold: the steps
+cycle 4 distinct 256 MiB buckets + planes (2 GiB, past the 256 MiB Infinity
+Cache).  1 GiB: one configs[3]-sized job.  Knobs: slices per wave tile
+(sml_set_quantize_tile_slices: 4 = round-1/2 tiles of 1024 elements, 1 =
+256-element tiles) and XCD run length (sml_set_xcd_chunk, runs of C x 16 KiB
+of input whatever the tile).  Interleaved rounds, medians; every arm's
+planes are checked equal to the first arm's."""
 import json
 import os
 import statistics
@@ -16,7 +19,8 @@ import torch  # noqa: E402
 import switchml_amd as sw  # noqa: E402
 
 
-def main(N=64 << 20, P=256, nbuf=4, rounds=7, reps=40):
+def main(N=64 << 20, nbuf=4, rounds=7, reps=30):
+    P = int(os.environ.get("SWEEP_P", "256"))
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(9)
@@ -24,41 +28,76 @@ def main(N=64 << 20, P=256, nbuf=4, rounds=7, reps=40):
     xs = [torch.randn(N, device=dev, generator=g) for _ in range(nbuf)]
     pls = [torch.empty(B * P, dtype=torch.int32, device=dev) for _ in range(nbuf)]
     exs = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nbuf)]
+    NB = 4 * N
+    xb = torch.randn(NB, device=dev, generator=g)
+    BB = sw.num_blocks(NB, P)
+    pb = torch.empty(BB * P, dtype=torch.int32, device=dev)
+    eb = torch.empty(BB, dtype=torch.int8, device=dev)
     st = torch.cuda.current_stream()
-    arms = [("xcd64 tpw1", 64, 1, 0), ("xcd0 tpw1", 0, 1, 0), ("xcd32 tpw1", 32, 1, 0), ("xcd128 tpw1", 128, 1, 0),
-            ("xcd256 tpw1", 256, 1, 0), ("xcd64 tpw2", 64, 2, 0), ("xcd64 grid8192", 64, 1, 8192),
-            ("xcd64 grid4096", 64, 1, 4096), ("xcd64 grid2048", 64, 1, 2048)]
-    times = {a[0]: [] for a in arms}
+    arms = [("slices4 xcd64", 4, 64), ("slices1 xcd64", 1, 64), ("slices2 xcd64", 2, 64),
+            ("slices1 xcd32", 1, 32), ("slices1 xcd128", 1, 128)]
+    kinds = ("K1 resident", "K1 cold", "K1 1GiB", "K3 cold", "K2 cold")
+    times = {(a[0], k): [] for a in arms for k in kinds}
     i = [0]
 
-    def step():
-        k = i[0]
-        i[0] = (k + 1) % nbuf
+    def k1(nb):
+        k = i[0] % nb
+        i[0] += 1
         sw.quantize_pack(xs[k], P, 1, payload=pls[k], exps_out=exs[k], stream=st)
 
+    def k3(nb):
+        k = i[0] % nb
+        i[0] += 1
+        sw.quantize_pack(xs[k], P, 2, global_exps=exs[k], payload=pls[k], stream=st)
+
+    def k2(nb):
+        k = i[0] % nb
+        i[0] += 1
+        sw.exponents(xs[k], P, out=exs[k], stream=st)
+
+    def big(_):
+        sw.quantize_pack(xb, P, 1, payload=pb, exps_out=eb, stream=st)
+
+    fns = {"K1 resident": (k1, 1), "K1 cold": (k1, nbuf), "K1 1GiB": (big, 1), "K3 cold": (k3, nbuf),
+           "K2 cold": (k2, nbuf)}
+    ref = None
+    for name, sl, xcd in arms:                       # equal planes for every shape
+        sw.set_quantize_tile_slices(sl)
+        sw.set_xcd_chunk(xcd)
+        sw.quantize_pack(xs[0], P, 3, payload=pls[0], exps_out=exs[0], stream=st)
+        torch.cuda.synchronize()
+        cur = (pls[0].clone(), exs[0].clone())
+        if ref is None:
+            ref = cur
+        assert torch.equal(ref[0], cur[0]) and torch.equal(ref[1], cur[1]), name
     for _ in range(50):
-        step()
+        k1(nbuf)
     for _ in range(rounds):
-        for name, xcd, tpw, grid in arms:
+        for name, sl, xcd in arms:
+            sw.set_quantize_tile_slices(sl)
             sw.set_xcd_chunk(xcd)
-            sw.set_tiles_per_wave(tpw)
-            sw.set_grid_limit(grid)
-            for _ in range(8):
-                step()
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(st)
-            for _ in range(reps):
-                step()
-            b.record(st)
-            torch.cuda.synchronize()
-            times[name].append(a.elapsed_time(b) / reps * 1e3)
+            for kind in kinds:
+                fn, nb = fns[kind]
+                r = reps if kind != "K1 1GiB" else max(4, reps // 4)
+                for _ in range(6):
+                    fn(nb)
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(st)
+                for _ in range(r):
+                    fn(nb)
+                b.record(st)
+                torch.cuda.synchronize()
+                times[(name, kind)].append(a.elapsed_time(b) / r * 1e3)
     sw.set_xcd_chunk(64)
-    sw.set_tiles_per_wave(1)
-    sw.set_grid_limit(0)
-    alg = 8 * N + B
-    out = {k: {"median_us": round(statistics.median(v), 2), "GBps": round(alg / statistics.median(v) / 1e3, 1)}
-           for k, v in times.items()}
-    print(json.dumps({"what": "K1, 4 cold 256 MiB buckets cycled, P=256, W=1", "res": out}, indent=1))
+    sw.set_quantize_tile_slices(4)
+    alg = {"K1 resident": 8 * N + B, "K1 cold": 8 * N + B, "K1 1GiB": 8 * NB + BB, "K3 cold": 8 * N + B,
+           "K2 cold": 4 * N + B}
+    out = {}
+    for (name, kind), v in times.items():
+        m = statistics.median(v)
+        out.setdefault(name, {})[kind] = {"median_us": round(m, 2), "GBps": round(alg[kind] / m / 1e3, 1)}
+    print(json.dumps({"what": f"K1/K3/K2 tile slices x XCD run length, P={P}: resident 256 MiB, cold "
+                      "(4 x 256 MiB cycled), one 1 GiB job", "res": out}, indent=1))
 
 
 if __name__ == "__main__":

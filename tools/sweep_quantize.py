@@ -31,7 +31,7 @@ def main():
     st = torch.cuda.current_stream()
     alg = 8 * N + B
     grids = [int(g) for g in os.environ.get("SWEEP_GRIDS", "0,4096,8192").split(",")]
-    tpws = [int(t) for t in os.environ.get("SWEEP_TPW", "1,2").split(",")]
+    tpws = [int(t) for t in os.environ.get("SWEEP_TPW", "4,1").split(",")]
     variants = list(itertools.product(grids, tpws))
     res = {v: [] for v in variants}
     copy, ntcopy = [], []
@@ -49,16 +49,16 @@ def main():
     for _ in range(rounds):
         for g, tpw in variants:
             sw.set_grid_limit(g)
-            sw.set_tiles_per_wave(tpw)
+            sw.set_quantize_tile_slices(tpw)
             res[(g, tpw)].append(t_of(lambda: sw.quantize_pack(x, P, W, payload=payload, exps_out=exps, stream=st)))
         sw.set_grid_limit(0)
-        sw.set_tiles_per_wave(1)
+        sw.set_quantize_tile_slices(4)
         copy.append(t_of(lambda: out.copy_(x)))
         ntcopy.append(t_of(lambda: sw.stream_copy(x, out, stream=st)))
     rows = []
     for (g, tpw), ts in res.items():
         m = statistics.median(ts)
-        rows.append({"grid_limit": g, "tiles_per_wave": tpw, "median_us": round(m * 1e6, 2),
+        rows.append({"grid_limit": g, "tile_slices": tpw, "median_us": round(m * 1e6, 2),
                      "min_us": round(min(ts) * 1e6, 2), "GBps": round(alg / m / 1e9, 1)})
     rows.sort(key=lambda r: r["median_us"])
     cm, nm = statistics.median(copy), statistics.median(ntcopy)

@@ -22,18 +22,18 @@ def main(N=64 * 1024 * 1024, P=256, reps=3, rounds=3):
     st = torch.cuda.current_stream()
     res = {}
     for _ in range(rounds):
-        for g, tpw in itertools.product([0, 1024, 2048, 4096], [1, 2]):
+        for g, tpw in itertools.product([0, 1024, 2048, 4096], [4, 1]):
             sw.set_grid_limit(g)
-            sw.set_tiles_per_wave(tpw)
+            sw.set_quantize_tile_slices(tpw)
             sw.quantize_pack(hx, P, 1, payload=hp, exps_out=he, stream=st)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(reps):
                 sw.quantize_pack(hx, P, 1, payload=hp, exps_out=he, stream=st)
             torch.cuda.synchronize()
-            res.setdefault(f"grid{g}_tpw{tpw}", []).append(4 * N * reps / (time.perf_counter() - t0) / 1e9)
+            res.setdefault(f"grid{g}_slices{tpw}", []).append(4 * N * reps / (time.perf_counter() - t0) / 1e9)
     sw.set_grid_limit(0)
-    sw.set_tiles_per_wave(1)
+    sw.set_quantize_tile_slices(4)
     print(json.dumps({k: round(statistics.median(v), 2) for k, v in res.items()}, indent=1))
 
 
