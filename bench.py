@@ -318,9 +318,13 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
+    # The closing barrier brackets the region but its own latency (a
+    # collective, tens of us at N = 8 against ~0.4 ms of K1 at 20 steps of
+    # 128 MiB) is not a step: each rank stops its clock at its device sync
+    # and the MAX over ranks below is the job's time.
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -551,8 +555,9 @@ def weak_measure(sw, torch, dist, N, P, stream, dev, world, reps=200):
     for _ in range(reps):
         fn()
     torch.cuda.synchronize()
+    el = time.perf_counter() - t0          # the closing barrier is not a step (see main)
     dist.barrier()
-    t = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+    t = torch.tensor([el / reps], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t = float(t[0])
     alg = 8 * N + B

@@ -305,3 +305,21 @@ def test_configs4_resnet50_buckets_through_plugin(cuda):
     assert all(out["device_ok"]) and out["device_send_untouched"]
     assert out["host_sizes"] == [4 * n for n in RESNET50_BUCKETS]
     assert all(out["host_ok"])
+
+
+@pytest.mark.gpu
+def test_configs4_native_proxy_driver(cuda):
+    """bin/collnet_bench: the CollNet table driven from native code in RCCL's
+    proxy call order (dlopen, init, listen/connect, regMr, iallreduce x 4
+    buckets, test until done) on device and pinned host buffers; every test()
+    reports the bucket's byte size and both placements give the same bytes."""
+    import json
+    ini = ("[general]\nnum_workers = 8\nnum_worker_threads = 4\npacket_numel = 256\n"
+           "max_outstanding_packets = 256\n[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = fused\n")
+    env = dict(os.environ, SWITCHML_CONFIG_INI=ini, SWITCHML_COLLNET_LOOPBACK="1")
+    exe = os.path.join(ROOT, "p4app-switchml_amd", "bin", "collnet_bench")
+    r = subprocess.run([exe, "3", PLUGIN], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["placements_agree"] is True
+    assert out["params"] == sum(RESNET50_BUCKETS)
