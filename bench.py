@@ -600,6 +600,38 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
     del ge
 
     res, outs = {}, {}
+    # calibration: RCCL's own fp32 all-reduce of the same buckets on this node
+    # (what the switch paths compete with; same xGMI links)
+    try:
+        y = x.clone()
+        dist.all_reduce(y)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dist.all_reduce(y)
+        torch.cuda.synchronize()
+        tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt[0])
+        res["rccl_fp32_allreduce"] = {"ms_per_allreduce": round(t * 1e3, 3),
+                                      "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
+                                      "frac_of_xgmi_bound": round(bound_s / t, 4)}
+        del y
+    except Exception as e:  # noqa: BLE001 - calibration only
+        res["rccl_fp32_allreduce"] = {"error": repr(e)[:300]}
+
+    def phase_ms(ar, call):
+        """One more call with the instance's phase marks on: per-phase
+        milliseconds, max over ranks (diagnostic; syncs between phases)."""
+        ar.phases = {}
+        call()
+        ph, ar.phases = ar.phases, None
+        keys = list(ph)
+        d = torch.tensor([ph[b] - ph[a] for a, b in zip(keys, keys[1:])], dtype=torch.float64, device=dev)
+        dist.all_reduce(d, op=dist.ReduceOp.MAX)
+        return {k: round(float(v) * 1e3, 3) for k, v in zip(keys[1:], d.tolist())}
+
     for name, cls, pipe in (
             ("switchsim", SwitchSimAllReduce,
              "K2 exps -> all_reduce(int8, MAX) -> K3 LE payload -> all_reduce(int32, SUM) -> K4"),
@@ -621,6 +653,10 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
             tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             t = float(tt[0])
+            try:
+                phases = phase_ms(ar, lambda: ar(x, out))
+            except Exception as e:  # noqa: BLE001 - diagnostic only
+                phases = {"error": repr(e)[:200]}
             if hasattr(ar, "close"):
                 ar.close()
             del ar
@@ -634,7 +670,7 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
                          "frac_of_xgmi_bound": round(bound_s / t, 4),
                          "within_quantization_bound": bool(ok_t.item()),
                          "max_abs_err_vs_fp32_allreduce": float(err.max().item()),
-                         "pipeline": pipe}
+                         "pipeline": pipe, "phases_ms": phases}
             del err
         except Exception as e:  # noqa: BLE001
             res[name] = {"error": repr(e)[:400], "pipeline": pipe}

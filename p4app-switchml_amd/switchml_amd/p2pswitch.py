@@ -25,6 +25,7 @@ all-gather moves equal shards.
 from __future__ import annotations
 
 import ctypes
+import time
 
 import torch
 import torch.distributed as dist
@@ -108,6 +109,7 @@ class PeerSwitchAllReduce:
         mine = _handle_of(self.payload)
         allh = [None] * self.W
         dist.all_gather_object(allh, mine, group=group)
+        self.phases = None      # diagnostics: see SwitchSimAllReduce.phases
         self.peers = {}
         for w, (h, off) in enumerate(allh):
             if w != self.rank:
@@ -123,6 +125,11 @@ class PeerSwitchAllReduce:
         torch.cuda.current_stream(self.dev).synchronize()
         dist.barrier(group=self.group)
 
+    def _mark(self, name: str):
+        if self.phases is not None:
+            torch.cuda.current_stream(self.dev).synchronize()
+            self.phases[name] = time.perf_counter()
+
     def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """All-reduce (SUM) of a FLOAT32 bucket (quantized, as the exponent
         quantizer PPP does) or an INT32 bucket (byte order only: ppp.cc:158-190,
@@ -137,6 +144,7 @@ class PeerSwitchAllReduce:
             raise TypeError("out must have the bucket's dtype")
         P, S = self.P, self.S
         is_int = x.dtype == torch.int32
+        self._mark("start")
         if is_int:
             bswap_i32(x, out=self.payload[:self.numel])                         # INT32 PPP: wire words
         else:
@@ -149,6 +157,7 @@ class PeerSwitchAllReduce:
                 dist.all_reduce(self.exps, op=dist.ReduceOp.MAX, group=self.group)  # switch: int8 max
             quantize_pack(x, P, self.W, global_exps=self.exps, payload=self.payload)  # K3, BE wire words
         self._barrier()                                                         # every plane written
+        self._mark("k2_max_k3")
         blk0, nblk = shard_blocks(self.B, self.W, self.rank)
         # gather straight into `out` when the shards tile it exactly
         pad = self.out_pad.view(torch.int32) if is_int else self.out_pad
@@ -165,6 +174,7 @@ class PeerSwitchAllReduce:
                 ex = self.exps[blk0:blk0 + nblk]
                 switch_aggregate(planes, [ex] * self.W, n_el, P, out=shard[:n_el])  # K6 over xGMI
         self._barrier()                                                         # peers done reading
+        self._mark("k6")
         if self.host_collectives:
             parts = [torch.empty(S * P, dtype=dst.dtype) for _ in range(self.W)]
             dist.all_gather(parts, shard.cpu(), group=self.group)
@@ -173,6 +183,7 @@ class PeerSwitchAllReduce:
             dist.all_gather_into_tensor(dst, shard, group=self.group)
         if dst is not out:
             out.copy_(dst[:self.numel])
+        self._mark("gather")
         return out
 
     def close(self):

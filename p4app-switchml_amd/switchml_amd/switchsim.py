@@ -23,6 +23,8 @@ backend/device ("nccl" = RCCL on ROCm for GPU tensors; "gloo" for CPU tests).
 """
 from __future__ import annotations
 
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -58,6 +60,14 @@ class SwitchSimAllReduce:
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.exps = torch.empty(self.B, dtype=torch.int8, device=dev)
         self.payload = torch.empty(self.B * packet_numel, dtype=torch.int32, device=dev)
+        # diagnostics: a dict here makes the next call record host times at
+        # its phase boundaries (each after a stream sync) — bench.py's breakdown
+        self.phases = None
+
+    def _mark(self, name: str, x: torch.Tensor):
+        if self.phases is not None:
+            torch.cuda.current_stream(x.device).synchronize()
+            self.phases[name] = time.perf_counter()
 
     def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """All-reduce (SUM) of a FLOAT32 bucket (quantized, as the exponent
@@ -78,13 +88,19 @@ class SwitchSimAllReduce:
             exchange_payload(plane, self.group)                              # switch: int32 sum
             out.copy_(plane)
             return out
+        self._mark("start", x)
         exponents(x, self.P, out=self.exps)                                  # K2
+        self._mark("k2", x)
         exchange_exponents(self.exps, self.group)                            # switch: int8 max
+        self._mark("exps_max", x)
         quantize_pack(x, self.P, self.W, global_exps=self.exps, payload=self.payload,
                       flags=FLAG_PAYLOAD_LE)                                 # K3, LE words
+        self._mark("k3", x)
         exchange_payload(self.payload, self.group)                           # switch: int32 sum
+        self._mark("payload_sum", x)
         dequantize(self.payload, self.exps, self.numel, self.P, self.W, out=out,
                    flags=FLAG_PAYLOAD_LE)                                    # K4
+        self._mark("k4", x)
         return out
 
 
