@@ -181,6 +181,14 @@ sml_status_t sml_switch_exps(const int8_t* const* d_exps, uint16_t num_workers, 
  * in-node switch backend.  16-B accesses, the streaming kernels' tile shape. */
 sml_status_t sml_copy_words(const void* d_src, void* d_dst, uint64_t num_words, void* stream);
 
+/* Up to SML_MAX_SWITCH_WORKERS copies in ONE launch: d_dsts[i][0..n_i) =
+ * d_srcs[i][0..n_i), n_i = num_words[i] (HOST arrays of DEVICE pointers, any
+ * 4-byte alignment; segments must not overlap).  The in-node switch's
+ * multicast: the tiles are dealt round-robin over the segments, so W peers'
+ * shards come over their xGMI links at the same time, not one after another. */
+sml_status_t sml_copy_segments(const void* const* d_srcs, void* const* d_dsts, const uint64_t* num_words,
+                               uint32_t num_segments, void* stream);
+
 /* Plane sharing for the peer-to-peer switch: export the allocation holding
  * d_ptr as an IPC handle of sml_ipc_handle_bytes() bytes plus d_ptr's byte
  * offset inside it; open a peer's handle in this process (returns the

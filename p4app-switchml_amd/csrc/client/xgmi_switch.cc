@@ -222,16 +222,29 @@ void XgmiSwitch::FloatChunk(int tid, const float* in, float* out, uint64_t n, hi
     }
     hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
     Barrier(tid);
-    // the multicast: every shard into this worker's tensor
+    // the multicast: every shard into this worker's tensor, all peers' links at once
+    Gather(tp, out, n, B, S, st);
+    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    Barrier(tid);   // peers are done reading our planes before the next chunk
+}
+
+// Worker w's shard of every plane (blocks [w S, min((w+1) S, B))) from its
+// out plane into `out`, one sml_copy_segments launch for the W shards.
+void XgmiSwitch::Gather(ThreadPlanes& tp, void* out, uint64_t n, uint64_t B, uint64_t S, hipStream_t st) {
+    const void* srcs[kMaxW];
+    void* dsts[kMaxW];
+    uint64_t words[kMaxW];
+    uint32_t k = 0;
     for (int w = 0; w < W_; w++) {
         const uint64_t b0 = std::min<uint64_t>((uint64_t)w * S, B);
         const uint64_t nbw = std::min<uint64_t>(S, B - b0);
         if (!nbw) continue;
-        const uint64_t n_el = std::min<uint64_t>(nbw * P_, n - b0 * P_);
-        sml_ok(sml_copy_words(tp.peer_out[w] + b0 * P_, out + b0 * P_, n_el, st), "sml_copy_words");
+        srcs[k] = reinterpret_cast<const uint32_t*>(tp.peer_out[w]) + b0 * P_;
+        dsts[k] = static_cast<uint32_t*>(out) + b0 * P_;
+        words[k] = std::min<uint64_t>(nbw * P_, n - b0 * P_);
+        k++;
     }
-    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
-    Barrier(tid);   // peers are done reading our planes before the next chunk
+    sml_ok(sml_copy_segments(srcs, dsts, words, k, st), "sml_copy_segments");
 }
 
 void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, hipStream_t st) {
@@ -253,13 +266,7 @@ void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, 
     }
     hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
     Barrier(tid);
-    for (int w = 0; w < W_; w++) {
-        const uint64_t b0 = std::min<uint64_t>((uint64_t)w * S, B);
-        const uint64_t nbw = std::min<uint64_t>(S, B - b0);
-        if (!nbw) continue;
-        const uint64_t n_el = std::min<uint64_t>(nbw * P_, n - b0 * P_);
-        sml_ok(sml_copy_words(tp.peer_out[w] + b0 * P_, out + b0 * P_, n_el, st), "sml_copy_words");
-    }
+    Gather(tp, out, n, B, S, st);
     hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
     Barrier(tid);
 }

@@ -74,6 +74,7 @@ class XgmiSwitch {
     void Barrier(int index);
     void FloatChunk(int tid, const float* in, float* out, uint64_t n, hipStream_t st);
     void IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, hipStream_t st);
+    void Gather(ThreadPlanes& tp, void* out, uint64_t n, uint64_t B, uint64_t S, hipStream_t st);
 
     int rank_, W_, T_;
     uint32_t P_;

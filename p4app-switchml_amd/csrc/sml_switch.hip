@@ -167,6 +167,55 @@ struct CopyOp {
     __device__ __forceinline__ uint32_t operator()(uint32_t q) const { return q; }
 };
 
+// The in-node switch's multicast: the W workers' shards gathered in ONE
+// launch.  Copied one after another, each shard would come over one peer's
+// xGMI link at a time; here the tiles are dealt round-robin over the
+// segments in groups of kSegGroup (64 KiB of words), so every resident wave
+// set reads from all W peers — all links at once — while each group stays a
+// contiguous run.  Group g of the launch: segment g % nseg, that segment's
+// group g / nseg (idle once the segment is done: shards differ by at most one
+// block's words).
+constexpr uint32_t kSegGroup = 16;   // tiles per group
+
+struct SegCopyArgs {
+    const uint32_t* src[SML_MAX_SWITCH_WORKERS];
+    uint32_t* dst[SML_MAX_SWITCH_WORKERS];
+    uint64_t n[SML_MAX_SWITCH_WORKERS];
+    uint32_t nseg;
+    uint64_t ntiles;        // nseg x (the largest segment's groups) x kSegGroup
+    uint32_t xcd;
+};
+
+__global__ __launch_bounds__(kBlockThreads) void k_copy_segments(SegCopyArgs a) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
+        const uint64_t g = t / kSegGroup;
+        const uint32_t s = (uint32_t)(g % a.nseg);
+        const uint64_t base = ((g / a.nseg) * kSegGroup + t % kSegGroup) * (uint64_t)kTileElems;
+        const uint64_t n = a.n[s];
+        if (base >= n) continue;
+        const uint32_t* in = a.src[s];
+        uint32_t* out = a.dst[s];
+        if (base + kTileElems <= n) {
+            u4a v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; u++)
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(in + base + (u * kWave + lane) * 4));
+#pragma unroll
+            for (int u = 0; u < kU; u++) *reinterpret_cast<u4a*>(out + base + (u * kWave + lane) * 4) = v[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < kU; u++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4 + j;
+                    if (idx < n) out[idx] = in[idx];
+                }
+        }
+    }
+}
+
 template <bool ALIGNED, bool BE, bool RCP, bool EXPS>
 static void launch_switch_p(uint32_t P, dim3 grid, hipStream_t st, const SwitchArgs& a) {
     switch (P) {
@@ -261,6 +310,31 @@ sml_status_t sml_copy_words(const void* d_src, void* d_dst, uint64_t num_words, 
     k_words<<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(
         static_cast<const uint32_t*>(d_src), static_cast<uint32_t*>(d_dst), num_words,
         g_xcd_chunk.load(std::memory_order_relaxed), CopyOp{});
+    return launch_check();
+}
+
+sml_status_t sml_copy_segments(const void* const* d_srcs, void* const* d_dsts, const uint64_t* num_words,
+                               uint32_t num_segments, void* stream) {
+    if (num_segments == 0) return SML_OK;
+    if (!d_srcs || !d_dsts || !num_words || num_segments > SML_MAX_SWITCH_WORKERS) return SML_ERR_INVALID_ARG;
+    SegCopyArgs a;
+    a.nseg = 0;
+    uint64_t groups = 0;
+    const uint64_t gw = (uint64_t)kSegGroup * kTileElems;   // words per group
+    for (uint32_t i = 0; i < num_segments; i++) {
+        if (num_words[i] == 0) continue;                    // empty segments touch nothing
+        if (!d_srcs[i] || !d_dsts[i] || !aligned4(d_srcs[i]) || !aligned4(d_dsts[i])) return SML_ERR_INVALID_ARG;
+        a.src[a.nseg] = static_cast<const uint32_t*>(d_srcs[i]);
+        a.dst[a.nseg] = static_cast<uint32_t*>(d_dsts[i]);
+        a.n[a.nseg] = num_words[i];
+        const uint64_t gi = (num_words[i] + gw - 1) / gw;
+        groups = gi > groups ? gi : groups;
+        a.nseg++;
+    }
+    if (a.nseg == 0) return SML_OK;
+    a.ntiles = (uint64_t)a.nseg * groups * kSegGroup;
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    k_copy_segments<<<grid_for_tiles(a.ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(a);
     return launch_check();
 }
 

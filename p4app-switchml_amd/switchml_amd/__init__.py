@@ -122,6 +122,8 @@ def lib():
     L.sml_rx_reset.argtypes = [vp, u64, vp]
     L.sml_switch_aggregate.restype = i32
     L.sml_switch_aggregate.argtypes = [vp, vp, u16, u64, u32, vp, vp, vp, u32, vp]
+    L.sml_copy_segments.restype = i32
+    L.sml_copy_segments.argtypes = [vp, vp, vp, u32, vp]
     L.sml_ipc_handle_bytes.restype = u32
     L.sml_ipc_get_handle.restype = i32
     L.sml_ipc_get_handle.argtypes = [vp, vp, ctypes.POINTER(u64)]
@@ -366,6 +368,28 @@ def switch_aggregate(payloads, exps=None, numel: int | None = None, packet_numel
         None if exps_out is None else _dev(exps_out, torch.int8, "exps_out"),
         None if out is None else _dev(out, torch.float32, "out"), flags, _stream(stream, payloads[0])))
     return out
+
+
+def copy_segments(pairs, stream=None):
+    """sml_copy_segments: every (src, dst) pair of 32-bit tensors (same
+    numel; CUDA or pinned host) copied in ONE launch, the tiles dealt
+    round-robin over the pairs (the in-node switch's multicast)."""
+    torch = _torch()
+    k = len(pairs)
+    if k > MAX_SWITCH_WORKERS:
+        raise ValueError(f"at most {MAX_SWITCH_WORKERS} segments")
+    srcs = (ctypes.c_void_p * max(1, k))()
+    dsts = (ctypes.c_void_p * max(1, k))()
+    words = (ctypes.c_uint64 * max(1, k))()
+    for i, (s, d) in enumerate(pairs):
+        if s.numel() != d.numel() or s.element_size() != 4 or d.element_size() != 4:
+            raise ValueError("segments are pairs of equal-size 32-bit tensors")
+        srcs[i] = _dev(s, s.dtype, "src").value
+        dsts[i] = _dev(d, d.dtype, "dst").value
+        words[i] = s.numel()
+    _check("sml_copy_segments", lib().sml_copy_segments(
+        ctypes.cast(srcs, ctypes.c_void_p), ctypes.cast(dsts, ctypes.c_void_p), ctypes.cast(words, ctypes.c_void_p),
+        k, _stream(stream, pairs[0][0] if pairs else None)))
 
 
 def stream_copy(src, dst, stream=None):

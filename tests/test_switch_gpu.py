@@ -151,3 +151,33 @@ def test_switch_aggregate_rejects_bad_args():
     st = S.lib().sml_switch_aggregate(ctypes.cast(ptrs, ctypes.c_void_p), None, 1, 1024, 256,
                                       ctypes.c_void_p(pl.data_ptr() + 4), None, None, 0, None)
     assert st == 3   # SML_ERR_ALIGNMENT: output plane not 16-byte aligned
+
+
+@pytest.mark.parametrize("sizes,offs", [
+    ([1000, 1000, 999], [0, 0, 0]),
+    ([16384 * 3 + 5, 0, 1, 17, 16384 * 16 + 1024, 33], [1, 0, 2, 3, 0, 1]),
+    ([1 << 20] * 8, [0, 1, 2, 3, 0, 1, 2, 3]),
+    ([(1 << 22) + 7] * 15 + [3], [3] * 16),
+])
+def test_copy_segments(cuda, sizes, offs):
+    """sml_copy_segments (the in-node switch's multicast in one launch: tiles
+    dealt round-robin over the segments in 64 KiB groups): every segment
+    copied exactly — ragged, empty, one-word and 4-byte-offset segments —
+    and nothing outside the segments written."""
+    import torch
+    import switchml_amd as sw
+    g = torch.Generator(device="cuda")
+    g.manual_seed(sum(sizes))
+    total = sum(n + o for n, o in zip(sizes, offs)) + 64
+    src = torch.randint(-2**31, 2**31 - 1, (total,), dtype=torch.int32, device="cuda", generator=g)
+    dst = torch.full((total,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    want = dst.clone()
+    pairs, pos = [], 0
+    for n, o in zip(sizes, offs):
+        pos += o
+        pairs.append((src[pos:pos + n], dst[pos:pos + n]))
+        want[pos:pos + n] = src[pos:pos + n]
+        pos += n
+    sw.copy_segments(pairs)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, want)
