@@ -103,6 +103,7 @@ XgmiSwitch::XgmiSwitch(const Config& config, int device) {
         hip_ok(hipMalloc(&tp.payload, cap_ * 4), "hipMalloc");
         hip_ok(hipMalloc(&tp.out, cap_ * 4), "hipMalloc");
         hip_ok(hipMalloc(&tp.gexp, cap_b), "hipMalloc");
+        hip_ok(hipStreamCreateWithFlags(&tp.xst, hipStreamNonBlocking), "hipStreamCreate");
         ShmPlanes& sp = shm_->planes[rank_][t];
         hipIpcMemHandle_t h;
         hip_ok(hipIpcGetMemHandle(&h, tp.exps), "hipIpcGetMemHandle");
@@ -165,6 +166,7 @@ XgmiSwitch::~XgmiSwitch() {
         (void)hipFree(tp.payload);
         (void)hipFree(tp.out);
         (void)hipFree(tp.gexp);
+        if (tp.xst) (void)hipStreamDestroy(tp.xst);
     }
     const bool last = shm_->detached.fetch_add(1) + 1 == (uint32_t)W_;
     munmap(shm_, sizeof(XgmiShm));
@@ -193,39 +195,72 @@ void XgmiSwitch::Barrier(int index) {
     }
 }
 
-void XgmiSwitch::FloatChunk(int tid, const float* in, float* out, uint64_t n, hipStream_t st) {
-    ThreadPlanes& tp = planes_[tid];
+namespace {
+void stream_sync(hipStream_t st) { hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize"); }
+}  // namespace
+
+// The switch's exponent max over the W planes into gexp, then K3: quantize
+// with the global exponents into the own BE payload plane.
+void XgmiSwitch::Quantize(ThreadPlanes& tp, const float* in, uint64_t n, hipStream_t st) {
+    const uint64_t B = sml_num_blocks(n, P_);
+    sml_ok(sml_switch_exps(tp.peer_exps.data(), (uint16_t)W_, B, tp.gexp, st), "sml_switch_exps");
+    sml_ok(sml_quantize_pack(in, n, P_, (uint16_t)W_, tp.gexp, tp.payload, nullptr, 0, st), "sml_quantize_pack");
+}
+
+// K6: the wrapping sum of this worker's shard over the W planes, dequantized
+// into the own output plane.
+void XgmiSwitch::Aggregate(ThreadPlanes& tp, uint64_t n, hipStream_t st) {
     const uint64_t B = sml_num_blocks(n, P_);
     const uint64_t S = (B + W_ - 1) / W_;
-    // K2: this worker's exponents; the switch's int8 max over the W planes
-    sml_ok(sml_exponents(in, n, P_, tp.exps, st), "sml_exponents");
-    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
-    Barrier(tid);
-    sml_ok(sml_switch_exps(tp.peer_exps.data(), (uint16_t)W_, B, tp.gexp, st), "sml_switch_exps");
-    // K3: quantize with the global exponents into the own BE payload plane
-    sml_ok(sml_quantize_pack(in, n, P_, (uint16_t)W_, tp.gexp, tp.payload, nullptr, 0, st), "sml_quantize_pack");
-    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
-    Barrier(tid);
-    // K6: the wrapping sum of this worker's shard over the W planes, dequantized
     const uint64_t blk0 = std::min<uint64_t>((uint64_t)rank_ * S, B);
     const uint64_t nb = std::min<uint64_t>(S, B - blk0);
-    if (nb) {
-        const uint64_t n_el = std::min<uint64_t>(nb * P_, n - blk0 * P_);
-        const int32_t* planes[kMaxW];
-        const int8_t* exps[kMaxW];
-        for (int w = 0; w < W_; w++) {
-            planes[w] = tp.peer_payload[w] + blk0 * P_;
-            exps[w] = tp.gexp + blk0;
-        }
-        sml_ok(sml_switch_aggregate(planes, exps, (uint16_t)W_, n_el, P_, nullptr, nullptr, tp.out + blk0 * P_, 0, st),
-               "sml_switch_aggregate");
+    if (!nb) return;
+    const uint64_t n_el = std::min<uint64_t>(nb * P_, n - blk0 * P_);
+    const int32_t* planes[kMaxW];
+    const int8_t* exps[kMaxW];
+    for (int w = 0; w < W_; w++) {
+        planes[w] = tp.peer_payload[w] + blk0 * P_;
+        exps[w] = tp.gexp + blk0;
     }
-    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    sml_ok(sml_switch_aggregate(planes, exps, (uint16_t)W_, n_el, P_, nullptr, nullptr, tp.out + blk0 * P_, 0, st),
+           "sml_switch_aggregate");
+}
+
+// A FLOAT32 slice, chunk by chunk, pipelined on two streams (the caller's
+// `st` for the local HBM work, tp.xst for the xGMI phases):
+//   prologue   K2(0) | barrier | max + K3(0) | barrier
+//   chunk c    K6(c) on xst  beside  K2(c+1) on st          | barrier
+//              gather(c) on xst  beside  max + K3(c+1) on st | barrier
+// Every plane's readers finish before the barrier that precedes its next
+// writer: exps (peers' max of chunk c+1, phase 2) before K2(c+2) (phase 1 of
+// the next chunk); payload (peers' K6(c), phase 1) before K3(c+1) (phase 2);
+// out (peers' gather(c), phase 2) before K6(c+1); gexp (own K6(c)) before
+// the max of chunk c+1.  So one set of planes serves the pipeline.
+void XgmiSwitch::FloatSlice(int tid, const float* in, float* out, uint64_t numel, hipStream_t st) {
+    ThreadPlanes& tp = planes_[tid];
+    const uint64_t nchunks = (numel + cap_ - 1) / cap_;
+    auto len = [&](uint64_t c) { return std::min<uint64_t>(cap_, numel - c * cap_); };
+    sml_ok(sml_exponents(in, len(0), P_, tp.exps, st), "sml_exponents");
+    stream_sync(st);
     Barrier(tid);
-    // the multicast: every shard into this worker's tensor, all peers' links at once
-    Gather(tp, out, n, B, S, st);
-    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
-    Barrier(tid);   // peers are done reading our planes before the next chunk
+    Quantize(tp, in, len(0), st);
+    stream_sync(st);
+    Barrier(tid);
+    for (uint64_t c = 0; c < nchunks; c++) {
+        const uint64_t n = len(c), B = sml_num_blocks(n, P_), S = (B + W_ - 1) / W_;
+        const bool next = c + 1 < nchunks;
+        const float* in_next = in + (c + 1) * cap_;
+        Aggregate(tp, n, tp.xst);
+        if (next) sml_ok(sml_exponents(in_next, len(c + 1), P_, tp.exps, st), "sml_exponents");
+        stream_sync(tp.xst);
+        stream_sync(st);
+        Barrier(tid);
+        Gather(tp, out + c * cap_, n, B, S, tp.xst);
+        if (next) Quantize(tp, in_next, len(c + 1), st);
+        stream_sync(tp.xst);
+        stream_sync(st);
+        Barrier(tid);   // peers are done reading our planes before they are written again
+    }
 }
 
 // Worker w's shard of every plane (blocks [w S, min((w+1) S, B))) from its
@@ -273,12 +308,14 @@ void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, 
 
 void XgmiSwitch::AllReduceSlice(int tid, const void* in, void* out, uint64_t numel, DataType type, hipStream_t st) {
     if (tid < 0 || tid >= T_) throw SwitchMLFatal("xgmi switch: bad worker thread id");
+    if (numel == 0) return;
+    if (type == FLOAT32) {
+        FloatSlice(tid, static_cast<const float*>(in), static_cast<float*>(out), numel, st);
+        return;
+    }
     for (uint64_t off = 0; off < numel; off += cap_) {
         const uint64_t n = std::min<uint64_t>(cap_, numel - off);
-        if (type == FLOAT32)
-            FloatChunk(tid, static_cast<const float*>(in) + off, static_cast<float*>(out) + off, n, st);
-        else
-            IntChunk(tid, static_cast<const int32_t*>(in) + off, static_cast<int32_t*>(out) + off, n, st);
+        IntChunk(tid, static_cast<const int32_t*>(in) + off, static_cast<int32_t*>(out) + off, n, st);
     }
 }
 

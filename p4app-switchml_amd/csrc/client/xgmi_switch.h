@@ -12,13 +12,19 @@
 //     switchml.proto:21-91) holds every worker thread's plane IPC handles and
 //     one barrier per worker thread;
 //   * per FIFO slice (thread t of every worker, the same slice geometry on all
-//     workers, as the switch's slots are): K2 exponents into the own plane →
-//     barrier → the max over the W exponent planes (sml_switch_exps) → K3
-//     quantize with the global exponents into the own BE payload plane →
-//     barrier → K6 on this worker's shard of ceil(B / W) blocks, reading the W
-//     payload planes (W − 1 over xGMI) and writing the dequantized fp32 shard
-//     into the own output plane → barrier → every worker copies the W shards
-//     into its tensor (the multicast) → barrier;
+//     workers, as the switch's slots are), chunk by chunk: K2 exponents into
+//     the own plane → barrier → the max over the W exponent planes
+//     (sml_switch_exps) → K3 quantize with the global exponents into the own
+//     BE payload plane → barrier → K6 on this worker's shard of ceil(B / W)
+//     blocks, reading the W payload planes (W − 1 over xGMI) and writing the
+//     dequantized fp32 shard into the own output plane → barrier → every
+//     worker gathers the W shards into its tensor (the multicast, one
+//     sml_copy_segments launch) → barrier.  FLOAT32 slices of several chunks
+//     are pipelined on two streams: chunk c's K6 runs beside chunk c + 1's K2
+//     and chunk c's gather beside chunk c + 1's exponent max and K3 (local
+//     HBM work beside the xGMI phases), two barriers per chunk; one set of
+//     planes suffices because every plane's readers finish one phase before
+//     its next writer starts (xgmi_switch.cc, FloatSlice);
 //   * INT32 slices: the words themselves are summed (the INT32 PPP only
 //     reorders bytes, ppp.cc:158-190, 262-298).
 // Results are bit-identical to the oracle's W-worker software switch
@@ -69,10 +75,13 @@ class XgmiSwitch {
         std::vector<const int8_t*> peer_exps;      // [W], own included
         std::vector<const int32_t*> peer_payload;  // [W]
         std::vector<const float*> peer_out;        // [W]
+        hipStream_t xst = nullptr;     // the exchange stream (K6, gather) beside the caller's
     };
 
     void Barrier(int index);
-    void FloatChunk(int tid, const float* in, float* out, uint64_t n, hipStream_t st);
+    void FloatSlice(int tid, const float* in, float* out, uint64_t numel, hipStream_t st);
+    void Aggregate(ThreadPlanes& tp, uint64_t n, hipStream_t st);
+    void Quantize(ThreadPlanes& tp, const float* in, uint64_t n, hipStream_t st);
     void IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, hipStream_t st);
     void Gather(ThreadPlanes& tp, void* out, uint64_t n, uint64_t B, uint64_t S, hipStream_t st);
 
