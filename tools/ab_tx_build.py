@@ -6,6 +6,12 @@ tools/ab/ (sources copied and patched there; tools/ab/ is git-ignored):
             slices' scales read from the LDS table before any store
   tx_nohdr  DIAGNOSTIC ONLY (frames wrong): no lane-parallel header stores —
             what do the headers cost?
+  fr_w8     k_quantize_frames and k_rx_apply held to 8 waves per SIMD
+            (amdgpu_waves_per_eu): both are SGPR-limited to 7 otherwise
+  tx_w8     the same for k_quantize_frames only
+  sw_w8     the same for K6 k_switch_aggregate (6-7 waves otherwise)
+  rx_vec    rx apply reads its state words with vector (broadcast) loads
+  rx_vec_w8 rx_vec held to 8 waves per SIMD
 Timed by tools/ab_frames.py on the GPU (AB_NOCHECK=1 when tx_nohdr is in)."""
 import os
 import shutil
@@ -55,12 +61,12 @@ def build(name, patches=()):
     if os.path.isdir(d):
         shutil.rmtree(d)
     shutil.copytree(os.path.join(PKG, "csrc"), os.path.join(d, "csrc"))
-    f = os.path.join(d, "csrc", "sml_frames.hip")
-    s = open(f).read()
-    for old, new in patches:
+    for patch in patches:
+        fname, old, new = patch if len(patch) == 3 else ("sml_frames.hip",) + tuple(patch)
+        f = os.path.join(d, "csrc", fname)
+        s = open(f).read()
         assert s.count(old) == 1, old
-        s = s.replace(old, new)
-    open(f, "w").write(s)
+        open(f, "w").write(s.replace(old, new))
     objs = []
     for k in ("sml_quantizer", "sml_frames", "sml_switch"):
         o = os.path.join(d, k + ".o")
@@ -75,7 +81,24 @@ def build(name, patches=()):
     print(out)
 
 
-VARIANTS = {"tx_base": (), "tx_bf": ((PAYLOAD, PAYLOAD_BF),), "tx_nohdr": ((HDR, NOHDR),)}
+TXK = "__global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) {"
+RXK = "__global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {"
+W8 = "__attribute__((amdgpu_waves_per_eu(8, 8))) "
+RXS = "        if constexpr (kChunksPerFrame >= kWave) {"
+SWK = "__global__ __launch_bounds__(kBlockThreads) void k_switch_aggregate(SwitchArgs a) {"
+
+VARIANTS = {"tx_base": (), "tx_bf": ((PAYLOAD, PAYLOAD_BF),), "tx_nohdr": ((HDR, NOHDR),),
+            # occupancy: both frames kernels are SGPR-limited to 7 waves per SIMD (106 SGPRs)
+            "fr_w8": ((TXK, TXK.replace("__global__ ", "__global__ " + W8)),
+                      (RXK, RXK.replace("__global__ ", "__global__ " + W8))),
+            "tx_w8": ((TXK, TXK.replace("__global__ ", "__global__ " + W8)),),
+            # rx apply: state words by (broadcast) vector loads instead of scalar loads, so the
+            # SGPR budget fits 8 waves without spilling into the loop; with and without the hint
+            "rx_vec": ((RXS, RXS.replace("kChunksPerFrame >= kWave", "false && kChunksPerFrame >= kWave")),),
+            "rx_vec_w8": ((RXS, RXS.replace("kChunksPerFrame >= kWave", "false && kChunksPerFrame >= kWave")),
+                          (RXK, RXK.replace("__global__ ", "__global__ " + W8))),
+            # K6 (switch aggregate): 6-7 waves per SIMD by its SGPRs / VGPRs
+            "sw_w8": (("sml_switch.hip", SWK, SWK.replace("__global__ ", "__global__ " + W8)),)}
 
 if __name__ == "__main__":
     os.makedirs(AB, exist_ok=True)
