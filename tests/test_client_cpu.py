@@ -82,6 +82,10 @@ def test_config_validation(ctx):
     C.stop()
     C.start(C.make_config(prepostprocessor="bypass", num_worker_threads=4, max_outstanding_packets=255, bandwidth=0))
     assert "max_outstanding_packets = 256" in C.config_text()
+    assert "coalesce_us = 20" in C.config_text()          # zero-copy coalescing window, default
+    C.stop()
+    C.start(C.make_config(prepostprocessor="bypass", coalesce_us=0, bandwidth=0))
+    assert "coalesce_us = 0" in C.config_text()
     C.stop()
     for bad in (dict(prepostprocessor="nope"), dict(backend="dpdk"), dict(mode="turbo"),
                 dict(num_worker_threads=8, max_outstanding_packets=4)):
