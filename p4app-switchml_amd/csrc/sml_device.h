@@ -180,6 +180,14 @@ __device__ __forceinline__ void store4_guarded(float* p, f4 v, uint64_t idx, uin
 // non-temporal stores on the 256 MiB bucket (loads stay non-temporal,
 // which is 15 % faster than default-policy loads) — profiles/r01/ab*.json.
 __device__ __forceinline__ void store_payload(u4* dst, u4 q) { *dst = q; }
+// Past the Infinity Cache's reach (a slice whose payload plane cannot stay
+// resident) non-temporal payload stores stream faster: K1 picks the policy by
+// plane size (sml_set_payload_nt_threshold).
+template <bool NT>
+__device__ __forceinline__ void store_payload_as(u4* dst, u4 q) {
+    if constexpr (NT) __builtin_nontemporal_store(q, dst);
+    else *dst = q;
+}
 
 // ---------------------------------------------------- per-packet reductions
 

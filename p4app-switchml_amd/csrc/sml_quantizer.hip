@@ -32,7 +32,7 @@ __device__ __forceinline__ void global_tile_exponents(const QuantArgs& a, uint64
 }
 
 // Quantize + pack 4 consecutive elements (one lane's part of a slice).
-template <int P, bool BE, bool RNE>
+template <int P, bool BE, bool RNE, bool NTS>
 __device__ __forceinline__ void quant_slice(const QuantArgs& a, uint64_t idx, f4 v, const float* lut, int e) {
     const float s = lut[(uint8_t)e];
     uint64_t body = 0;
@@ -45,12 +45,12 @@ __device__ __forceinline__ void quant_slice(const QuantArgs& a, uint64_t idx, f4
     }
     u4 q = quantize4<RNE>(v, s, idx, body);
     if constexpr (BE) { q.x = bswap(q.x); q.y = bswap(q.y); q.z = bswap(q.z); q.w = bswap(q.w); }
-    store_payload(a.payload + idx / 4, q);
+    store_payload_as<NTS>(a.payload + idx / 4, q);
 }
 
 // Exponents, quantize and pack of one loaded tile (K3: `e` holds the global
 // exponents already).
-template <int P, bool GLOBAL, bool BE, bool RNE, int U>
+template <int P, bool GLOBAL, bool BE, bool RNE, int U, bool NTS>
 __device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, int lane, const f4 (&v)[U],
                                            const float* lut, int (&e)[U]) {
     const uint64_t padded = a.nblocks * P;
@@ -76,13 +76,13 @@ __device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, in
     // ab_k3_waitcnt.json.
     if (base + kElems <= padded) {
 #pragma unroll
-        for (int u = 0; u < U; u++) quant_slice<P, BE, RNE>(a, base + (uint64_t)(u * kWave + lane) * 4, v[u], lut, e[u]);
+        for (int u = 0; u < U; u++) quant_slice<P, BE, RNE, NTS>(a, base + (uint64_t)(u * kWave + lane) * 4, v[u], lut, e[u]);
         return;
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-        if (idx < padded) quant_slice<P, BE, RNE>(a, idx, v[u], lut, e[u]);
+        if (idx < padded) quant_slice<P, BE, RNE, NTS>(a, idx, v[u], lut, e[u]);
     }
 }
 
@@ -91,7 +91,7 @@ __device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, in
 // of 256 elements (one 16-B load per lane per slice, all issued before any
 // arithmetic); U = 4 by default — four loads in flight per lane keep the
 // stream at the copy rate, smaller tiles measured slower.
-template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE, int U>
+template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE, int U, bool NTS = false>
 __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
     __shared__ float lut[256];
     if (a.payload) build_lut(lut, a.W);
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
         // K3: the exponent dword is read after the data loads are in flight
         // (read first, the compiler waits on it before issuing them: asm)
         if constexpr (GLOBAL) global_tile_exponents<P>(a, base, lane, e);
-        quant_tile<P, GLOBAL, BE, RNE>(a, base, lane, v, lut, e);
+        quant_tile<P, GLOBAL, BE, RNE, U, NTS>(a, base, lane, v, lut, e);
     }
 }
 
@@ -367,24 +367,25 @@ __global__ void k_scale_lut(float* lut, uint32_t W) {
 // Dispatch tables: runtime (P, tile slices U, alignment, mode) -> template
 // instance.  U is 1, 2 or 4 and at least P / 256 (quantize_common).
 template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
-static void launch_quant_u(uint32_t U, dim3 grid, hipStream_t st, const QuantArgs& a) {
+static void launch_quant_u(uint32_t U, bool nts, dim3 grid, hipStream_t st, const QuantArgs& a) {
     if constexpr (P <= 256) {
         if (U == 1) { k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 1><<<grid, kBlockThreads, 0, st>>>(a); return; }
     }
     if constexpr (P <= 512) {
         if (U == 2) { k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 2><<<grid, kBlockThreads, 0, st>>>(a); return; }
     }
+    if (nts) { k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 4, true><<<grid, kBlockThreads, 0, st>>>(a); return; }
     k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 4><<<grid, kBlockThreads, 0, st>>>(a);
 }
 
 template <bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
-static void launch_quant_p(uint32_t P, uint32_t U, dim3 grid, hipStream_t st, const QuantArgs& a) {
+static void launch_quant_p(uint32_t P, uint32_t U, bool nts, dim3 grid, hipStream_t st, const QuantArgs& a) {
     switch (P) {
-        case 64:   launch_quant_u<64, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
-        case 128:  launch_quant_u<128, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
-        case 256:  launch_quant_u<256, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
-        case 512:  launch_quant_u<512, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
-        default:   launch_quant_u<1024, ALIGNED, GLOBAL, BE, RNE>(U, grid, st, a); break;
+        case 64:   launch_quant_u<64, ALIGNED, GLOBAL, BE, RNE>(U, nts, grid, st, a); break;
+        case 128:  launch_quant_u<128, ALIGNED, GLOBAL, BE, RNE>(U, nts, grid, st, a); break;
+        case 256:  launch_quant_u<256, ALIGNED, GLOBAL, BE, RNE>(U, nts, grid, st, a); break;
+        case 512:  launch_quant_u<512, ALIGNED, GLOBAL, BE, RNE>(U, nts, grid, st, a); break;
+        default:   launch_quant_u<1024, ALIGNED, GLOBAL, BE, RNE>(U, nts, grid, st, a); break;
     }
 }
 
@@ -395,6 +396,15 @@ static void launch_quant_p(uint32_t P, uint32_t U, dim3 grid, hipStream_t st, co
 // 2-slice tiles are level on cold HBM and lose up to 11 % resident.
 static std::atomic<uint32_t> g_quant_slices{4};
 
+// Payload planes of at least this many bytes take non-temporal stores
+// (sml_set_payload_nt_threshold; UINT64_MAX = never, 0 = always).  Measured,
+// one bucket re-read every step (profiles/r02c/ab_store_size*.json): up to
+// 256 MiB default-policy stores win (7.13 vs 6.35 TB/s at 256 MiB: the
+// planes stay in the 256 MiB Infinity Cache); from 288 MiB on, where they
+// cannot, non-temporal stores win by 5 % (6.33-6.41 vs 6.01-6.11 TB/s at
+// 288 MiB-1 GiB).  So: non-temporal past the Infinity Cache's size.
+static std::atomic<uint64_t> g_nt_threshold{(256ull << 20) + 1};
+
 static uint32_t quant_slices(uint32_t P) {
     const uint32_t need = P > 256 ? P / 256 : 1;
     const uint32_t want = g_quant_slices.load(std::memory_order_relaxed);
@@ -402,15 +412,16 @@ static uint32_t quant_slices(uint32_t P) {
 }
 
 template <bool ALIGNED, bool GLOBAL, bool BE>
-static void launch_quant_r(bool rne, uint32_t P, uint32_t U, dim3 g, hipStream_t st, const QuantArgs& a) {
-    if (rne) launch_quant_p<ALIGNED, GLOBAL, BE, true>(P, U, g, st, a);
-    else launch_quant_p<ALIGNED, GLOBAL, BE, false>(P, U, g, st, a);
+static void launch_quant_r(bool rne, uint32_t P, uint32_t U, bool nts, dim3 g, hipStream_t st, const QuantArgs& a) {
+    if (rne) launch_quant_p<ALIGNED, GLOBAL, BE, true>(P, U, nts, g, st, a);
+    else launch_quant_p<ALIGNED, GLOBAL, BE, false>(P, U, nts, g, st, a);
 }
 
 template <bool ALIGNED, bool GLOBAL>
-static void launch_quant_b(bool be, bool rne, uint32_t P, uint32_t U, dim3 g, hipStream_t st, const QuantArgs& a) {
-    if (be) launch_quant_r<ALIGNED, GLOBAL, true>(rne, P, U, g, st, a);
-    else launch_quant_r<ALIGNED, GLOBAL, false>(rne, P, U, g, st, a);
+static void launch_quant_b(bool be, bool rne, uint32_t P, uint32_t U, bool nts, dim3 g, hipStream_t st,
+                           const QuantArgs& a) {
+    if (be) launch_quant_r<ALIGNED, GLOBAL, true>(rne, P, U, nts, g, st, a);
+    else launch_quant_r<ALIGNED, GLOBAL, false>(rne, P, U, nts, g, st, a);
 }
 
 template <bool ALIGNED, bool BE, bool RCP>
@@ -487,6 +498,8 @@ uint32_t sml_set_xcd_chunk(uint32_t chunk) {
     return g_xcd_chunk.exchange(chunk);
 }
 
+uint64_t sml_set_payload_nt_threshold(uint64_t bytes) { return g_nt_threshold.exchange(bytes); }
+
 uint32_t sml_set_quantize_tile_slices(uint32_t slices) {
     return g_quant_slices.exchange(slices == 1 || slices == 2 ? slices : 4u);
 }
@@ -536,12 +549,14 @@ static sml_status_t quantize_common(const float* d_in, uint64_t numel, uint32_t 
     dim3 grid(grid_for_tiles(a.ntiles));
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_in), be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
+    // payload store policy by plane size (4-slice tiles only)
+    const bool nts = d_payload && U == 4 && 4 * numel >= g_nt_threshold.load(std::memory_order_relaxed);
     if (d_gexp) {
-        if (al) launch_quant_b<true, true>(be, rne, P, U, grid, st, a);
-        else launch_quant_b<false, true>(be, rne, P, U, grid, st, a);
+        if (al) launch_quant_b<true, true>(be, rne, P, U, nts, grid, st, a);
+        else launch_quant_b<false, true>(be, rne, P, U, nts, grid, st, a);
     } else {
-        if (al) launch_quant_b<true, false>(be, rne, P, U, grid, st, a);
-        else launch_quant_b<false, false>(be, rne, P, U, grid, st, a);
+        if (al) launch_quant_b<true, false>(be, rne, P, U, nts, grid, st, a);
+        else launch_quant_b<false, false>(be, rne, P, U, nts, grid, st, a);
     }
     return launch_check();
 }

@@ -114,6 +114,8 @@ def lib():
     L.sml_quantize_pack_frames.argtypes = [vp, u64, u32, u16, vp, u32, ctypes.POINTER(FrameParams), vp, u64, vp]
     L.sml_set_quantize_tile_slices.restype = u32
     L.sml_set_quantize_tile_slices.argtypes = [u32]
+    L.sml_set_payload_nt_threshold.restype = u64
+    L.sml_set_payload_nt_threshold.argtypes = [u64]
     L.sml_set_xcd_chunk.restype = u32
     L.sml_set_xcd_chunk.argtypes = [u32]
     L.sml_dequantize_frames.restype = i32
@@ -179,6 +181,13 @@ def shard_quantize_pack(job, rank: int, world: int, packet_numel: int = 256, num
 
 def set_grid_limit(max_workgroups: int) -> int:
     return int(lib().sml_set_grid_limit(max_workgroups))
+
+
+def set_payload_nt_threshold(nbytes: int) -> int:
+    """Payload planes of at least `nbytes` bytes take non-temporal stores in
+    K1/K3 (default: larger than the 256 MiB Infinity Cache; 2**64-1 = never,
+    0 = always); returns the previous threshold."""
+    return int(lib().sml_set_payload_nt_threshold(nbytes))
 
 
 def set_quantize_tile_slices(slices: int) -> int:

@@ -108,8 +108,9 @@ def test_quantize_tile_slices_invariant(sw, P):
             xs, xn = xd[off:off + n], x_np[off:off + n]
             want_q, want_e = O.quantize(xn, P, W), O.exponents(xn, P)
             want_rne = O.quantize(xn, P, W, rounding=O.RNE_VCL)
-            for sl in (0, 1, 2, 4):
+            for sl, nt in ((0, 0), (1, 0), (2, 0), (4, 0), (4, 2 ** 64 - 1)):
                 sw.set_quantize_tile_slices(sl)
+                sw.set_payload_nt_threshold(nt)      # 0: non-temporal payload stores; max: default policy
                 for cap, chunk in GEOMETRIES[:3] + GEOMETRIES[6:8]:
                     sw.set_grid_limit(cap)
                     sw.set_xcd_chunk(chunk)
@@ -126,3 +127,4 @@ def test_quantize_tile_slices_invariant(sw, P):
                     assert np.array_equal(rne.cpu().numpy().view(np.uint32), want_rne), tag
     finally:
         sw.set_quantize_tile_slices(0)
+        sw.set_payload_nt_threshold((256 << 20) + 1)

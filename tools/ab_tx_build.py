@@ -12,6 +12,7 @@ tools/ab/ (sources copied and patched there; tools/ab/ is git-ignored):
   sw_w8     the same for K6 k_switch_aggregate (6-7 waves otherwise)
   rx_vec    rx apply reads its state words with vector (broadcast) loads
   rx_vec_w8 rx_vec held to 8 waves per SIMD
+  k1_ntstore K1's payload stores non-temporal (tools/ab_store_size.py)
 Timed by tools/ab_frames.py on the GPU (AB_NOCHECK=1 when tx_nohdr is in)."""
 import os
 import shutil
@@ -92,6 +93,9 @@ VARIANTS = {"tx_base": (), "tx_bf": ((PAYLOAD, PAYLOAD_BF),), "tx_nohdr": ((HDR,
             "fr_w8": ((TXK, TXK.replace("__global__ ", "__global__ " + W8)),
                       (RXK, RXK.replace("__global__ ", "__global__ " + W8))),
             "tx_w8": ((TXK, TXK.replace("__global__ ", "__global__ " + W8)),),
+            # K1: non-temporal payload stores (sml_device.h store_payload)
+            "k1_ntstore": (("sml_device.h", "__device__ __forceinline__ void store_payload(u4* dst, u4 q) { *dst = q; }",
+                            "__device__ __forceinline__ void store_payload(u4* dst, u4 q) { __builtin_nontemporal_store(q, dst); }"),),
             # rx apply: state words by (broadcast) vector loads instead of scalar loads, so the
             # SGPR budget fits 8 waves without spilling into the loop; with and without the hint
             "rx_vec": ((RXS, RXS.replace("kChunksPerFrame >= kWave", "false && kChunksPerFrame >= kWave")),),
