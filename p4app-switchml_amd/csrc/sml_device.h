@@ -160,12 +160,16 @@ __device__ __forceinline__ f4 load4_guarded(const float* p, uint64_t idx, uint64
     return v;
 }
 
-template <bool ALIGNED>
+// NT: non-temporal (for output planes larger than the Infinity Cache: see
+// g_nt_threshold in sml_quantizer.hip); default policy otherwise.
+template <bool ALIGNED, bool NT = false>
 __device__ __forceinline__ void store4(float* p, f4 v) {
     if constexpr (ALIGNED) {
-        *reinterpret_cast<f4*>(p) = v;   // default policy: faster than nt stores here
+        if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
+        else *reinterpret_cast<f4*>(p) = v;   // default policy: faster than nt stores up to 256 MiB
     } else {
-        *reinterpret_cast<f4a*>(p) = f4a{v.x, v.y, v.z, v.w};
+        if constexpr (NT) __builtin_nontemporal_store(f4a{v.x, v.y, v.z, v.w}, reinterpret_cast<f4a*>(p));
+        else *reinterpret_cast<f4a*>(p) = f4a{v.x, v.y, v.z, v.w};
     }
 }
 

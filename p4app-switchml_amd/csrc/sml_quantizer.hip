@@ -134,7 +134,7 @@ struct DequantArgs {
 // K4: dequantize the aggregated payload (PostprocessSingle, ppp.cc:197-251).
 // RCP (power-of-two W): multiply by the exact reciprocal instead of the IEEE
 // division — same bits (rcp_scale_pow2).
-template <int P, bool ALIGNED, bool BE, bool RCP>
+template <int P, bool ALIGNED, bool BE, bool RCP, bool NT = false>
 __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
     __shared__ float lut[256];
     if constexpr (RCP) build_rcp_lut(lut, a.W);
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
 #pragma unroll
             for (int u = 0; u < kU; u++) {
                 const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-                store4<ALIGNED>(a.out + idx, dequant_words<BE, RCP>(w[u], s[u]));
+                store4<ALIGNED, NT>(a.out + idx, dequant_words<BE, RCP>(w[u], s[u]));
             }
             continue;
         } else {
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
             const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
             if (!full && idx >= a.numel) continue;
             const f4 o = dequant_words<BE, RCP>(w[u], s[u]);
-            if (full) store4<ALIGNED>(a.out + idx, o);
+            if (full) store4<ALIGNED, NT>(a.out + idx, o);
             else store4_guarded(a.out + idx, o, idx, a.numel);
         }
     }
@@ -199,7 +199,7 @@ struct RoundTripArgs {
 // Fused dummy-backend round trip: PreprocessSingle -> ProcessPacket (x W) ->
 // PostprocessSingle for every packet of the slice in one HBM pass.  One tile
 // of one slice (blocks restart at the slice start, as in the reference).
-template <int P, bool ALIGNED, bool BE, bool RNE>
+template <int P, bool ALIGNED, bool BE, bool RNE, bool NT = false>
 __device__ __forceinline__ void roundtrip_tile(const RoundTripArgs& a, uint64_t t, const float* lut, int lane) {
     const bool pow2 = (a.W & (a.W - 1)) == 0;
     const uint32_t log2W = 31 - __builtin_clz(a.W);
@@ -255,19 +255,19 @@ __device__ __forceinline__ void roundtrip_tile(const RoundTripArgs& a, uint64_t 
             o = mkf4(dequantize1(q[0] * a.W, s), dequantize1(q[1] * a.W, s), dequantize1(q[2] * a.W, s),
                      dequantize1(q[3] * a.W, s));
         }
-        if (full) store4<ALIGNED>(a.out + idx, o);
+        if (full) store4<ALIGNED, NT>(a.out + idx, o);
         else if (idx < a.numel) store4_guarded(a.out + idx, o, idx, a.numel);
     }
 }
 
-template <int P, bool ALIGNED, bool BE, bool RNE>
+template <int P, bool ALIGNED, bool BE, bool RNE, bool NT = false>
 __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
     __shared__ float lut[256];
     build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves)
-        roundtrip_tile<P, ALIGNED, BE, RNE>(a, t, lut, lane);
+        roundtrip_tile<P, ALIGNED, BE, RNE, NT>(a, t, lut, lane);
 }
 
 // The fused round trip over a batch of slices (of one or several jobs) in ONE
@@ -424,32 +424,44 @@ static void launch_quant_b(bool be, bool rne, uint32_t P, uint32_t U, bool nts, 
     else launch_quant_r<ALIGNED, GLOBAL, false>(rne, P, U, nts, g, st, a);
 }
 
-template <bool ALIGNED, bool BE, bool RCP>
-static void launch_deq_p(uint32_t P, dim3 grid, hipStream_t st, const DequantArgs& a) {
+template <bool ALIGNED, bool BE, bool RCP, bool NT>
+static void launch_deq_pn(uint32_t P, dim3 grid, hipStream_t st, const DequantArgs& a) {
     switch (P) {
-        case 64:   k_dequantize<64, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_dequantize<128, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_dequantize<256, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_dequantize<512, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_dequantize<1024, ALIGNED, BE, RCP><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   k_dequantize<64, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_dequantize<128, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_dequantize<256, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_dequantize<512, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_dequantize<1024, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
     }
+}
+
+template <bool ALIGNED, bool BE, bool RCP>
+static void launch_deq_p(uint32_t P, bool nt, dim3 grid, hipStream_t st, const DequantArgs& a) {
+    if (nt) launch_deq_pn<ALIGNED, BE, RCP, true>(P, grid, st, a);
+    else launch_deq_pn<ALIGNED, BE, RCP, false>(P, grid, st, a);
 }
 
 template <bool ALIGNED, bool BE>
-static void launch_deq_w(uint32_t P, dim3 grid, hipStream_t st, const DequantArgs& a) {
-    if ((a.W & (a.W - 1)) == 0) launch_deq_p<ALIGNED, BE, true>(P, grid, st, a);
-    else launch_deq_p<ALIGNED, BE, false>(P, grid, st, a);
+static void launch_deq_w(uint32_t P, bool nt, dim3 grid, hipStream_t st, const DequantArgs& a) {
+    if ((a.W & (a.W - 1)) == 0) launch_deq_p<ALIGNED, BE, true>(P, nt, grid, st, a);
+    else launch_deq_p<ALIGNED, BE, false>(P, nt, grid, st, a);
+}
+
+template <bool ALIGNED, bool BE, bool RNE, bool NT>
+static void launch_rt_pn(uint32_t P, dim3 grid, hipStream_t st, const RoundTripArgs& a) {
+    switch (P) {
+        case 64:   k_roundtrip<64, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_roundtrip<128, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_roundtrip<256, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_roundtrip<512, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_roundtrip<1024, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
 }
 
 template <bool ALIGNED, bool BE, bool RNE>
-static void launch_rt_p(uint32_t P, dim3 grid, hipStream_t st, const RoundTripArgs& a) {
-    switch (P) {
-        case 64:   k_roundtrip<64, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_roundtrip<128, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_roundtrip<256, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_roundtrip<512, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_roundtrip<1024, ALIGNED, BE, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-    }
+static void launch_rt_p(uint32_t P, bool nt, dim3 grid, hipStream_t st, const RoundTripArgs& a) {
+    if (nt) launch_rt_pn<ALIGNED, BE, RNE, true>(P, grid, st, a);
+    else launch_rt_pn<ALIGNED, BE, RNE, false>(P, grid, st, a);
 }
 
 template <bool RNE>
@@ -464,9 +476,9 @@ static void launch_rtb_p(uint32_t P, dim3 grid, hipStream_t st, const RoundTripB
 }
 
 template <bool ALIGNED>
-static void launch_rt_a(bool be, bool rne, uint32_t P, dim3 g, hipStream_t st, const RoundTripArgs& a) {
-    if (be) { if (rne) launch_rt_p<ALIGNED, true, true>(P, g, st, a); else launch_rt_p<ALIGNED, true, false>(P, g, st, a); }
-    else    { if (rne) launch_rt_p<ALIGNED, false, true>(P, g, st, a); else launch_rt_p<ALIGNED, false, false>(P, g, st, a); }
+static void launch_rt_a(bool be, bool rne, bool nt, uint32_t P, dim3 g, hipStream_t st, const RoundTripArgs& a) {
+    if (be) { if (rne) launch_rt_p<ALIGNED, true, true>(P, nt, g, st, a); else launch_rt_p<ALIGNED, true, false>(P, nt, g, st, a); }
+    else    { if (rne) launch_rt_p<ALIGNED, false, true>(P, nt, g, st, a); else launch_rt_p<ALIGNED, false, false>(P, nt, g, st, a); }
 }
 
 }  // namespace sml
@@ -597,8 +609,9 @@ sml_status_t sml_dequantize(const int32_t* d_payload, const int8_t* d_exps, uint
     dim3 grid(grid_for_tiles(a.ntiles));
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_out), be = !(flags & SML_FLAG_PAYLOAD_LE);
-    if (al) { if (be) launch_deq_w<true, true>(packet_numel, grid, st, a); else launch_deq_w<true, false>(packet_numel, grid, st, a); }
-    else    { if (be) launch_deq_w<false, true>(packet_numel, grid, st, a); else launch_deq_w<false, false>(packet_numel, grid, st, a); }
+    const bool nt = 4 * numel >= g_nt_threshold.load(std::memory_order_relaxed);   // output plane past the Infinity Cache
+    if (al) { if (be) launch_deq_w<true, true>(packet_numel, nt, grid, st, a); else launch_deq_w<true, false>(packet_numel, nt, grid, st, a); }
+    else    { if (be) launch_deq_w<false, true>(packet_numel, nt, grid, st, a); else launch_deq_w<false, false>(packet_numel, nt, grid, st, a); }
     return launch_check();
 }
 
@@ -627,8 +640,9 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
     // unless the caller passed differently aligned buffers.
     const bool al = aligned16(d_in) && aligned16(d_out);
     const bool be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
-    if (al) launch_rt_a<true>(be, rne, packet_numel, grid, st, a);
-    else launch_rt_a<false>(be, rne, packet_numel, grid, st, a);
+    const bool nt = 4 * numel >= g_nt_threshold.load(std::memory_order_relaxed);   // output plane past the Infinity Cache
+    if (al) launch_rt_a<true>(be, rne, nt, packet_numel, grid, st, a);
+    else launch_rt_a<false>(be, rne, nt, packet_numel, grid, st, a);
     return launch_check();
 }
 

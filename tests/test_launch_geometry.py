@@ -128,3 +128,35 @@ def test_quantize_tile_slices_invariant(sw, P):
     finally:
         sw.set_quantize_tile_slices(0)
         sw.set_payload_nt_threshold((256 << 20) + 1)
+
+
+@pytest.mark.parametrize("P", [64, 256, 1024])
+def test_output_store_policy_invariant(sw, P):
+    """K1, K4 and the fused round trip with their output planes written
+    non-temporally (sml_set_payload_nt_threshold(0): what planes larger than
+    the Infinity Cache get) and with default-policy stores: the same bytes
+    as the oracle, aligned and 4-byte-offset slices."""
+    import torch
+    W, n = 3, 300_007
+    x_np = O.splitmix_normal(P + 77, n + 1)
+    xd = torch.from_numpy(x_np).cuda()
+    try:
+        for off in (0, 1):
+            xs, xn = xd[off:off + n], x_np[off:off + n]
+            q, e = O.quantize(xn, P, W), O.exponents(xn, P)
+            dq = O.dequantize(O.loopback_aggregate(q, W), e, n, P, W)
+            for nt in (0, 2 ** 64 - 1):
+                sw.set_payload_nt_threshold(nt)
+                payload, exps = sw.quantize_pack(xs, P, W)
+                agg = payload.clone()
+                sw.loopback_aggregate(agg, W)
+                out = torch.empty(n + 1, device="cuda")[off:off + n]
+                sw.dequantize(agg, exps, n, P, W, out=out)
+                rt = torch.empty(n + 1, device="cuda")[off:off + n]
+                sw.roundtrip_loopback(xs, P, W, out=rt)
+                torch.cuda.synchronize()
+                assert np.array_equal(payload.cpu().numpy().view(np.uint32), q), (off, nt)
+                assert np.array_equal(out.cpu().numpy().view(np.uint32), dq.view(np.uint32)), (off, nt)
+                assert np.array_equal(rt.cpu().numpy().view(np.uint32), dq.view(np.uint32)), (off, nt)
+    finally:
+        sw.set_payload_nt_threshold((256 << 20) + 1)
