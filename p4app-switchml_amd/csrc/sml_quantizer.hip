@@ -286,7 +286,7 @@ struct RoundTripBatchArgs {
     uint32_t xcd;
 };
 
-template <int P, bool RNE>
+template <int P, bool RNE, bool NT = false>
 __global__ __launch_bounds__(kBlockThreads) void k_roundtrip_batch(RoundTripBatchArgs a) {
     __shared__ float lut[256];
     build_lut(lut, a.W);
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip_batch(RoundTripBatc
         r.exps_out = nullptr;
         r.W = a.W;
         r.xcd = a.xcd;
-        roundtrip_tile<P, false, true, RNE>(r, t - t0, lut, lane);
+        roundtrip_tile<P, false, true, RNE, NT>(r, t - t0, lut, lane);
     }
 }
 
@@ -464,15 +464,21 @@ static void launch_rt_p(uint32_t P, bool nt, dim3 grid, hipStream_t st, const Ro
     else launch_rt_pn<ALIGNED, BE, RNE, false>(P, grid, st, a);
 }
 
-template <bool RNE>
-static void launch_rtb_p(uint32_t P, dim3 grid, hipStream_t st, const RoundTripBatchArgs& a) {
+template <bool RNE, bool NT>
+static void launch_rtb_pn(uint32_t P, dim3 grid, hipStream_t st, const RoundTripBatchArgs& a) {
     switch (P) {
-        case 64:   k_roundtrip_batch<64, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_roundtrip_batch<128, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_roundtrip_batch<256, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_roundtrip_batch<512, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_roundtrip_batch<1024, RNE><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   k_roundtrip_batch<64, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_roundtrip_batch<128, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_roundtrip_batch<256, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_roundtrip_batch<512, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_roundtrip_batch<1024, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
     }
+}
+
+template <bool RNE>
+static void launch_rtb_p(uint32_t P, bool nt, dim3 grid, hipStream_t st, const RoundTripBatchArgs& a) {
+    if (nt) launch_rtb_pn<RNE, true>(P, grid, st, a);
+    else launch_rtb_pn<RNE, false>(P, grid, st, a);
 }
 
 template <bool ALIGNED>
@@ -673,8 +679,12 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
                                       flags & SML_FLAG_ROUND_RNE, stream);
     const dim3 grid(grid_for_tiles(tiles));
     hipStream_t st = (hipStream_t)stream;
-    if (flags & SML_FLAG_ROUND_RNE) launch_rtb_p<true>(packet_numel, grid, st, a);
-    else launch_rtb_p<false>(packet_numel, grid, st, a);
+    // the outputs of the whole batch past the Infinity Cache: non-temporal stores
+    uint64_t out_bytes = 0;
+    for (uint32_t i = 0; i < a.nslices; i++) out_bytes += 4 * a.numel[i];
+    const bool nt = out_bytes >= g_nt_threshold.load(std::memory_order_relaxed);
+    if (flags & SML_FLAG_ROUND_RNE) launch_rtb_p<true>(packet_numel, nt, grid, st, a);
+    else launch_rtb_p<false>(packet_numel, nt, grid, st, a);
     return launch_check();
 }
 
