@@ -271,6 +271,32 @@ def quantize_pack(x, packet_numel: int = 256, num_workers: int = 1, global_exps=
     return payload, (global_exps if global_exps is not None else exps_out)
 
 
+def quantize_pack_launcher(x, packet_numel: int, num_workers: int, payload, exps_out=None, global_exps=None,
+                           flags: int = 0, stream=None):
+    """A zero-argument callable that launches sml_quantize_pack on these
+    tensors: every argument checked and converted once, so a loop over the
+    same bucket (a training step's gradient bucket, the bench's steps) pays
+    one C call per launch instead of the wrapper's tensor checks.  The
+    tensors must stay alive while the callable is used."""
+    torch = _torch()
+    B = num_blocks(x.numel(), packet_numel)
+    if payload.numel() != B * packet_numel:
+        raise ValueError(f"payload must hold B*P = {B * packet_numel} words")
+    if exps_out is not None and exps_out.numel() != B:
+        raise ValueError(f"exps_out must hold B = {B} bytes")
+    args = (_dev(x, torch.float32, "x"), x.numel(), packet_numel, num_workers,
+            None if global_exps is None else _dev(global_exps, torch.int8, "global_exps"),
+            _dev(payload, torch.int32, "payload"),
+            None if exps_out is None else _dev(exps_out, torch.int8, "exps_out"), flags, _stream(stream, x))
+    fn = lib().sml_quantize_pack
+
+    def launch():
+        s = fn(*args)
+        if s != SML_OK:
+            raise SwitchMLError("sml_quantize_pack", s)
+    return launch
+
+
 def dequantize(payload, exps, numel: int, packet_numel: int = 256, num_workers: int = 1,
                out=None, flags: int = 0, stream=None):
     torch = _torch()

@@ -339,3 +339,31 @@ def test_beyond_2_31_elements_sampled_blocks(cuda):
         assert float_bits_equal_nan_ok(host(out[k * P:k * P + n]), ref), k
     del x, payload, exps, out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("P", [64, 256, 1024])
+def test_quantize_pack_launcher(cuda, P):
+    """switchml_amd.quantize_pack_launcher (one prepared C call per launch, the
+    bench's step): the same planes as the oracle, twice in a row, and K3 with
+    global exponents through it."""
+    import torch
+    n, W = 100_003, 3
+    x = O.splitmix_normal(P + 9, n)
+    xd = torch.from_numpy(x).cuda()
+    B = sw().num_blocks(n, P)
+    pl = torch.empty(B * P, dtype=torch.int32, device="cuda")
+    ex = torch.empty(B, dtype=torch.int8, device="cuda")
+    go = sw().quantize_pack_launcher(xd, P, W, pl, exps_out=ex)
+    for _ in range(2):
+        pl.zero_()
+        go()
+        torch.cuda.synchronize()
+        assert bits_equal(host(pl), O.quantize(x, P, W))
+        assert np.array_equal(host(ex), O.exponents(x, P))
+    g = torch.from_numpy(O.exponents(x, P) + 1).cuda()
+    k3 = sw().quantize_pack_launcher(xd, P, W, pl, global_exps=g)
+    k3()
+    torch.cuda.synchronize()
+    assert bits_equal(host(pl), O.quantize(x, P, W, global_exps=O.exponents(x, P) + 1))
+    with pytest.raises(ValueError):
+        sw().quantize_pack_launcher(xd, P, W, pl[:-1])
