@@ -13,6 +13,7 @@ tools/ab/ (sources copied and patched there; tools/ab/ is git-ignored):
   rx_vec    rx apply reads its state words with vector (broadcast) loads
   rx_vec_w8 rx_vec held to 8 waves per SIMD
   k1_ntstore K1's payload stores non-temporal (tools/ab_store_size.py)
+  rx_ntout  rx apply's fp32 output stores non-temporal
 Timed by tools/ab_frames.py on the GPU (AB_NOCHECK=1 when tx_nohdr is in)."""
 import os
 import shutil
@@ -85,6 +86,7 @@ def build(name, patches=()):
 TXK = "__global__ __launch_bounds__(kBlockThreads) void k_quantize_frames(FrameArgs a) {"
 RXK = "__global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {"
 W8 = "__attribute__((amdgpu_waves_per_eu(8, 8))) "
+RXO = "            if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o[u];"
 RXS = "        if constexpr (kChunksPerFrame >= kWave) {"
 SWK = "__global__ __launch_bounds__(kBlockThreads) void k_switch_aggregate(SwitchArgs a) {"
 
@@ -93,6 +95,9 @@ VARIANTS = {"tx_base": (), "tx_bf": ((PAYLOAD, PAYLOAD_BF),), "tx_nohdr": ((HDR,
             "fr_w8": ((TXK, TXK.replace("__global__ ", "__global__ " + W8)),
                       (RXK, RXK.replace("__global__ ", "__global__ " + W8))),
             "tx_w8": ((TXK, TXK.replace("__global__ ", "__global__ " + W8)),),
+            # rx apply: non-temporal fp32 output stores
+            "rx_ntout": ((RXO, RXO.replace("*reinterpret_cast<f4*>(p) = o[u];",
+                                            "__builtin_nontemporal_store(o[u], reinterpret_cast<f4*>(p));")),),
             # K1: non-temporal payload stores (sml_device.h store_payload)
             "k1_ntstore": (("sml_device.h", "__device__ __forceinline__ void store_payload(u4* dst, u4 q) { *dst = q; }",
                             "__device__ __forceinline__ void store_payload(u4* dst, u4 q) { __builtin_nontemporal_store(q, dst); }"),),
