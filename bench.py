@@ -74,9 +74,10 @@ def parse(argv=None):
                          "measured, with a failure, and exits 1 (a hang would otherwise print nothing)")
     ap.add_argument("--no-plugin", action="store_true",
                     help="N > 1: skip the configs4_plugin field (ResNet-50 buckets through the CollNet table per rank)")
-    ap.add_argument("--buckets", type=int, default=1,
-                    help="distinct input buckets (and output planes) the timed steps cycle through: 1 = one "
-                         "resident bucket (the headline); >= 4 streams past the 256 MiB Infinity Cache (cold HBM)")
+    ap.add_argument("--buckets", type=int, default=4,
+                    help="distinct input buckets (and output planes) the timed steps cycle through: 4 (default) "
+                         "streams 2 GiB past the 256 MiB Infinity Cache, so the headline is an HBM-proper rate; "
+                         "1 = one resident bucket (HBM + Infinity Cache; reported as side.resident)")
     ap.add_argument("--grid-limit", type=int, default=0, help="workgroups per launch (0 = one per 4 tiles)")
     ap.add_argument("--xcd-chunk", type=int, default=64,
                     help="workgroups per contiguous run on one XCD (0 = plain blockIdx order)")
@@ -141,6 +142,69 @@ def host_cores():
         pass
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
     return aff, quota, share
+
+
+BENCH_SEED0 = 4242   # bucket b of a run holds bench_bucket(4242 + b, ...) (tests/golden/make_bench_digests.py)
+DIGESTS_BENCH = os.path.join(ROOT, "tests", "golden", "digests_bench.json")
+
+
+def _u64(c):
+    """A 64-bit constant as the int64 with the same bits (torch has no uint64 arithmetic)."""
+    c &= (1 << 64) - 1
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def _lsr(torch, z, s):
+    """Logical right shift of int64 bit patterns."""
+    return (z >> s) & ((1 << (64 - s)) - 1)
+
+
+def bench_bucket(torch, seed, off, n, device):
+    """Gradient-like fp32 from integer arithmetic only, elements [off, off+n)
+    of a job: the same bits on every host and device.  Restates oracle.py's
+    splitmix_grad (a signed 24-bit mantissa from splitmix64, scaled by
+    2^-(24+k), k in 0..15 varying per 256-block, so block exponents differ)
+    over the GLOBAL element index, so a rank's FIFO slice of a job is exactly
+    that slice of the job; int64 products wrap like the uint64 ones."""
+    out = torch.empty(n, dtype=torch.float32, device=device)
+    step = 1 << 25
+    for a in range(0, n, step):          # bounded temporaries
+        m = min(step, n - a)
+        i = torch.arange(off + a, off + a + m, dtype=torch.int64, device=device)
+        z = i * _u64(0xBF58476D1CE4E5B9) + _u64(seed * 0x9E3779B97F4A7C15)
+        z = (z ^ _lsr(torch, z, 31)) * _u64(0x94D049BB133111EB)
+        z = z ^ _lsr(torch, z, 29)
+        mant = _lsr(torch, z, 40) - (1 << 23)                       # [-2^23, 2^23)
+        k = ((i >> 8) * 7 + (z & 1)) % 16
+        scale = ((127 - 24 - k).to(torch.int32) << 23).view(torch.float32)   # 2^-(24+k), exact
+        out[a:a + m] = mant.to(torch.float32) * scale
+    return out
+
+
+def planes_sha256(torch, exps, payload, numel, P):
+    """SHA-256 of an exponent plane and the first numel words of a payload
+    plane (host copies; outside any timed region)."""
+    import hashlib
+    e = exps.cpu().numpy().tobytes()
+    q = payload[:numel].cpu().numpy().tobytes()
+    return {"exps": hashlib.sha256(e).hexdigest(), "payload": hashlib.sha256(q).hexdigest()}
+
+
+def expected_digests(job_numel, world, rank, N, P, nb):
+    """The committed digests of this rank's buckets, or None when the run's
+    shape has none (other packet size / bucket size / bucket count)."""
+    try:
+        with open(DIGESTS_BENCH) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if P != d["packet_numel"] or nb > d["buckets"]:
+        return None
+    if job_numel == 0 and N == d["bucket_numel"]:
+        return d["bucket_T1"][:nb]
+    if job_numel == d["job_numel"] and f"T{world}" in d["job"]:
+        return [d["job"][f"T{world}"][b][rank] for b in range(nb)]
+    return None
 
 
 def cpu_baseline(numel, P, budget_s):
@@ -260,9 +324,10 @@ def main():
 
     P = args.packet_numel
     job_numel = args.job_numel if args.job_numel >= 0 else (CFG3_JOB_NUMEL if world > 1 else 0)
+    off = 0
     if job_numel:
         # configs[3]: one job sharded over the ranks, slice g -> GPU g (fifo_scheduler.cc:93-109)
-        N = sw.fifo_slice(job_numel, world, rank)[1]
+        off, N = sw.fifo_slice(job_numel, world, rank)
         total_alg = sum(8 * n + sw.num_blocks(n, P)
                         for n in (sw.fifo_slice(job_numel, world, r)[1] for r in range(world)))
     else:
@@ -274,7 +339,9 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
     nb = max(1, args.buckets)
-    xs = [torch.randn(N, dtype=torch.float32, device=dev, generator=gen) for _ in range(nb)]
+    # bucket b = elements [off, off + N) of the job bench_bucket(4242 + b, .):
+    # integer-exact, so the timed planes can be checked against committed digests
+    xs = [bench_bucket(torch, BENCH_SEED0 + b, off, N, dev) for b in range(nb)]
     pls = [torch.empty(B * P, dtype=torch.int32, device=dev) for _ in range(nb)]
     exs = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nb)]
     x, payload, exps = xs[0], pls[0], exs[0]
@@ -346,15 +413,26 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms_max = float(t[0]), float(t[1])
 
-    # sanity: the timed output is the HIP kernel's and it is deterministic
-    ok = bool(torch.equal(exps[:4].cpu(), sw.exponents(x[:4 * P], P).cpu()))
-    ok_t = torch.tensor([int(ok)], dtype=torch.int32, device=dev)
+    # self-check: the planes the TIMED launches left (the last launch on each
+    # bucket, the kernel instance and knobs of this run) hashed and compared
+    # with the oracle's digests of the same inputs (tests/golden/digests_bench.json)
+    want = expected_digests(job_numel, world, rank, N, P, nb)
+    if want is None:
+        ok, check_note = True, "no committed digest for this shape: not checked"
+        checked = 0
+    else:
+        got = [planes_sha256(torch, exs[b], pls[b], N, P) for b in range(nb)]
+        bad = [b for b in range(nb) if got[b] != want[b]]
+        ok, checked = not bad, nb
+        check_note = ("timed exponent + BE payload planes of every bucket == tests/golden/digests_bench.json"
+                      if ok else f"buckets {bad} differ from tests/golden/digests_bench.json")
+    ok_t = torch.tensor([int(ok), checked], dtype=torch.int32, device=dev)
     if world > 1:
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
-    ok = bool(ok_t.item())
+    ok, checked = bool(ok_t[0].item()), int(ok_t[1].item())
     del xs, pls, exs, x, payload, exps
 
-    failures = [] if ok else ["self_check: K1 exponent plane != K2 exponents"]
+    failures = [] if ok else ["self_check: " + check_note]
     side, fields, extra = {}, {}, {}
 
     def emit():
@@ -384,7 +462,8 @@ def main():
             "scaling": "strong" if job_numel else "weak",
             "vs_baseline": None,
             "dtype": "f32->i32",
-            "data": "synthetic N(0,1) fp32 (torch.randn on device, seed 42+rank)",
+            "data": ("synthetic gradient-like fp32 generated on device from integers only (bench_bucket: "
+                     "splitmix64 24-bit mantissas x 2^-(24..39), seed 4242 + bucket, global element index)"),
             "config": {
                 "workload": workload,
                 "job_numel": job_numel or world * N,
@@ -409,11 +488,14 @@ def main():
                 "kernel": f"sml::k_quantize_pack<{P},aligned,fused,BE,half-away>",
             },
             "self_check": ok,
+            "self_check_detail": {"what": check_note, "buckets_checked_min_over_ranks": checked},
         }
-        if "cold_hbm" in side:
-            c = side["cold_hbm"]
-            line["roofline"]["frac_cold"] = c["frac"]
-            line["roofline"]["traffic_cold"] = load_traffic(args.numel, P, "quantize_pack_cold")
+        if nb > 1:
+            line["roofline"]["note"] = (f"steps cycle {nb} distinct buckets + planes ({nb * (8 * N + B) >> 20} MiB "
+                                        "per GPU, past the 256 MiB Infinity Cache): an HBM-proper rate")
+        if "resident" in side:
+            line["roofline"]["frac_resident"] = side["resident"]["frac"]
+            line["roofline"]["traffic_resident"] = load_traffic(args.numel, P, "quantize_pack")
         line.update(fields)
         if side:
             line["side"] = side
@@ -427,7 +509,10 @@ def main():
 
     side_cpu = {}
     if world == 1 and not args.no_side:
-        side["cold_hbm"] = cold_measure(sw, torch, args.numel, P, stream)
+        if nb > 1:
+            side["resident"] = bucket_measure(sw, torch, args.numel, P, stream, nbuf=1)
+        else:
+            side["cold_hbm"] = bucket_measure(sw, torch, args.numel, P, stream, nbuf=4)
         side["configs3_1gpu"] = job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev)
     if world > 1 and not args.no_side:
         side["weak_256MiB_per_gpu"] = weak_measure(sw, torch, dist, args.numel, P, stream, dev, world)
@@ -507,10 +592,12 @@ def time_launches(torch, fn, stream, reps, warm=3):
     return a.elapsed_time(b) / reps * 1e-3
 
 
-def cold_measure(sw, torch, N, P, stream, nbuf=4, reps=200):
+def bucket_measure(sw, torch, N, P, stream, nbuf=4, reps=200):
     """K1 with the steps cycling through nbuf distinct 256 MiB buckets and
-    output planes (nbuf x 512 MiB >> the 256 MiB Infinity Cache): every launch
-    streams from / to HBM proper.  The headline re-reads one resident bucket."""
+    output planes.  nbuf = 4 (nbuf x 512 MiB >> the 256 MiB Infinity Cache):
+    every launch streams from / to HBM proper (the headline's own setting).
+    nbuf = 1: one bucket re-read every step, partly served by the Infinity
+    Cache — reported as side.resident, labelled so."""
     B = sw.num_blocks(N, P)
     g = torch.Generator(device=stream.device)
     g.manual_seed(4242)
@@ -527,9 +614,12 @@ def cold_measure(sw, torch, N, P, stream, nbuf=4, reps=200):
     settle(fn, 30.0)
     t = time_launches(torch, fn, stream, reps)
     alg = 8 * N + B
+    note = ("K1 cycling distinct buckets and planes: HBM-proper rate (no Infinity Cache reuse)" if nbuf > 1 else
+            "K1 re-reading ONE resident bucket: HBM + Infinity Cache (part of the bucket is served by the "
+            "256 MiB MALL), not an HBM fraction")
     return {"buckets": nbuf, "bucket_MiB": N * 4 >> 20, "kernel_ms": round(t * 1e3, 5),
             "achieved_GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
-            "note": "K1 cycling distinct buckets and planes: HBM-proper rate (no Infinity Cache reuse)"}
+            "note": note}
 
 
 def job_measure(sw, torch, job_numel, P, stream, dev, reps=50):
@@ -660,10 +750,11 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
             torch.cuda.synchronize()
             err = (out - ref).abs()
             within = bool((err <= tol).all().item())
+            touts = [torch.empty_like(x) for _ in range(reps)]   # every timed call keeps its result
             dist.barrier()
             t0 = time.perf_counter()
-            for _ in range(reps):
-                ar(x, out)
+            for i in range(reps):
+                ar(x, touts[i])
             torch.cuda.synchronize()
             tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -675,15 +766,20 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
             if hasattr(ar, "close"):
                 ar.close()
             del ar
-            ok_t = torch.tensor([int(within)], dtype=torch.int32, device=dev)
+            # planes are reused call after call: every timed call must give the first call's bits
+            same = all(bool(torch.equal(o, out)) for o in touts)
+            del touts
+            ok_t = torch.tensor([int(within), int(same)], dtype=torch.int32, device=dev)
             dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+            same = bool(ok_t[1].item())
             outs[name] = out
             res[name] = {"workers": W, "numel_per_worker": n, "packet_numel": P,
                          "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * n / t / 1e9, 2),
                          "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
                          "xgmi_bound_ms": round(bound_s * 1e3, 3),
                          "frac_of_xgmi_bound": round(bound_s / t, 4),
-                         "within_quantization_bound": bool(ok_t.item()),
+                         "within_quantization_bound": bool(ok_t[0].item()),
+                         "timed_calls_equal_first": same,
                          "max_abs_err_vs_fp32_allreduce": float(err.max().item()),
                          "pipeline": pipe, "phases_ms": phases}
             del err
@@ -707,23 +803,27 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
         torch.cuda.synchronize()
         err = (out - ref).abs()
         within = bool((err <= tol).all().item())
+        touts = [torch.empty_like(x) for _ in range(reps)]
         dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(reps):
-            C.allreduce(x, out)
+        for i in range(reps):
+            C.allreduce(x, touts[i])
         torch.cuda.synchronize()
         tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt[0])
         C.stop()
-        ok_t = torch.tensor([int(within)], dtype=torch.int32, device=dev)
+        same = all(bool(torch.equal(o, out)) for o in touts)
+        del touts
+        ok_t = torch.tensor([int(within), int(same)], dtype=torch.int32, device=dev)
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        same = bool(ok_t[1].item())
         outs["xgmi_switch"] = out
         res["xgmi_switch"] = {"workers": W, "numel_per_worker": n, "packet_numel": P,
                               "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * n / t / 1e9, 2),
                               "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
                               "xgmi_bound_ms": round(bound_s * 1e3, 3), "frac_of_xgmi_bound": round(bound_s / t, 4),
-                              "within_quantization_bound": bool(ok_t.item()),
+                              "within_quantization_bound": bool(ok_t[0].item()), "timed_calls_equal_first": same,
                               "max_abs_err_vs_fp32_allreduce": float(err.max().item()), "pipeline": pipe}
         del err
     except Exception as e:  # noqa: BLE001
@@ -742,7 +842,7 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
         if "error" not in r:
             same = all(eqs.values()) if name == "switchsim" else eqs.get(name)
             r["bit_equal_to_switchsim" if name != "switchsim" else "bit_equal_to_other_paths"] = same
-            r["verified"] = bool(r["within_quantization_bound"] and same)
+            r["verified"] = bool(r["within_quantization_bound"] and same and r["timed_calls_equal_first"])
         r["xgmi_link_GBps_assumed"] = XGMI_LINK_GBPS
     res["p2p_switch"]["status"] = "experimental (first cross-GPU run is the driver's multi-GPU bench)"
     return res

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define SML_ABI_VERSION 1
+#define SML_ABI_VERSION 2   /* 2: flags on sml_switch_exps / sml_copy_segments, sml_release_to_peers */
 
 typedef enum {
     SML_OK = 0,
@@ -63,6 +63,14 @@ typedef enum { SML_FLOAT32 = 0, SML_INT32 = 1 } sml_data_type_t;
                                        half-away tail; out-of-range -> INT32_MIN.
                                        PARITY UNPINNED (VCL is un-vendored). Default is the
                                        VCL=0 scalar path: roundf half-away-from-zero. */
+#define SML_FLAG_PEER_PLANES  0x4u  /* the switch entry points (sml_switch_aggregate,
+                                       sml_switch_exps, sml_copy_segments): some input
+                                       planes were written by OTHER GPUs (peers' HBM mapped
+                                       over xGMI).  Every workgroup performs a system-scope
+                                       acquire before its first load, so no copy of a peer
+                                       line this GPU cached before the peer rewrote it is
+                                       read; the peer must have run sml_release_to_peers
+                                       after its writes (memory model). */
 
 int sml_abi_version(void);
 const char* sml_status_string(sml_status_t s);
@@ -174,7 +182,7 @@ sml_status_t sml_switch_aggregate(const int32_t* const* d_payloads, const int8_t
  * max_w (int8) d_exps[w][k], k < num_blocks — W planes of num_blocks bytes
  * (local or mapped peers' planes; HOST array of DEVICE pointers). */
 sml_status_t sml_switch_exps(const int8_t* const* d_exps, uint16_t num_workers, uint64_t num_blocks,
-                             int8_t* d_exps_out, void* stream);
+                             int8_t* d_exps_out, uint32_t flags, void* stream);
 
 /* Copy num_words 32-bit words (any 4-byte alignment; either side may be a
  * peer's mapped plane or pinned host memory): the all-gather step of the
@@ -187,7 +195,53 @@ sml_status_t sml_copy_words(const void* d_src, void* d_dst, uint64_t num_words, 
  * multicast: the tiles are dealt round-robin over the segments, so W peers'
  * shards come over their xGMI links at the same time, not one after another. */
 sml_status_t sml_copy_segments(const void* const* d_srcs, void* const* d_dsts, const uint64_t* num_words,
-                               uint32_t num_segments, void* stream);
+                               uint32_t num_segments, uint32_t flags, void* stream);
+
+/* The writer's half of a hand-off to other GPUs: a system-scope release on
+ * every XCD of the stream's device (each XCD's L2 writes its dirty lines back
+ * to HBM), ordered after the work already on `stream`.  The in-node switch
+ * runs it after the kernels that write planes peers will read, before the
+ * stream synchronization that precedes the workers' barrier; the readers'
+ * kernels then take SML_FLAG_PEER_PLANES (the acquire).  One small launch. */
+sml_status_t sml_release_to_peers(void* stream);
+
+/* ---- per-packet calls, a burst per launch ---------------------------------
+ * PreprocessSingle / PostprocessSingle (ppp.cc:69-192, 194-299) for up to
+ * SML_MAX_BURST packets of one job slice in ONE launch: the DPDK worker's rx
+ * burst (PostprocessSingle per received packet, dpdk_worker_thread.cc:300-345)
+ * and the tx burst it refills (ReusePacket -> PreprocessSingle of pkt_id + b,
+ * dpdk_worker_thread_utils.inc:134,177), or an RDMA worker's completions
+ * (rdma_worker_thread.cc:244,356).  entries[i] / extras[i] are packet i's
+ * payload words and 2-byte extra-info slot, anywhere the DEVICE can address
+ * (HBM, or pinned host memory such as a NIC's buffer pool) — read / written in
+ * place.  Packet q of a FLOAT32 slice: preprocess writes block q - b's
+ * quantized big-endian words (q >= b; only the block's real words, a partial
+ * block's tail stays as it was) and block q's exponent into byte 0 of the
+ * extra slot (q < B); postprocess dequantizes block q - b into `out` (q >= b)
+ * and keeps the packet's exponent byte as block q's received exponent in
+ * recv_exps[q] (q < B).  INT32 slices: byte swaps, packet q = block q.
+ * recv_exps: DEVICE array of B int8 owned by the caller for the slice.  Bit-
+ * identical to the per-packet calls in the reference's order; packet ids of a
+ * burst are distinct and never include both q and q + b (the reference sends
+ * q + b only after receiving q).  Flags: SML_FLAG_ROUND_RNE. */
+#define SML_MAX_BURST 64
+typedef struct {
+    const float* in;          /* the job slice (int32 words for INT32) */
+    float* out;
+    uint64_t numel;
+    uint32_t packet_numel;    /* P */
+    uint16_t num_workers;     /* W */
+    uint16_t data_type;       /* sml_data_type_t */
+    uint64_t batch_num_ltus;  /* b (FLOAT32: the extra batch) */
+    int8_t* recv_exps;
+    uint32_t count;
+    uint32_t flags;
+    uint64_t pkt_ids[SML_MAX_BURST];
+    void* entries[SML_MAX_BURST];
+    void* extras[SML_MAX_BURST];
+} sml_packet_burst;
+sml_status_t sml_preprocess_burst(const sml_packet_burst* burst, void* stream);
+sml_status_t sml_postprocess_burst(const sml_packet_burst* burst, void* stream);
 
 /* Plane sharing for the peer-to-peer switch: export the allocation holding
  * d_ptr as an IPC handle of sml_ipc_handle_bytes() bytes plus d_ptr's byte

@@ -89,9 +89,10 @@ PacketMem packet_mem(void* p) {
 
 // PreprocessSingle — ppp.cc:69-192.  One kernel per half (quantize of block
 // ltu_id - b, exponent of block ltu_id), writing the packet buffer directly
-// when the device can address it.  Device-memory packets are stream-ordered
-// on stream() (no host sync); a host-memory packet is complete on return, as
-// the reference's is, because the caller hands it to the NIC next.
+// when the device can address it.  The packet is complete on return, as the
+// reference's is, because the caller hands it to the NIC next; only a caller
+// that opted into stream order (SetStreamOrdered) with a device-memory packet
+// skips the host sync.
 void HipExponentQuantizerPPP::PreprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
     const Tensor& s = job_slice_->slice;
     const uint32_t P = (uint32_t)ltu_numel_;
@@ -134,7 +135,7 @@ void HipExponentQuantizerPPP::PreprocessSingle(uint64_t ltu_id, void* entries_pt
     } else {
         throw SwitchMLFatal("unsupported data type");
     }
-    if (sync) hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    if (sync || !stream_ordered_) hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
 // PostprocessSingle — ppp.cc:194-299.  The dequantize kernel reads the packet
@@ -182,7 +183,58 @@ void HipExponentQuantizerPPP::PostprocessSingle(uint64_t ltu_id, void* entries_p
     } else {
         throw SwitchMLFatal("unsupported data type");
     }
-    if (sync) hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+    if (sync || !stream_ordered_) hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+// A burst of per-LTU calls as one launch per SML_MAX_BURST packets.  The
+// buffers of a burst come from one pool (a ring, a NIC's mbuf pool), so one
+// pointer query per burst decides where they live: HBM or pinned host memory
+// go to the kernel in place (pinned host memory at its device address — the
+// same offset applies to every buffer of the pool); pageable memory takes the
+// per-packet path, which stages.
+void HipExponentQuantizerPPP::burst(bool pre, uint32_t n, const uint64_t* ltu_ids, void* const* entries,
+                                   void* const* extras) {
+    if (n == 0) return;
+    const Tensor& s = job_slice_->slice;
+    ensure_single_buffers();
+    const PacketMem m = packet_mem(entries[0]);
+    if (!m.dev) {
+        for (uint32_t i = 0; i < n; i++)
+            pre ? PreprocessSingle(ltu_ids[i], entries[i], extras ? extras[i] : nullptr)
+                : PostprocessSingle(ltu_ids[i], entries[i], extras ? extras[i] : nullptr);
+        return;
+    }
+    const intptr_t delta = static_cast<char*>(m.dev) - static_cast<char*>(entries[0]);
+    sml_packet_burst b{};
+    b.in = static_cast<const float*>(s.in_ptr);
+    b.out = static_cast<float*>(s.out_ptr);
+    b.numel = s.numel;
+    b.packet_numel = (uint32_t)ltu_numel_;
+    b.num_workers = config_.general_.num_workers;
+    b.data_type = s.data_type == FLOAT32 ? SML_FLOAT32 : SML_INT32;
+    b.batch_num_ltus = s.data_type == FLOAT32 ? batch_num_ltus_ : 0;
+    b.recv_exps = d_recv_exps_;
+    for (uint32_t i0 = 0; i0 < n; i0 += SML_MAX_BURST) {
+        b.count = std::min<uint32_t>(SML_MAX_BURST, n - i0);
+        for (uint32_t i = 0; i < b.count; i++) {
+            b.pkt_ids[i] = ltu_ids[i0 + i];
+            b.entries[i] = static_cast<char*>(entries[i0 + i]) + delta;
+            b.extras[i] = extras && extras[i0 + i] ? static_cast<char*>(extras[i0 + i]) + delta : nullptr;
+        }
+        check(pre ? sml_preprocess_burst(&b, stream_) : sml_postprocess_burst(&b, stream_),
+              pre ? "sml_preprocess_burst" : "sml_postprocess_burst");
+    }
+    if (m.host || !stream_ordered_) hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+}
+
+void HipExponentQuantizerPPP::PreprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries,
+                                              void* const* extras) {
+    burst(true, n, ltu_ids, entries, extras);
+}
+
+void HipExponentQuantizerPPP::PostprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries,
+                                               void* const* extras) {
+    burst(false, n, ltu_ids, entries, extras);
 }
 
 void HipExponentQuantizerPPP::ExponentsBulk(void* exps_plane) {

@@ -6,7 +6,8 @@
 //   * per-LTU calls keep the reference's packet semantics exactly (packet p
 //     carries the exponent of block p, p < B, and the payload of block p - b,
 //     p >= b; the scale of block k comes from the exponent received with
-//     packet k) — one small kernel launch per call, for packet-driven callers;
+//     packet k) — one small kernel launch per call, or per BURST of packets
+//     (a DPDK rx / tx burst) for packet-driven callers;
 //   * bulk calls process the whole slice in one launch (the fast path).
 // The job slice's in_ptr / out_ptr must be DEVICE memory (the loopback
 // backend stages host tensors); entries / extra-info pointers of the
@@ -31,6 +32,18 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     void PostprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) override;
     void CleanupJobSlice() override;
 
+    // One launch per burst of up to SML_MAX_BURST packets (sml_preprocess_burst
+    // / sml_postprocess_burst): the packet buffers must be device-addressable
+    // (HBM or pinned host memory); pageable ones take the per-packet path.
+    void PreprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras) override;
+    void PostprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras) override;
+
+    // A per-LTU / burst call returns with its packet complete, as the
+    // reference's does (the caller hands a packet to the NIC next).  A caller
+    // whose packets stay in HBM and are consumed on stream() (the loopback
+    // backend's device ring) may opt out of the host sync.
+    void SetStreamOrdered(bool on) { stream_ordered_ = on; }
+
     void ExponentsBulk(void* exps_plane) override;
     void PreprocessBulk(void* payload_plane, void* exps_plane, const void* global_exps, bool payload_le) override;
     void PostprocessBulk(const void* payload_plane, const void* global_exps, bool payload_le) override;
@@ -43,6 +56,7 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
   private:
     void check(int status, const char* what) const;
     void ensure_single_buffers();
+    void burst(bool pre, uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras);
 
     JobSlice* job_slice_ = nullptr;
     uint64_t total_main_num_ltus_ = 0;  // B
@@ -55,6 +69,7 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     uint64_t d_recv_exps_cap_ = 0;
     int32_t* d_stage_ = nullptr;
     int8_t* d_stage_exp_ = nullptr;
+    bool stream_ordered_ = false;
 };
 
 }  // namespace switchml

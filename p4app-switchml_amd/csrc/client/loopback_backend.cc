@@ -113,21 +113,43 @@ void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerStat
         std::memset(ring, 0, b * P * 4);
     }
     // ProcessPacket (every entry of the packet x W) on the CPU for a host ring,
-    // as dummy_backend.cc:72-84 does, on the device for an HBM ring
+    // as dummy_backend.cc:72-84 does, on the device for an HBM ring.
+    //
+    // The reference handles one packet per loop trip: packet p comes back,
+    // ProcessPacket, PostprocessSingle(p), PreprocessSingle(p + b) into the
+    // same ring slot.  Slots are independent, so the packets of one pass over
+    // the ring (slots s0 .. s0 + w - 1, w <= b) go as bursts — the way a DPDK
+    // worker handles an rx burst and refills a tx burst — with the same calls
+    // per slot in the same order: ProcessPacket(window), PostprocessBurst,
+    // PreprocessBurst.  A device ring stays stream-ordered (no host sync per
+    // burst); a host ring completes each burst before the CPU touches it.
     const uint16_t W = cfg.general_.num_workers;
-    for (uint64_t p = 0; p < b; p++) ppp.PreprocessSingle(p, ring + (p % b) * P, extra + (p % b) * 2);
-    for (uint64_t p = 0; p < total; p++) {
-        int32_t* ent = ring + (p % b) * P;
-        uint8_t* ex = extra + (p % b) * 2;
-        if (cfg.backend_.dummy.process_packets && where == "device")
-            sml_ok(sml_loopback_aggregate(ent, P, W, 0, ppp.stream()), "sml_loopback_aggregate");
-        else if (cfg.backend_.dummy.process_packets)
-            for (uint64_t i = 0; i < P; i++)
-                ent[i] = (int32_t)__builtin_bswap32(__builtin_bswap32((uint32_t)ent[i]) * (uint32_t)W);
-        ppp.PostprocessSingle(p, ent, ex);
-        const uint64_t np = p + b;
-        if (np < total) ppp.PreprocessSingle(np, ent, ex);
+    const bool dev_ring = where == "device";
+    ppp.SetStreamOrdered(dev_ring);
+    std::vector<uint64_t> ids(b), nids(b);
+    std::vector<void*> ents(b), exs(b);
+    for (uint64_t p = 0; p < b; p++) {
+        ids[p] = p;
+        ents[p] = ring + p * P;
+        exs[p] = extra + p * 2;
     }
+    ppp.PreprocessBurst((uint32_t)b, ids.data(), ents.data(), exs.data());
+    for (uint64_t p0 = 0; p0 < total; p0 += b) {
+        const uint64_t w = std::min<uint64_t>(b, total - p0);   // p0 % b == 0: slots 0 .. w - 1
+        if (cfg.backend_.dummy.process_packets && dev_ring)
+            sml_ok(sml_loopback_aggregate(ring, w * P, W, 0, ppp.stream()), "sml_loopback_aggregate");
+        else if (cfg.backend_.dummy.process_packets)
+            for (uint64_t i = 0; i < w * P; i++)
+                ring[i] = (int32_t)__builtin_bswap32(__builtin_bswap32((uint32_t)ring[i]) * (uint32_t)W);
+        uint32_t nn = 0;
+        for (uint64_t s = 0; s < w; s++) {
+            ids[s] = p0 + s;
+            if (p0 + s + b < total) nids[nn++] = p0 + s + b;
+        }
+        ppp.PostprocessBurst((uint32_t)w, ids.data(), ents.data(), exs.data());
+        ppp.PreprocessBurst(nn, nids.data(), ents.data(), exs.data());   // slots 0 .. nn - 1
+    }
+    ppp.SetStreamOrdered(false);
 }
 
 uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, JobSlice& js, XgmiSwitch* xs,
@@ -549,7 +571,12 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
         // (dummy_worker_thread.cc:87-93)
         const bool work = js.slice.numel > 0 && !g.instant_job_completion;
         bool ok = !work || ppp != nullptr;
-        if (work && tid == config_.backend_.dummy.fail_worker_thread) ok = false;  // injected fault
+        if (work && tid == config_.backend_.dummy.fail_worker_thread) {   // injected fault
+            ok = false;
+            // with the in-node switch the fault fails the exchange for every
+            // worker (as a real mid-exchange failure does), not a barrier wait
+            if (xgmi_) xgmi_->Poison();
+        }
         uint64_t packets = 0;
         if (ok && work) {
             try {

@@ -3,8 +3,9 @@
 // reference reserved but never defined (prepostprocessor.h:112-116).
 //
 // Per-LTU calls (PreprocessSingle / PostprocessSingle) keep the reference's
-// exact contract so packet-driven backends can call them; the bulk calls are
-// how a GPU PPP is driven: one call per job slice, planes in HBM.
+// exact contract so packet-driven backends can call them, one packet or one
+// burst of packets per call; the bulk calls are how a GPU PPP is driven best:
+// one call per job slice, planes in HBM.
 #ifndef SWITCHML_AMD_PREPOSTPROCESSOR_H_
 #define SWITCHML_AMD_PREPOSTPROCESSOR_H_
 
@@ -52,6 +53,19 @@ class PrePostProcessor {
     // the slice's out_ptr.
     virtual void PostprocessBulk(const void* payload_plane, const void* global_exps,
                                  bool payload_le = false) = 0;
+
+    // ---- burst hooks: the per-LTU calls for n packets at once ----
+    // Same contract as n calls of PreprocessSingle(ltu_ids[i], entries[i],
+    // extras[i]) (PostprocessSingle) in that order — the packets of one DPDK
+    // rx burst and the tx burst it refills (dpdk_worker_thread.cc:276-345),
+    // or one RDMA completion batch.  This default is that loop; the HIP PPP
+    // runs a burst as one launch.
+    virtual void PreprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras) {
+        for (uint32_t i = 0; i < n; i++) PreprocessSingle(ltu_ids[i], entries[i], extras ? extras[i] : nullptr);
+    }
+    virtual void PostprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras) {
+        for (uint32_t i = 0; i < n; i++) PostprocessSingle(ltu_ids[i], entries[i], extras ? extras[i] : nullptr);
+    }
 
     Numel ltu_size() const { return ltu_size_; }
 

@@ -1,7 +1,9 @@
 // xgmi_switch.cc — see xgmi_switch.h.
 #include "xgmi_switch.h"
 
+#include <errno.h>
 #include <fcntl.h>
+#include <signal.h>
 #include <sys/mman.h>
 #include <unistd.h>
 
@@ -49,6 +51,8 @@ struct XgmiShm {
     std::atomic<uint32_t> magic;
     uint32_t W, T, P;
     uint64_t cap;
+    std::atomic<int32_t> creator_pid;      // worker 0, which creates the segment (O_EXCL)
+    std::atomic<uint32_t> poisoned;        // a worker failed inside an exchange: every later barrier throws
     std::atomic<uint32_t> attached;
     std::atomic<uint32_t> detached;
     ShmBarrier bar[kMaxT + 1];             // [t]: worker thread t; [kMaxT]: setup / teardown
@@ -56,6 +60,75 @@ struct XgmiShm {
 };
 
 static_assert(std::atomic<uint32_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
+
+namespace {
+bool pid_alive(int32_t pid) { return pid > 0 && (kill(pid, 0) == 0 || errno == EPERM); }
+}  // namespace
+
+// Worker 0 creates the segment (O_EXCL), replacing one left behind by a run
+// whose worker 0 is gone; the other workers wait for a segment whose creator
+// is alive.  So no worker joins a crashed run's barrier counts or handles.
+void XgmiSwitch::OpenSegment() {
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
+    auto fail = [&](const std::string& what) { throw SwitchMLFatal("xgmi switch: " + what); };
+    if (rank_ == 0) {
+        for (int attempt = 0;; attempt++) {
+            const int fd = shm_open(name_.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+            if (fd >= 0) {
+                created_ = true;
+                const bool sized = ftruncate(fd, sizeof(XgmiShm)) == 0;
+                void* m = sized ? mmap(nullptr, sizeof(XgmiShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0)
+                                : MAP_FAILED;
+                close(fd);
+                if (m == MAP_FAILED) fail("mapping " + name_ + ": " + strerror(errno));
+                shm_ = static_cast<XgmiShm*>(m);
+                shm_->W = (uint32_t)W_;
+                shm_->T = (uint32_t)T_;
+                shm_->P = P_;
+                shm_->cap = cap_;
+                shm_->creator_pid.store(getpid());
+                shm_->magic.store(kMagic, std::memory_order_release);
+                return;
+            }
+            if (errno != EEXIST || attempt > 3) fail("shm_open " + name_ + ": " + strerror(errno));
+            const int fe = shm_open(name_.c_str(), O_RDONLY, 0600);
+            if (fe >= 0) {
+                void* o = mmap(nullptr, sizeof(XgmiShm), PROT_READ, MAP_SHARED, fe, 0);
+                close(fe);
+                if (o != MAP_FAILED) {
+                    const int32_t pid = static_cast<XgmiShm*>(o)->creator_pid.load();
+                    munmap(o, sizeof(XgmiShm));
+                    if (pid_alive(pid) && pid != getpid())
+                        fail("session " + name_ + " is in use by process " + std::to_string(pid) +
+                             " (pick another backend.xgmi.session)");
+                }
+            }
+            fprintf(stderr, "[switchml] xgmi switch: replacing %s left behind by an earlier run\n", name_.c_str());
+            shm_unlink(name_.c_str());
+        }
+    }
+    for (;;) {
+        const int fd = shm_open(name_.c_str(), O_RDWR, 0600);
+        if (fd >= 0) {
+            void* m = mmap(nullptr, sizeof(XgmiShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            close(fd);
+            if (m != MAP_FAILED) {
+                auto* s = static_cast<XgmiShm*>(m);
+                while (s->magic.load(std::memory_order_acquire) != kMagic &&
+                       std::chrono::steady_clock::now() < deadline)
+                    std::this_thread::sleep_for(std::chrono::microseconds(200));
+                if (s->magic.load(std::memory_order_acquire) == kMagic && pid_alive(s->creator_pid.load())) {
+                    shm_ = s;
+                    return;
+                }
+                munmap(m, sizeof(XgmiShm));   // stale: worker 0 replaces it
+            }
+        }
+        if (std::chrono::steady_clock::now() > deadline)
+            fail("worker 0 did not open session " + name_ + " within backend.xgmi.timeout_ms");
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+}
 
 XgmiSwitch::XgmiSwitch(const Config& config, int device) {
     const GeneralConfig& g = config.general_;
@@ -69,31 +142,20 @@ XgmiSwitch::XgmiSwitch(const Config& config, int device) {
     if (T_ < 1 || T_ > kMaxT) throw SwitchMLFatal("xgmi switch: num_worker_threads must be 1..16");
     if (rank_ < 0 || rank_ >= W_) throw SwitchMLFatal("xgmi switch: general.rank must be < num_workers");
     name_ = "/switchml-" + config.backend_.xgmi.session;
+    try {
+        Setup(device);
+    } catch (...) {
+        Release();   // no planes, mappings or segment left behind by a failed construction
+        throw;
+    }
+}
 
+void XgmiSwitch::Setup(int device) {
     hip_ok(hipSetDevice(device), "hipSetDevice");
-    const int fd = shm_open(name_.c_str(), O_CREAT | O_RDWR, 0600);
-    if (fd < 0) throw SwitchMLFatal("xgmi switch: shm_open " + name_ + ": " + strerror(errno));
-    if (ftruncate(fd, sizeof(XgmiShm)) != 0) {
-        close(fd);
-        throw SwitchMLFatal("xgmi switch: ftruncate: " + std::string(strerror(errno)));
-    }
-    void* m = mmap(nullptr, sizeof(XgmiShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    close(fd);
-    if (m == MAP_FAILED) throw SwitchMLFatal("xgmi switch: mmap: " + std::string(strerror(errno)));
-    shm_ = static_cast<XgmiShm*>(m);
-    // every worker writes the same geometry; a mismatch is caught after the
-    // setup barrier
-    uint32_t expected = 0;
-    if (shm_->magic.compare_exchange_strong(expected, kMagic)) {
-        shm_->W = (uint32_t)W_;
-        shm_->T = (uint32_t)T_;
-        shm_->P = P_;
-        shm_->cap = cap_;
-    } else if (expected != kMagic) {
-        throw SwitchMLFatal("xgmi switch: " + name_ + " is not a SwitchML session segment");
-    }
+    OpenSegment();
     if (shm_->attached.fetch_add(1) >= (uint32_t)W_)
-        throw SwitchMLFatal("xgmi switch: session " + name_ + " already has num_workers workers (stale segment?)");
+        throw SwitchMLFatal("xgmi switch: session " + name_ + " already has num_workers workers");
+    attached_ = true;
 
     const uint64_t cap_b = (cap_ + 63) / 64 + 64;   // blocks at the smallest packet size, padded
     planes_.resize(T_);
@@ -150,17 +212,11 @@ XgmiSwitch::XgmiSwitch(const Config& config, int device) {
     }
 }
 
-XgmiSwitch::~XgmiSwitch() {
-    if (!shm_) return;
-    try {
-        Barrier(kMaxT);   // nobody reads a peer's planes any more
-    } catch (...) {
-    }
+// Everything this worker holds, in reverse order of Setup; safe on a
+// partially built instance.
+void XgmiSwitch::Release() {
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
-    try {
-        Barrier(kMaxT);   // every mapping of our planes is closed
-    } catch (...) {
-    }
+    opened_.clear();
     for (ThreadPlanes& tp : planes_) {
         (void)hipFree(tp.exps);
         (void)hipFree(tp.payload);
@@ -168,9 +224,37 @@ XgmiSwitch::~XgmiSwitch() {
         (void)hipFree(tp.gexp);
         if (tp.xst) (void)hipStreamDestroy(tp.xst);
     }
-    const bool last = shm_->detached.fetch_add(1) + 1 == (uint32_t)W_;
+    planes_.clear();
+    if (!shm_) return;
+    bool last = false;
+    if (attached_) last = shm_->detached.fetch_add(1) + 1 == (uint32_t)W_;
+    const bool poisoned = shm_->poisoned.load() != 0;
     munmap(shm_, sizeof(XgmiShm));
-    if (last) shm_unlink(name_.c_str());
+    shm_ = nullptr;
+    // the last worker out removes the name; so does worker 0 when the session
+    // failed (no peer may join it again)
+    if (last || (created_ && poisoned)) shm_unlink(name_.c_str());
+}
+
+XgmiSwitch::~XgmiSwitch() {
+    if (!shm_) return;
+    if (!shm_->poisoned.load()) {
+        try {
+            Barrier(kMaxT);   // nobody reads a peer's planes any more
+        } catch (...) {
+        }
+        for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+        opened_.clear();
+        try {
+            Barrier(kMaxT);   // every mapping of our planes is closed
+        } catch (...) {
+        }
+    }
+    Release();
+}
+
+void XgmiSwitch::Poison() {
+    if (shm_) shm_->poisoned.store(1, std::memory_order_release);
 }
 
 // Sense-reversing barrier over the W workers (one per worker thread, so the
@@ -178,6 +262,8 @@ XgmiSwitch::~XgmiSwitch() {
 // not arrive within backend.xgmi.timeout_ms fails the slice.
 void XgmiSwitch::Barrier(int index) {
     ShmBarrier& b = shm_->bar[index];
+    if (shm_->poisoned.load(std::memory_order_acquire))
+        throw SwitchMLFatal("xgmi switch: the session failed on another worker");
     const uint32_t g = b.gen.load(std::memory_order_acquire);
     if (b.count.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)W_) {
         b.count.store(0, std::memory_order_relaxed);
@@ -189,21 +275,34 @@ void XgmiSwitch::Barrier(int index) {
     while (b.gen.load(std::memory_order_acquire) == g) {
         if (++spins > 256) {
             std::this_thread::yield();
-            if ((spins & 1023) == 0 && std::chrono::steady_clock::now() > deadline)
-                throw SwitchMLFatal("xgmi switch: barrier timeout (a worker did not arrive)");
+            if ((spins & 1023) == 0) {
+                // A worker that failed mid-exchange poisons the session: its
+                // arrival (or absence) would put every later barrier of this
+                // thread index out of phase, so nobody proceeds past it.
+                if (shm_->poisoned.load(std::memory_order_acquire))
+                    throw SwitchMLFatal("xgmi switch: the session failed on another worker");
+                if (std::chrono::steady_clock::now() > deadline) {
+                    Poison();
+                    throw SwitchMLFatal("xgmi switch: barrier timeout (a worker did not arrive)");
+                }
+            }
         }
     }
 }
 
 namespace {
 void stream_sync(hipStream_t st) { hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize"); }
+// The writer's half of every hand-off to the peers: write
+// this GPU's L2 back before the stream sync that precedes the barrier.
+void release(hipStream_t st) { sml_ok(sml_release_to_peers(st), "sml_release_to_peers"); }
+constexpr uint32_t kPeer = SML_FLAG_PEER_PLANES;   // the reader's half: acquire in the reading kernels
 }  // namespace
 
 // The switch's exponent max over the W planes into gexp, then K3: quantize
 // with the global exponents into the own BE payload plane.
 void XgmiSwitch::Quantize(ThreadPlanes& tp, const float* in, uint64_t n, hipStream_t st) {
     const uint64_t B = sml_num_blocks(n, P_);
-    sml_ok(sml_switch_exps(tp.peer_exps.data(), (uint16_t)W_, B, tp.gexp, st), "sml_switch_exps");
+    sml_ok(sml_switch_exps(tp.peer_exps.data(), (uint16_t)W_, B, tp.gexp, kPeer, st), "sml_switch_exps");
     sml_ok(sml_quantize_pack(in, n, P_, (uint16_t)W_, tp.gexp, tp.payload, nullptr, 0, st), "sml_quantize_pack");
 }
 
@@ -222,7 +321,8 @@ void XgmiSwitch::Aggregate(ThreadPlanes& tp, uint64_t n, hipStream_t st) {
         planes[w] = tp.peer_payload[w] + blk0 * P_;
         exps[w] = tp.gexp + blk0;
     }
-    sml_ok(sml_switch_aggregate(planes, exps, (uint16_t)W_, n_el, P_, nullptr, nullptr, tp.out + blk0 * P_, 0, st),
+    sml_ok(sml_switch_aggregate(planes, exps, (uint16_t)W_, n_el, P_, nullptr, nullptr, tp.out + blk0 * P_, kPeer,
+                                st),
            "sml_switch_aggregate");
 }
 
@@ -241,9 +341,11 @@ void XgmiSwitch::FloatSlice(int tid, const float* in, float* out, uint64_t numel
     const uint64_t nchunks = (numel + cap_ - 1) / cap_;
     auto len = [&](uint64_t c) { return std::min<uint64_t>(cap_, numel - c * cap_); };
     sml_ok(sml_exponents(in, len(0), P_, tp.exps, st), "sml_exponents");
+    release(st);
     stream_sync(st);
     Barrier(tid);
     Quantize(tp, in, len(0), st);
+    release(st);
     stream_sync(st);
     Barrier(tid);
     for (uint64_t c = 0; c < nchunks; c++) {
@@ -251,12 +353,19 @@ void XgmiSwitch::FloatSlice(int tid, const float* in, float* out, uint64_t numel
         const bool next = c + 1 < nchunks;
         const float* in_next = in + (c + 1) * cap_;
         Aggregate(tp, n, tp.xst);
-        if (next) sml_ok(sml_exponents(in_next, len(c + 1), P_, tp.exps, st), "sml_exponents");
+        release(tp.xst);
+        if (next) {
+            sml_ok(sml_exponents(in_next, len(c + 1), P_, tp.exps, st), "sml_exponents");
+            release(st);
+        }
         stream_sync(tp.xst);
         stream_sync(st);
         Barrier(tid);
         Gather(tp, out + c * cap_, n, B, S, tp.xst);
-        if (next) Quantize(tp, in_next, len(c + 1), st);
+        if (next) {
+            Quantize(tp, in_next, len(c + 1), st);
+            release(st);
+        }
         stream_sync(tp.xst);
         stream_sync(st);
         Barrier(tid);   // peers are done reading our planes before they are written again
@@ -279,7 +388,7 @@ void XgmiSwitch::Gather(ThreadPlanes& tp, void* out, uint64_t n, uint64_t B, uin
         words[k] = std::min<uint64_t>(nbw * P_, n - b0 * P_);
         k++;
     }
-    sml_ok(sml_copy_segments(srcs, dsts, words, k, st), "sml_copy_segments");
+    sml_ok(sml_copy_segments(srcs, dsts, words, k, kPeer, st), "sml_copy_segments");
 }
 
 void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, hipStream_t st) {
@@ -287,6 +396,7 @@ void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, 
     const uint64_t B = sml_num_blocks(n, P_);
     const uint64_t S = (B + W_ - 1) / W_;
     sml_ok(sml_copy_words(in, tp.payload, n, st), "sml_copy_words");
+    release(st);
     hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
     Barrier(tid);
     const uint64_t blk0 = std::min<uint64_t>((uint64_t)rank_ * S, B);
@@ -296,8 +406,9 @@ void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, 
         for (int w = 0; w < W_; w++) planes[w] = tp.peer_payload[w] + blk0 * P_;
         int32_t* dst = reinterpret_cast<int32_t*>(tp.out) + blk0 * P_;
         sml_ok(sml_switch_aggregate(planes, nullptr, (uint16_t)W_, nb * P_, P_, dst, nullptr, nullptr,
-                                    SML_FLAG_PAYLOAD_LE, st),
+                                    SML_FLAG_PAYLOAD_LE | kPeer, st),
                "sml_switch_aggregate");
+        release(st);
     }
     hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
     Barrier(tid);
@@ -309,13 +420,25 @@ void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, 
 void XgmiSwitch::AllReduceSlice(int tid, const void* in, void* out, uint64_t numel, DataType type, hipStream_t st) {
     if (tid < 0 || tid >= T_) throw SwitchMLFatal("xgmi switch: bad worker thread id");
     if (numel == 0) return;
-    if (type == FLOAT32) {
-        FloatSlice(tid, static_cast<const float*>(in), static_cast<float*>(out), numel, st);
-        return;
-    }
-    for (uint64_t off = 0; off < numel; off += cap_) {
-        const uint64_t n = std::min<uint64_t>(cap_, numel - off);
-        IntChunk(tid, static_cast<const int32_t*>(in) + off, static_cast<int32_t*>(out) + off, n, st);
+    if (shm_->poisoned.load(std::memory_order_acquire))
+        throw SwitchMLFatal("xgmi switch: the session failed on another worker");
+    try {
+        if (type == FLOAT32) {
+            FloatSlice(tid, static_cast<const float*>(in), static_cast<float*>(out), numel, st);
+            return;
+        }
+        for (uint64_t off = 0; off < numel; off += cap_) {
+            const uint64_t n = std::min<uint64_t>(cap_, numel - off);
+            IntChunk(tid, static_cast<const int32_t*>(in) + off, static_cast<int32_t*>(out) + off, n, st);
+        }
+    } catch (...) {
+        // this worker's arrival count is now out of phase with its peers':
+        // fail the session for everyone rather than let a barrier pair
+        // different phases
+        Poison();
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamSynchronize(planes_[tid].xst);
+        throw;
     }
 }
 

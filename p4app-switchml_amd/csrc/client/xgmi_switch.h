@@ -10,7 +10,10 @@
 //   * rendezvous: a POSIX shared-memory segment named by
 //     backend.xgmi.session (the role of the controller's gRPC session setup,
 //     switchml.proto:21-91) holds every worker thread's plane IPC handles and
-//     one barrier per worker thread;
+//     one barrier per worker thread.  Worker 0 creates it (O_EXCL; a segment
+//     left by a crashed run whose worker 0 is gone is replaced), the others
+//     wait for it; a worker failing inside an exchange poisons the session so
+//     every peer's slices fail instead of pairing out-of-phase barriers;
 //   * per FIFO slice (thread t of every worker, the same slice geometry on all
 //     workers, as the switch's slots are), chunk by chunk: K2 exponents into
 //     the own plane → barrier → the max over the W exponent planes
@@ -56,7 +59,8 @@ class XgmiSwitch {
     // (a barrier over all W workers).  Throws SwitchMLFatal on failure.
     XgmiSwitch(const Config& config, int device);
     // Barrier with the other workers, unmap the peers' planes, barrier, free;
-    // the last worker removes the segment.
+    // the last worker removes the segment.  (A poisoned session skips the
+    // barriers.)
     ~XgmiSwitch();
     XgmiSwitch(const XgmiSwitch&) = delete;
     XgmiSwitch& operator=(const XgmiSwitch&) = delete;
@@ -65,6 +69,12 @@ class XgmiSwitch {
     // are device-accessible (HBM or pinned host), may alias; returns when the
     // result is in `out` (the stream is synchronised).
     void AllReduceSlice(int tid, const void* in, void* out, uint64_t numel, DataType type, hipStream_t stream);
+
+    // Fail the session for every worker: their next (or current) barrier
+    // throws, so their slices fail instead of pairing out-of-phase barriers.
+    // AllReduceSlice does this itself when it throws; the fault injection
+    // (backend.dummy.fail_worker_thread) calls it too.
+    void Poison();
 
   private:
     struct ThreadPlanes {
@@ -78,6 +88,9 @@ class XgmiSwitch {
         hipStream_t xst = nullptr;     // the exchange stream (K6, gather) beside the caller's
     };
 
+    void OpenSegment();
+    void Setup(int device);
+    void Release();
     void Barrier(int index);
     void FloatSlice(int tid, const float* in, float* out, uint64_t numel, hipStream_t st);
     void Aggregate(ThreadPlanes& tp, uint64_t n, hipStream_t st);
@@ -91,6 +104,8 @@ class XgmiSwitch {
     uint64_t timeout_ms_;
     std::string name_;
     XgmiShm* shm_ = nullptr;
+    bool created_ = false;    // this worker (rank 0) created the segment
+    bool attached_ = false;   // counted in shm_->attached
     std::vector<ThreadPlanes> planes_;
     std::vector<void*> opened_;  // peer mappings to close
 };

@@ -22,6 +22,36 @@
 
 namespace sml {
 
+// The reader's half of a hand-off from other GPUs (SML_FLAG_PEER_PLANES):
+// one system-scope acquire per workgroup before any load — on gfx950
+// `buffer_inv sc0 sc1`, which invalidates this CU's L1 and the XCD L2's
+// non-local lines (peer HBM is cached as such) — then the wait that holds
+// the workgroup until the invalidate is done (MI355X_MICROARCH.md: the
+// consumer's acquire -> s_waitcnt vmcnt(0) -> barrier -> plain loads).
+__device__ __forceinline__ void acquire_peer_planes(uint32_t flags) {
+    if (flags & SML_FLAG_PEER_PLANES) {   // uniform over the launch
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+}
+
+// The writer's half (sml_release_to_peers): a system-scope release from
+// kReleaseBlocks workgroups.  Workgroups are dealt round-robin over the 8
+// XCDs, so every XCD's L2 is written back by several of them (one per XCD
+// would do; the surplus costs nothing measurable and does not depend on the
+// dispatcher's exact placement).
+constexpr uint32_t kReleaseBlocks = 256;
+
+__global__ __launch_bounds__(64) void k_release_to_peers() {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
 struct SwitchArgs {
     const u4* payload[SML_MAX_SWITCH_WORKERS];
     const int8_t* exps[SML_MAX_SWITCH_WORKERS];
@@ -34,6 +64,7 @@ struct SwitchArgs {
     uint32_t nw;            // planes = num_workers
     uint32_t xcd;
     uint32_t exps_scalar;   // every exps[w] 4-byte aligned: one scalar load per slice
+    uint32_t flags;         // SML_FLAG_PEER_PLANES: acquire first
 };
 
 // W payload loads per lane-slice are issued before the adds (16-B
@@ -42,6 +73,7 @@ struct SwitchArgs {
 template <int P, bool ALIGNED, bool BE, bool RCP, bool EXPS>
 __global__ __launch_bounds__(kBlockThreads) void k_switch_aggregate(SwitchArgs a) {
     __shared__ float lut[256];
+    acquire_peer_planes(a.flags);
     if (a.out) {
         if constexpr (RCP) build_rcp_lut(lut, a.nw);
         else build_lut(lut, a.nw);
@@ -136,9 +168,11 @@ struct ExpsMaxArgs {
     uint64_t nblocks;
     uint32_t nw;
     uint32_t aligned;
+    uint32_t flags;
 };
 
 __global__ __launch_bounds__(kBlockThreads) void k_switch_exps(ExpsMaxArgs a) {
+    acquire_peer_planes(a.flags);
     const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; 4 * i < a.nblocks; i += stride) {
         const uint64_t k0 = 4 * i;
@@ -184,9 +218,11 @@ struct SegCopyArgs {
     uint32_t nseg;
     uint64_t ntiles;        // nseg x (the largest segment's groups) x kSegGroup
     uint32_t xcd;
+    uint32_t flags;
 };
 
 __global__ __launch_bounds__(kBlockThreads) void k_copy_segments(SegCopyArgs a) {
+    acquire_peer_planes(a.flags);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
@@ -273,6 +309,7 @@ sml_status_t sml_switch_aggregate(const int32_t* const* d_payloads, const int8_t
     a.ntiles = (a.nblocks * packet_numel + kTileElems - 1) / kTileElems;
     a.nw = num_workers;
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    a.flags = flags & SML_FLAG_PEER_PLANES;
     const dim3 grid(grid_for_tiles(a.ntiles));
     const hipStream_t st = (hipStream_t)stream;
     const bool al = !d_out || aligned16(d_out), be = !(flags & SML_FLAG_PAYLOAD_LE);
@@ -285,7 +322,7 @@ sml_status_t sml_switch_aggregate(const int32_t* const* d_payloads, const int8_t
 }
 
 sml_status_t sml_switch_exps(const int8_t* const* d_exps, uint16_t num_workers, uint64_t num_blocks,
-                             int8_t* d_exps_out, void* stream) {
+                             int8_t* d_exps_out, uint32_t flags, void* stream) {
     if (num_workers == 0 || !d_exps || !d_exps_out) return SML_ERR_INVALID_ARG;
     if (num_workers > SML_MAX_SWITCH_WORKERS) return SML_ERR_UNSUPPORTED;
     if (num_blocks == 0) return SML_OK;
@@ -299,6 +336,7 @@ sml_status_t sml_switch_exps(const int8_t* const* d_exps, uint16_t num_workers, 
     a.out = d_exps_out;
     a.nblocks = num_blocks;
     a.nw = num_workers;
+    a.flags = flags & SML_FLAG_PEER_PLANES;
     k_switch_exps<<<grid_for_vec((num_blocks + 3) / 4), kBlockThreads, 0, (hipStream_t)stream>>>(a);
     return launch_check();
 }
@@ -314,7 +352,7 @@ sml_status_t sml_copy_words(const void* d_src, void* d_dst, uint64_t num_words, 
 }
 
 sml_status_t sml_copy_segments(const void* const* d_srcs, void* const* d_dsts, const uint64_t* num_words,
-                               uint32_t num_segments, void* stream) {
+                               uint32_t num_segments, uint32_t flags, void* stream) {
     if (num_segments == 0) return SML_OK;
     if (!d_srcs || !d_dsts || !num_words || num_segments > SML_MAX_SWITCH_WORKERS) return SML_ERR_INVALID_ARG;
     SegCopyArgs a;
@@ -334,7 +372,13 @@ sml_status_t sml_copy_segments(const void* const* d_srcs, void* const* d_dsts, c
     if (a.nseg == 0) return SML_OK;
     a.ntiles = (uint64_t)a.nseg * groups * kSegGroup;
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    a.flags = flags & SML_FLAG_PEER_PLANES;
     k_copy_segments<<<grid_for_tiles(a.ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(a);
+    return launch_check();
+}
+
+sml_status_t sml_release_to_peers(void* stream) {
+    k_release_to_peers<<<kReleaseBlocks, 64, 0, (hipStream_t)stream>>>();
     return launch_check();
 }
 

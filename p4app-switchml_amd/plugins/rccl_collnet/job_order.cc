@@ -1,0 +1,152 @@
+// job_order.cc — see job_order.h.
+#include "job_order.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+namespace sml_collnet {
+
+namespace {
+constexpr uint32_t kMagic = 0x534d4c4fu;   // "SMLO"
+constexpr uint64_t kLog = 8192;            // entries in flight (keys not yet consumed by every worker)
+constexpr int kMaxWorkers = 16;
+
+bool pid_alive(int32_t pid) { return pid > 0 && (kill(pid, 0) == 0 || errno == EPERM); }
+}  // namespace
+
+struct alignas(64) Counter {
+    std::atomic<uint64_t> v;
+    char pad[56];
+};
+
+struct OrderShm {
+    std::atomic<uint32_t> magic;
+    uint32_t nworkers;
+    std::atomic<int32_t> creator_pid;
+    std::atomic<uint32_t> poisoned;
+    std::atomic<uint32_t> attached;
+    std::atomic<uint32_t> detached;
+    Counter head;                  // entries worker 0 appended
+    Counter done[kMaxWorkers];     // entries each worker > 0 consumed
+    CallKey log[kLog];
+};
+
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
+
+JobOrder::JobOrder(const std::string& session, int rank, int nworkers, uint64_t timeout_ms)
+    : name_("/switchml-collnet-" + session), rank_(rank), nworkers_(nworkers) {
+    if (nworkers < 1 || nworkers > kMaxWorkers || rank < 0 || rank >= nworkers)
+        throw std::runtime_error("job order: bad rank / worker count");
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+    auto expired = [&] { return std::chrono::steady_clock::now() > deadline; };
+    void* m = MAP_FAILED;
+    if (rank == 0) {
+        for (int attempt = 0;; attempt++) {
+            const int fd = shm_open(name_.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+            if (fd >= 0) {
+                if (ftruncate(fd, sizeof(OrderShm)) != 0) {
+                    close(fd);
+                    shm_unlink(name_.c_str());
+                    throw std::runtime_error("job order: ftruncate " + name_ + ": " + strerror(errno));
+                }
+                m = mmap(nullptr, sizeof(OrderShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+                close(fd);
+                if (m == MAP_FAILED) {
+                    shm_unlink(name_.c_str());
+                    throw std::runtime_error("job order: mmap: " + std::string(strerror(errno)));
+                }
+                break;
+            }
+            if (errno != EEXIST || attempt > 3)
+                throw std::runtime_error("job order: shm_open " + name_ + ": " + strerror(errno));
+            // a segment of that name exists: live (another job uses the session
+            // name) or left by a crashed run (its creator is gone): replace it
+            const int fe = shm_open(name_.c_str(), O_RDWR, 0600);
+            if (fe >= 0) {
+                void* o = mmap(nullptr, sizeof(OrderShm), PROT_READ, MAP_SHARED, fe, 0);
+                close(fe);
+                if (o != MAP_FAILED) {
+                    const int32_t pid = static_cast<OrderShm*>(o)->creator_pid.load();
+                    munmap(o, sizeof(OrderShm));
+                    if (pid_alive(pid))
+                        throw std::runtime_error("job order: session " + name_ + " is in use by process " +
+                                                 std::to_string(pid));
+                }
+            }
+            shm_unlink(name_.c_str());
+        }
+        shm_ = static_cast<OrderShm*>(m);
+        shm_->nworkers = (uint32_t)nworkers;
+        shm_->creator_pid.store(getpid());
+        shm_->attached.store(1);
+        shm_->magic.store(kMagic, std::memory_order_release);
+        return;
+    }
+    // workers > 0: wait for worker 0's live segment
+    for (;;) {
+        const int fd = shm_open(name_.c_str(), O_RDWR, 0600);
+        if (fd >= 0) {
+            m = mmap(nullptr, sizeof(OrderShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            close(fd);
+            if (m != MAP_FAILED) {
+                auto* s = static_cast<OrderShm*>(m);
+                while (s->magic.load(std::memory_order_acquire) != kMagic && !expired())
+                    std::this_thread::sleep_for(std::chrono::microseconds(200));
+                if (s->magic.load(std::memory_order_acquire) == kMagic && pid_alive(s->creator_pid.load())) {
+                    if (s->nworkers != (uint32_t)nworkers) {
+                        munmap(m, sizeof(OrderShm));
+                        throw std::runtime_error("job order: workers disagree on the worker count");
+                    }
+                    shm_ = s;
+                    shm_->attached.fetch_add(1);
+                    return;
+                }
+                munmap(m, sizeof(OrderShm));   // stale (creator gone): worker 0 replaces it
+            }
+        }
+        if (expired()) throw std::runtime_error("job order: worker 0 did not create " + name_ + " in time");
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+}
+
+JobOrder::~JobOrder() {
+    if (!shm_) return;
+    const bool last = shm_->detached.fetch_add(1) + 1 == (uint32_t)nworkers_;
+    munmap(shm_, sizeof(OrderShm));
+    if (last) shm_unlink(name_.c_str());
+}
+
+bool JobOrder::Append(const CallKey& k) {
+    const uint64_t h = shm_->head.v.load(std::memory_order_relaxed);
+    for (int r = 1; r < nworkers_; r++)
+        if (h - shm_->done[r].v.load(std::memory_order_acquire) >= kLog) return false;
+    shm_->log[h % kLog] = k;
+    shm_->head.v.store(h + 1, std::memory_order_release);
+    return true;
+}
+
+bool JobOrder::Peek(CallKey* k) const {
+    if (pos_ >= shm_->head.v.load(std::memory_order_acquire)) return false;
+    *k = shm_->log[pos_ % kLog];
+    return true;
+}
+
+void JobOrder::Consume() {
+    pos_++;
+    shm_->done[rank_].v.store(pos_, std::memory_order_release);
+}
+
+void JobOrder::Poison() { shm_->poisoned.store(1, std::memory_order_release); }
+
+bool JobOrder::Poisoned() const { return shm_->poisoned.load(std::memory_order_acquire) != 0; }
+
+}  // namespace sml_collnet

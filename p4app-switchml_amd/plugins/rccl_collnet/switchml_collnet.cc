@@ -25,28 +25,45 @@
 //
 // Beside the CollNet table the library exports a p2p net table,
 // ncclNetPlugin_v6, as the reference does (switchml_plugin.cc:37): NCCL/RCCL
-// resolve the CollNet table from a net plugin library.  The reference leaves
-// its net table empty for a patched NCCL to fill with NCCL's own IB net
-// (switchml_nccl.patch:24-81); this one forwards every call to the net plugin
-// named by SWITCHML_NET_PLUGIN (a library exporting ncclNetPlugin_v6, loaded
-// with dlopen at init).  With none named, init() fails cleanly
-// (ncclInternalError) and RCCL falls back to its internal IB / socket nets.
+// take the CollNet table of a library only together with its net table, and
+// drop both when that net fails init.  The reference leaves its net table
+// empty for a patched NCCL to fill with NCCL's own IB net
+// (switchml_nccl.patch:24-81); this library carries its own TCP net
+// (socket_net.h), so RCCL keeps the CollNet table with no patch and no other
+// plugin.  SWITCHML_NET_PLUGIN=<library exporting ncclNetPlugin_v6> forwards
+// the net table to that library instead (e.g. a vendor RDMA net).
+//
+// switchml_collnet_stats() (C symbol) reports how often RCCL called the
+// CollNet entry points, so a run can prove that its all-reduces went through
+// iallreduce.
 #include <dlfcn.h>
 
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
+#include <deque>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 
 #include "collnet_abi.h"
 #include "context.h"
 #include "loopback_backend.h"
+#include "job_order.h"
+#include "socket_net.h"
 
 namespace {
 
 ncclDebugLogger_t g_logger = nullptr;
+
+// Calls RCCL made into the CollNet table (switchml_collnet_stats()).
+struct Counters {
+    std::atomic<uint64_t> init{0}, connect{0}, iallreduce{0}, iallreduce_bytes{0}, test_done{0}, reg_mr{0},
+        iallreduce_submitted{0};
+} g_calls;
 
 void log_info(const char* msg) {
     if (g_logger) g_logger(NCCL_LOG_INFO, 0, __FILE__, __LINE__, "%s", msg);
@@ -59,19 +76,36 @@ struct ListenComm {
 struct CollComm {
     int nranks;
     int rank;
+    uint32_t ordinal;                    // connect() ordinal in this process
+    uint32_t next_mr = 0;                // registration ordinals (job_order.h keys)
+    std::map<uint32_t, uint64_t> calls;  // per send-buffer registration: calls so far
 };
 
 struct MemHandle {
     int type;
+    uint32_t id;
 };
 
 struct Request {
-    std::shared_ptr<switchml::Job> job;
+    std::shared_ptr<switchml::Job> job;   // null until submitted (job_order.h)
     ncclDataType_t dtype;
     int count;
-    void* recv;            // caller's recv buffer (uint8 case)
-    int32_t* widened;      // temp int32 buffer (uint8 case)
+    void* send;
+    void* recv;                           // what the job reduces into
+    void* user_recv;                      // caller's recv buffer (uint8 case)
+    int32_t* widened;                     // temp int32 buffer (uint8 case)
+    sml_collnet::CallKey key;
+    bool failed;
 };
+
+// One submission order for every worker of the in-node switch (job_order.h);
+// null with the loopback backend or a single worker.  RCCL calls the CollNet
+// table from its proxy thread; the mutex makes other callers safe too.
+std::mutex g_mu;
+std::unique_ptr<sml_collnet::JobOrder> g_order;
+std::deque<Request*> g_unsubmitted;   // worker 0: not yet logged (log full); others: waiting for their turn
+uint32_t g_comms = 0, g_open_comms = 0;
+bool g_trace = false;
 
 int type_size(ncclDataType_t t) {
     switch (t) {
@@ -84,6 +118,7 @@ int type_size(ncclDataType_t t) {
 
 ncclResult_t sml_init(ncclDebugLogger_t logger) {
     g_logger = logger;
+    g_calls.init++;
     try {
         switchml::Context& ctx = switchml::Context::GetInstance();
         if (ctx.GetContextState() == switchml::Context::RUNNING) return ncclSuccess;
@@ -119,13 +154,12 @@ ncclResult_t sml_devices(int* ndev) {
 }
 
 char g_name[] = "SWITCHML";
-char g_pci[] = "/sys/devices/virtual/switchml";
 
 ncclResult_t sml_get_properties(int dev, ncclNetProperties_v6_t* props) {
     if (dev != 0 || !props) return ncclInvalidArgument;
     memset(props, 0, sizeof(*props));
     props->name = g_name;
-    props->pciPath = g_pci;
+    props->pciPath = nullptr;    // not a PCI device (the switch is reached through the net)
     props->guid = 0x53574d4cull;  // "SWML"
     props->ptrSupport = NCCL_PTR_HOST | NCCL_PTR_CUDA;
     props->speed = 100000;
@@ -150,8 +184,32 @@ ncclResult_t sml_connect(void* handles[], int nranks, int rank, void* listen_com
     if (rank < 0 || rank >= nranks) return ncclInternalError;  // switchml_plugin.cc:210-213
     // with the in-node switch the communicator must be the session's workers
     const switchml::GeneralConfig& g = switchml::Context::GetInstance().GetConfig().general_;
-    if (g.backend == "xgmi" && (nranks != g.num_workers || rank != g.rank)) return ncclInvalidUsage;
-    *coll_comm = new CollComm{nranks, rank};
+    if (g.backend == "xgmi" && (nranks != g.num_workers || rank != g.rank)) {
+        if (g_logger)
+            g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__,
+                     "SwitchML CollNet: communicator rank %d of %d, but the xgmi session is worker %d of %d",
+                     rank, nranks, (int)g.rank, (int)g.num_workers);
+        return ncclInvalidUsage;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g.backend == "xgmi" && nranks > 1 && !g_order) {
+        try {
+            const switchml::Config& cfg = switchml::Context::GetInstance().GetConfig();
+            g_order.reset(new sml_collnet::JobOrder(cfg.backend_.xgmi.session, rank, nranks,
+                                                    cfg.backend_.xgmi.timeout_ms));
+        } catch (const std::exception& e) {
+            if (g_logger) g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__, "SwitchML CollNet: %s", e.what());
+            return ncclSystemError;
+        }
+    }
+    g_trace = getenv("SWITCHML_COLLNET_TRACE") != nullptr;
+    g_calls.connect++;
+    auto* c = new CollComm;
+    c->nranks = nranks;
+    c->rank = rank;
+    c->ordinal = g_comms++;
+    g_open_comms++;
+    *coll_comm = c;
     return ncclSuccess;
 }
 
@@ -160,14 +218,16 @@ ncclResult_t sml_reduce_support(ncclDataType_t dtype, ncclRedOp_t op, int* suppo
     return ncclSuccess;
 }
 
-ncclResult_t sml_reg_mr(void*, void*, int, int type, void** mhandle) {
-    *mhandle = new MemHandle{type};
+ncclResult_t sml_reg_mr(void* coll_comm, void*, int, int type, void** mhandle) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_calls.reg_mr++;
+    auto* c = static_cast<CollComm*>(coll_comm);
+    *mhandle = new MemHandle{type, c ? c->next_mr++ : 0u};
     return ncclSuccess;
 }
 
-ncclResult_t sml_reg_mr_dmabuf(void*, void*, size_t, int type, uint64_t, int, void** mhandle) {
-    *mhandle = new MemHandle{type};
-    return ncclSuccess;
+ncclResult_t sml_reg_mr_dmabuf(void* coll_comm, void* data, size_t, int type, uint64_t, int, void** mhandle) {
+    return sml_reg_mr(coll_comm, data, 0, type, mhandle);
 }
 
 ncclResult_t sml_dereg_mr(void*, void* mhandle) {
@@ -175,13 +235,62 @@ ncclResult_t sml_dereg_mr(void*, void* mhandle) {
     return ncclSuccess;
 }
 
-ncclResult_t sml_iallreduce(void*, void* send, void* recv, int count, ncclDataType_t dtype, ncclRedOp_t op,
-                            void*, void*, void** request) {
+void submit(Request* r) {
+    const switchml::DataType sdt = r->dtype == ncclFloat32 ? switchml::FLOAT32 : switchml::INT32;
+    r->job = switchml::Context::GetInstance().AllReduceAsync(r->send, r->recv, (uint64_t)r->count, sdt,
+                                                             switchml::SUM);
+    g_calls.iallreduce_submitted++;
+    if (g_trace && g_logger)
+        g_logger(NCCL_LOG_INFO, 0, __FILE__, __LINE__, "SwitchML CollNet: job comm %u buf %u call %lu count %d",
+                 r->key.comm, r->key.buf, (unsigned long)r->key.seq, r->count);
+}
+
+// Submit whatever the job order allows (job_order.h); g_mu held.
+void pump() {
+    if (!g_order) return;
+    if (g_order->leader()) {
+        while (!g_unsubmitted.empty() && g_order->Append(g_unsubmitted.front()->key)) {
+            submit(g_unsubmitted.front());
+            g_unsubmitted.pop_front();
+        }
+        return;
+    }
+    sml_collnet::CallKey k;
+    while (g_order->Peek(&k)) {
+        auto it = g_unsubmitted.begin();
+        for (; it != g_unsubmitted.end(); ++it) {
+            const sml_collnet::CallKey& q = (*it)->key;
+            if (q.comm == k.comm && q.buf == k.buf && q.seq == k.seq) break;
+        }
+        if (it == g_unsubmitted.end()) return;   // this rank's call for the entry has not come yet
+        Request* r = *it;
+        g_unsubmitted.erase(it);
+        g_order->Consume();
+        if (r->key.count != k.count || r->key.dtype != k.dtype) {
+            if (g_logger)
+                g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__,
+                         "SwitchML CollNet: worker 0 reduces %ld elements of type %d for this call, this worker %ld "
+                         "of type %d", (long)k.count, k.dtype, (long)r->key.count, r->key.dtype);
+            r->failed = true;
+            g_order->Poison();
+            continue;
+        }
+        submit(r);
+    }
+}
+
+ncclResult_t sml_iallreduce(void* coll_comm, void* send, void* recv, int count, ncclDataType_t dtype,
+                            ncclRedOp_t op, void* send_mh, void*, void** request) {
     if (op != ncclSum || type_size(dtype) == 0 || count < 0) return ncclInvalidArgument;
     switchml::Context& ctx = switchml::Context::GetInstance();
     if (ctx.GetContextState() != switchml::Context::RUNNING) return ncclInvalidUsage;
-    auto* r = new Request{nullptr, dtype, count, recv, nullptr};
-    switchml::DataType sdt = dtype == ncclFloat32 ? switchml::FLOAT32 : switchml::INT32;
+    auto* c = static_cast<CollComm*>(coll_comm);
+    auto* r = new Request{nullptr, dtype, count, send, recv, recv, nullptr, {}, false};
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_order && g_order->Poisoned()) {
+        delete r;
+        return ncclRemoteError;
+    }
     try {
         if (dtype == ncclUint8) {
             if (switchml::IsDevicePointer(send) || switchml::IsDevicePointer(recv)) {
@@ -191,10 +300,20 @@ ncclResult_t sml_iallreduce(void*, void* send, void* recv, int count, ncclDataTy
             r->widened = new int32_t[count > 0 ? count : 1];
             const uint8_t* s8 = static_cast<const uint8_t*>(send);
             for (int i = 0; i < count; i++) r->widened[i] = s8[i];
-            send = recv = r->widened;
+            r->send = r->recv = r->widened;
         }
-        r->job = ctx.AllReduceAsync(send, recv, (uint64_t)count, sdt, switchml::SUM);
+        const uint32_t buf = send_mh ? static_cast<MemHandle*>(send_mh)->id : 0xffffffffu;
+        r->key = {c ? c->ordinal : 0u, buf, c ? c->calls[buf]++ : 0u, (int64_t)count, (int32_t)dtype, 0};
+        g_calls.iallreduce++;
+        g_calls.iallreduce_bytes += (uint64_t)count * type_size(dtype);
+        if (g_order) {
+            g_unsubmitted.push_back(r);
+            pump();
+        } else {
+            submit(r);
+        }
     } catch (const std::exception& e) {
+        if (g_logger) g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__, "SwitchML CollNet: %s", e.what());
         delete[] r->widened;
         delete r;
         return ncclInternalError;
@@ -212,30 +331,48 @@ ncclResult_t sml_iflush(void*, void*, int, void*, void** request) {
 
 ncclResult_t sml_test(void* request, int* done, int* size) {
     Request* r = static_cast<Request*>(request);
-    const switchml::JobStatus st = r->job->GetJobStatus();
-    if (st == switchml::FAILED) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    try {
+        pump();
+    } catch (const std::exception& e) {
+        if (g_logger) g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__, "SwitchML CollNet: %s", e.what());
+        if (g_order) g_order->Poison();
+    }
+    const bool poisoned = !r->job && g_order && g_order->Poisoned();
+    if (r->failed || poisoned || (r->job && r->job->GetJobStatus() == switchml::FAILED)) {
         *done = 0;
+        if (g_order) {
+            g_order->Poison();   // the peers' matching jobs cannot complete either
+            for (auto it = g_unsubmitted.begin(); it != g_unsubmitted.end(); ++it)
+                if (*it == r) {
+                    g_unsubmitted.erase(it);
+                    break;
+                }
+        }
         delete[] r->widened;
         delete r;
         return ncclInternalError;
     }
-    if (st != switchml::FINISHED) {
+    if (!r->job || r->job->GetJobStatus() != switchml::FINISHED) {
         *done = 0;
         return ncclSuccess;
     }
     if (r->dtype == ncclUint8) {   // switchml_plugin.cc:370-378
-        uint8_t* out = static_cast<uint8_t*>(r->recv);
+        uint8_t* out = static_cast<uint8_t*>(r->user_recv);
         for (int i = 0; i < r->count; i++) out[i] = (uint8_t)r->widened[i];
         delete[] r->widened;
     }
     *done = 1;
+    g_calls.test_done++;
     if (size) *size = r->count * type_size(r->dtype);
     delete r;
     return ncclSuccess;
 }
 
 ncclResult_t sml_close_coll(void* coll_comm) {
+    std::lock_guard<std::mutex> lk(g_mu);
     delete static_cast<CollComm*>(coll_comm);
+    if (g_open_comms && --g_open_comms == 0 && g_unsubmitted.empty()) g_order.reset();
     return ncclSuccess;
 }
 
@@ -245,20 +382,26 @@ ncclResult_t sml_close_listen(void* listen_comm) {
 }
 
 // ------------------------------------------------------------ p2p net --
-// Forwarding table over the underlying net plugin (SWITCHML_NET_PLUGIN).
+// The built-in TCP net (socket_net.h), or a forwarding table over the net
+// plugin named by SWITCHML_NET_PLUGIN.
+
+const ncclNet_v6_t kSocketNet = {
+    "SWITCHML",        sml_net::Init,      sml_net::Devices,   sml_net::GetProperties, sml_net::Listen,
+    sml_net::Connect,  sml_net::Accept,    sml_net::RegMr,     sml_net::RegMrDmaBuf,   sml_net::DeregMr,
+    sml_net::Isend,    sml_net::Irecv,     sml_net::Iflush,    sml_net::Test,          sml_net::CloseSend,
+    sml_net::CloseRecv, sml_net::CloseListen};
 
 void* g_net_lib = nullptr;
-ncclNet_v6_t* g_under = nullptr;
+const ncclNet_v6_t* g_under = nullptr;
 
 ncclResult_t net_init(ncclDebugLogger_t logger) {
     if (logger) g_logger = logger;
     if (g_under) return ncclSuccess;
     const char* path = getenv("SWITCHML_NET_PLUGIN");
     if (!path || !*path) {
-        if (g_logger)
-            g_logger(NCCL_LOG_INFO, 0, __FILE__, __LINE__,
-                     "SwitchML net: no underlying net plugin (SWITCHML_NET_PLUGIN unset)");
-        return ncclInternalError;
+        const ncclResult_t r = kSocketNet.init(logger);
+        if (r == ncclSuccess) g_under = &kSocketNet;
+        return r;
     }
     void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
     if (!h) {
@@ -319,6 +462,18 @@ ncclResult_t net_close_listen(void* c) { SML_FWD(closeListen, c); }
 }  // namespace
 
 extern "C" {
+// Counts of CollNet calls since the library was loaded: init, connect,
+// iallreduce, iallreduce bytes, test() completions, regMr, jobs submitted to
+// the Context.  Returns how many of the n slots it filled.
+__attribute__((visibility("default"))) int switchml_collnet_stats(uint64_t* out, int n) {
+    const uint64_t v[7] = {g_calls.init.load(),      g_calls.connect.load(),   g_calls.iallreduce.load(),
+                           g_calls.iallreduce_bytes.load(), g_calls.test_done.load(), g_calls.reg_mr.load(),
+                           g_calls.iallreduce_submitted.load()};
+    int k = 0;
+    for (; k < n && k < 7; k++) out[k] = v[k];
+    return k;
+}
+
 __attribute__((visibility("default"))) ncclNet_v6_t ncclNetPlugin_v6 = {
     "SWITCHML",         net_init,        net_devices,       net_get_properties, net_listen,
     net_connect,        net_accept,      net_reg_mr,        net_reg_mr_dmabuf,  net_dereg_mr,

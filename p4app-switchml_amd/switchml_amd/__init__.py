@@ -25,6 +25,7 @@ SML_ERR_HIP = 4
 
 FLAG_PAYLOAD_LE = 0x1
 FLAG_ROUND_RNE = 0x2
+FLAG_PEER_PLANES = 0x4   # inputs written by other GPUs: acquire first (sml_release_to_peers on the writer)
 
 PACKET_NUMELS = (64, 128, 256, 512, 1024)
 
@@ -57,6 +58,19 @@ def frame_params(dst_mac=b"\x02\x00\x00\x00\x00\x01", src_mac=b"\x02\x00\x00\x00
     fp.pool_index_shift = pool_index_shift
     fp.max_outstanding_pkts = max_outstanding_pkts
     return fp
+
+
+MAX_BURST = 64
+
+
+class PacketBurst(ctypes.Structure):
+    """sml_packet_burst (include/switchml_hip.h): up to MAX_BURST per-packet
+    calls of one job slice in one launch."""
+    _fields_ = [("in_", ctypes.c_void_p), ("out", ctypes.c_void_p), ("numel", ctypes.c_uint64),
+                ("packet_numel", ctypes.c_uint32), ("num_workers", ctypes.c_uint16), ("data_type", ctypes.c_uint16),
+                ("batch_num_ltus", ctypes.c_uint64), ("recv_exps", ctypes.c_void_p), ("count", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("pkt_ids", ctypes.c_uint64 * MAX_BURST),
+                ("entries", ctypes.c_void_p * MAX_BURST), ("extras", ctypes.c_void_p * MAX_BURST)]
 
 
 class SwitchMLError(RuntimeError):
@@ -125,7 +139,15 @@ def lib():
     L.sml_switch_aggregate.restype = i32
     L.sml_switch_aggregate.argtypes = [vp, vp, u16, u64, u32, vp, vp, vp, u32, vp]
     L.sml_copy_segments.restype = i32
-    L.sml_copy_segments.argtypes = [vp, vp, vp, u32, vp]
+    L.sml_copy_segments.argtypes = [vp, vp, vp, u32, u32, vp]
+    L.sml_switch_exps.restype = i32
+    L.sml_switch_exps.argtypes = [vp, u16, u64, vp, u32, vp]
+    L.sml_release_to_peers.restype = i32
+    L.sml_release_to_peers.argtypes = [vp]
+    L.sml_preprocess_burst.restype = i32
+    L.sml_preprocess_burst.argtypes = [ctypes.POINTER(PacketBurst), vp]
+    L.sml_postprocess_burst.restype = i32
+    L.sml_postprocess_burst.argtypes = [ctypes.POINTER(PacketBurst), vp]
     L.sml_ipc_handle_bytes.restype = u32
     L.sml_ipc_get_handle.restype = i32
     L.sml_ipc_get_handle.argtypes = [vp, vp, ctypes.POINTER(u64)]
@@ -405,10 +427,11 @@ def switch_aggregate(payloads, exps=None, numel: int | None = None, packet_numel
     return out
 
 
-def copy_segments(pairs, stream=None):
+def copy_segments(pairs, flags: int = 0, stream=None):
     """sml_copy_segments: every (src, dst) pair of 32-bit tensors (same
     numel; CUDA or pinned host) copied in ONE launch, the tiles dealt
-    round-robin over the pairs (the in-node switch's multicast)."""
+    round-robin over the pairs (the in-node switch's multicast).
+    flags = FLAG_PEER_PLANES when sources were written by other GPUs."""
     torch = _torch()
     k = len(pairs)
     if k > MAX_SWITCH_WORKERS:
@@ -424,7 +447,48 @@ def copy_segments(pairs, stream=None):
         words[i] = s.numel()
     _check("sml_copy_segments", lib().sml_copy_segments(
         ctypes.cast(srcs, ctypes.c_void_p), ctypes.cast(dsts, ctypes.c_void_p), ctypes.cast(words, ctypes.c_void_p),
-        k, _stream(stream, pairs[0][0] if pairs else None)))
+        k, flags, _stream(stream, pairs[0][0] if pairs else None)))
+
+
+def packet_burst(x, out, packet_numel: int, num_workers: int, batch_num_ltus: int, recv_exps, pkt_ids,
+                 entries, extras, flags: int = 0) -> PacketBurst:
+    """A PacketBurst over slice `x` (fp32 or int32 CUDA tensor) and output
+    `out`; entries / extras are device-addressable addresses (ints)."""
+    torch = _torch()
+    if len(pkt_ids) > MAX_BURST:
+        raise ValueError(f"at most {MAX_BURST} packets per burst")
+    b = PacketBurst()
+    b.in_ = x.data_ptr()
+    b.out = out.data_ptr() if out is not None else None
+    b.numel = x.numel()
+    b.packet_numel = packet_numel
+    b.num_workers = num_workers
+    b.data_type = 1 if x.dtype == torch.int32 else 0
+    b.batch_num_ltus = batch_num_ltus
+    b.recv_exps = recv_exps.data_ptr() if recv_exps is not None else None
+    b.count = len(pkt_ids)
+    b.flags = flags
+    for i, (q, e, x_) in enumerate(zip(pkt_ids, entries, extras)):
+        b.pkt_ids[i], b.entries[i], b.extras[i] = q, e, x_
+    return b
+
+
+def preprocess_burst(burst: PacketBurst, stream=None, like=None):
+    """sml_preprocess_burst: PreprocessSingle for every packet of the burst."""
+    _check("sml_preprocess_burst", lib().sml_preprocess_burst(ctypes.byref(burst), _stream(stream, like)))
+
+
+def postprocess_burst(burst: PacketBurst, stream=None, like=None):
+    """sml_postprocess_burst: PostprocessSingle for every packet of the burst."""
+    _check("sml_postprocess_burst", lib().sml_postprocess_burst(ctypes.byref(burst), _stream(stream, like)))
+
+
+def release_to_peers(stream=None, device=None):
+    """sml_release_to_peers: system-scope release on every XCD after the work
+    on `stream` (the writer's half of a hand-off to other GPUs)."""
+    if stream is None:
+        stream = _torch().cuda.current_stream(device)
+    _check("sml_release_to_peers", lib().sml_release_to_peers(_stream(stream)))
 
 
 def stream_copy(src, dst, stream=None):

@@ -135,12 +135,19 @@ def _ready(*tensors):
     the producing stream before AllReduceAsync (ProcessGroupSML.cpp:137-151)
     — device (or pinned host) torch tensors are made ready first: the
     current stream's pending kernels may still write the input, or read a
-    freed block the caching allocator has handed out again as the output."""
+    freed block the caching allocator has handed out again as the output.
+    Every device involved is waited for: each CUDA tensor's own
+    device, and for pinned host tensors the current device, whose stream is
+    the one torch produces them on."""
+    import torch
+    devices = set()
     for t in tensors:
-        if getattr(t, "is_cuda", False) or (hasattr(t, "is_pinned") and t.is_pinned()):
-            import torch
-            torch.cuda.current_stream(t.device if t.is_cuda else None).synchronize()
-            return
+        if getattr(t, "is_cuda", False):
+            devices.add(t.device.index if t.device.index is not None else torch.cuda.current_device())
+        elif hasattr(t, "is_pinned") and t.is_pinned():
+            devices.add(torch.cuda.current_device())
+    for d in sorted(devices):
+        torch.cuda.current_stream(d).synchronize()
 
 
 def allreduce_async(inp, out=None, numel: int | None = None) -> Job:

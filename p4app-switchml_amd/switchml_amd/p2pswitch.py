@@ -30,7 +30,8 @@ import time
 import torch
 import torch.distributed as dist
 
-from . import _check, bswap_i32, exponents, lib, num_blocks, quantize_pack, switch_aggregate
+from . import (FLAG_PEER_PLANES, _check, bswap_i32, exponents, lib, num_blocks, quantize_pack,
+               release_to_peers, switch_aggregate)
 
 
 def shard_blocks(num_blocks: int, world: int, rank: int) -> tuple[int, int]:
@@ -121,7 +122,12 @@ class PeerSwitchAllReduce:
             return self.payload[blk0 * self.P:(blk0 + nblk) * self.P]
         return _Ptr(self.peers[w].ptr + blk0 * self.P * 4, nblk * self.P, self.dev)
 
-    def _barrier(self):
+    def _barrier(self, release: bool = True):
+        """Hand-off to the peers: release this GPU's writes to
+        system scope (L2 written back), wait for them, meet the peers; the
+        kernels that then read peer planes acquire (FLAG_PEER_PLANES)."""
+        if release:
+            release_to_peers(device=self.dev)
         torch.cuda.current_stream(self.dev).synchronize()
         dist.barrier(group=self.group)
 
@@ -168,12 +174,13 @@ class PeerSwitchAllReduce:
             planes = [self._plane(w, blk0, nblk) for w in range(self.W)]
             if is_int:
                 # the switch's wrapping sum of the BE words, then ntohl
-                switch_aggregate(planes, None, nblk * P, P, payload_out=shard[:nblk * P])
+                switch_aggregate(planes, None, nblk * P, P, payload_out=shard[:nblk * P], flags=FLAG_PEER_PLANES)
                 bswap_i32(shard[:n_el], out=shard[:n_el])
             else:
                 ex = self.exps[blk0:blk0 + nblk]
-                switch_aggregate(planes, [ex] * self.W, n_el, P, out=shard[:n_el])  # K6 over xGMI
-        self._barrier()                                                         # peers done reading
+                switch_aggregate(planes, [ex] * self.W, n_el, P, out=shard[:n_el],
+                                 flags=FLAG_PEER_PLANES)                        # K6 over xGMI
+        self._barrier(release=False)                                            # peers done reading
         self._mark("k6")
         if self.host_collectives:
             parts = [torch.empty(S * P, dtype=dst.dtype) for _ in range(self.W)]

@@ -1,0 +1,297 @@
+"""RCCL itself dispatching all-reduces into the SwitchML CollNet plugin.
+
+The reference's integration (frameworks_integration/nccl_plugin) is a
+CollNet plugin NCCL calls for an all-reduce across nodes: every node's
+head rank hands its buffer to `iallreduce`, the switch sums the nodes' data
+(switchml_plugin.cc:293-387).  This module runs that for real with RCCL:
+
+* one process per worker (`python -m switchml_amd.rccl_collnet --rank r ...`),
+  torch.distributed backend "nccl" (= RCCL) with
+  NCCL_NET_PLUGIN = librccl-net-switchml.so and NCCL_COLLNET_ENABLE=1;
+* NCCL_HOSTID = a distinct id per rank, so every rank is a "node" of its own
+  and RCCL's CollNet — which reduces ACROSS nodes — spans all workers, the
+  way each SwitchML worker is a host with a NIC to the switch.  On an 8-GPU
+  node the ranks use GPUs 0..W-1; on a one-GPU box (`--same-gpu`) they share
+  cuda:0 (RCCL rejects two ranks on one device of one host; two hosts'
+  ranks are distinct);
+* the plugin's backend is the in-node switch (general.backend = xgmi,
+  xgmi_switch.h): the W ranks' plugin instances form one xgmi session and
+  reduce through each other's HBM;
+* RCCL's own p2p traffic (bootstrap aside) runs over the plugin library's
+  TCP net (plugins/rccl_collnet/socket_net.h).
+
+Each rank reports the plugin's call counters (`switchml_collnet_stats`),
+checks the RCCL all-reduce of integer-valued data bit for bit against the
+exact sum AND against the same buffer all-reduced through the plugin's
+iallreduce by hand (one job, the xgmi switch directly), checks N(0,1) data
+against the same by-hand all-reduce and against the fp32 sum within the
+quantization bound, and times RCCL all-reduces of configs[4]'s ResNet-50
+buckets.  The parent (`launch`) never touches the GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+import uuid
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PLUGIN_PATH = os.path.join(_HERE, "librccl-net-switchml.so")
+RESNET50_BUCKETS = [6_553_600, 6_553_600, 6_553_600, 5_896_232]
+STATS = ("init", "connect", "iallreduce", "iallreduce_bytes", "test_done", "reg_mr", "iallreduce_submitted")
+
+
+def collnet_stats(path: str = PLUGIN_PATH) -> dict:
+    """The plugin's CollNet call counters in THIS process (RCCL dlopens the
+    same file, so this is the instance RCCL calls)."""
+    lib = ctypes.CDLL(path)
+    buf = (ctypes.c_uint64 * len(STATS))()
+    n = lib.switchml_collnet_stats(buf, len(STATS))
+    return {k: int(buf[i]) for i, k in enumerate(STATS[:n])}
+
+
+def rank_env(rank: int, world: int, device: int, session: str, channels: int, algo: str | None,
+             log_dir: str | None, threads: int = 1, packet_numel: int = 256) -> dict:
+    ini = (f"[general]\nrank = {rank}\nnum_workers = {world}\nnum_worker_threads = {threads}\n"
+           f"packet_numel = {packet_numel}\nbackend = xgmi\nprepostprocessor = hip_exponent_quantizer\n"
+           f"[backend.xgmi]\nsession = {session}\ntimeout_ms = 120000\n[backend.hip]\ndevice = {device}\n")
+    env = {
+        "NCCL_NET_PLUGIN": PLUGIN_PATH,
+        "NCCL_COLLNET_ENABLE": "1",
+        "NCCL_HOSTID": f"switchml-worker-{session}-{rank}",
+        "RCCL_MSCCL_ENABLE": "0",
+        "RCCL_MSCCLPP_ENABLE": "0",
+        "SWITCHML_CONFIG_INI": ini,
+        "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+    }
+    env.pop("SWITCHML_NET_PLUGIN", None)
+    if channels > 0:
+        env["NCCL_MAX_NCHANNELS"] = str(channels)
+    if algo:
+        env["NCCL_ALGO"] = algo
+    if log_dir:
+        env.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,NET,GRAPH,ENV,TUNING",
+                   NCCL_DEBUG_FILE=os.path.join(log_dir, f"rccl.rank{rank}.%p.log"))
+    return env
+
+
+def _bound(xs, out_ref, world):
+    """|out - sum x| <= per-element quantization bound, with the global block
+    exponent e (max over workers): each worker rounds to 2^(e-31) * W units
+    (half a unit each), the dequantized sum rounds once more (half an ulp)."""
+    import numpy as np
+    s = np.sum(np.stack(xs).astype(np.float64), axis=0)
+    err = np.abs(out_ref.astype(np.float64) - s)
+    amax = max(float(np.max(np.abs(x))) for x in xs)
+    e = np.floor(np.log2(amax)) + 1 if amax > 0 else 0
+    unit = world * 2.0 ** (e - 31)
+    lim = world * 0.5 * unit + np.abs(s) * 2.0 ** -23 + unit
+    return float(err.max()), bool((err <= lim).all())
+
+
+def rank_main(a):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", a.device)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{a.port}", rank=a.rank, world_size=a.world,
+                            device_id=dev)
+    out = {"rank": a.rank, "device": a.device}
+    W = a.world
+    n = a.numel
+
+    def say(msg):
+        print(f"[rank {a.rank}] {msg}", flush=True)
+
+    say("process group up")
+
+    def allreduce(t):
+        dist.all_reduce(t)
+        torch.cuda.synchronize()
+
+    # 1) integer-valued data: every path is exact, so RCCL == exact sum bit for bit
+    gens = [np.random.default_rng(1000 + r) for r in range(W)]
+    xs = [g.integers(-1000, 1001, n).astype(np.float32) for g in gens]
+    exact = np.sum(np.stack(xs), axis=0, dtype=np.float32)
+    t = torch.from_numpy(xs[a.rank]).to(dev)
+    before = collnet_stats()
+    allreduce(t)
+    after = collnet_stats()
+    out["stats_before"], out["stats_after_first"] = before, after
+    say(f"integer all-reduce done, iallreduce calls {after['iallreduce'] - before['iallreduce']}")
+    r_int = t.cpu().numpy()
+    out["int_exact"] = bool(np.array_equal(r_int.view(np.uint32), exact.view(np.uint32)))
+
+    # the same buffer through the plugin's iallreduce by hand (RCCL is done
+    # with it): the xgmi switch, one job
+    from .collnet import CollNetComm
+    comm = CollNetComm(nranks=W, rank=a.rank, path=PLUGIN_PATH)
+    h = torch.from_numpy(xs[a.rank]).to(dev)
+    torch.cuda.synchronize()
+    comm.wait(comm.iallreduce(h.data_ptr(), h.data_ptr(), n))
+    r_hand = h.cpu().numpy()
+    out["int_equal_direct"] = bool(np.array_equal(r_hand.view(np.uint32), r_int.view(np.uint32)))
+    say(f"by-hand iallreduce done: int_exact {out['int_exact']} equal_direct {out['int_equal_direct']}")
+
+    # 2) N(0,1) data: RCCL vs by hand (equal when RCCL's CollNet chunks start
+    # on packet boundaries) and vs the fp32 sum within the quantization bound
+    ys = [np.random.default_rng(2000 + r).standard_normal(n).astype(np.float32) for r in range(W)]
+    t = torch.from_numpy(ys[a.rank]).to(dev)
+    allreduce(t)
+    r_rccl = t.cpu().numpy()
+    h = torch.from_numpy(ys[a.rank]).to(dev)
+    torch.cuda.synchronize()
+    comm.wait(comm.iallreduce(h.data_ptr(), h.data_ptr(), n))
+    r_hand = h.cpu().numpy()
+    out["normal_equal_direct"] = bool(np.array_equal(r_hand.view(np.uint32), r_rccl.view(np.uint32)))
+    out["normal_max_err"], out["normal_within_bound"] = _bound(ys, r_rccl, W)
+    say(f"N(0,1) done: equal_direct {out['normal_equal_direct']} within_bound {out['normal_within_bound']}")
+    comm.close()
+
+    # 3) configs[4]: ResNet-50 DDP buckets all-reduced by RCCL (through CollNet)
+    if a.iters > 0:
+        bk = [torch.randn(m, device=dev) * 1e-3 for m in RESNET50_BUCKETS]
+        for b in bk:
+            dist.all_reduce(b)
+        torch.cuda.synchronize()
+        dist.barrier()
+        c0 = collnet_stats()
+        t0 = time.perf_counter()
+        for _ in range(a.iters):
+            for b in bk:
+                dist.all_reduce(b)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        c1 = collnet_stats()
+        out["configs4_ms_per_iter"] = 1e3 * dt / a.iters
+        out["configs4_iallreduce_calls_per_iter"] = (c1["iallreduce"] - c0["iallreduce"]) / a.iters
+        say(f"configs[4] {out['configs4_ms_per_iter']:.3f} ms per iteration")
+    out["stats_end"] = collnet_stats()
+    print("RESULT " + json.dumps(out), flush=True)
+    # tear down under a deadline: the report is out, a teardown that blocks
+    # (RCCL's proxy threads) must not hold the run
+    import threading
+    threading.Timer(30.0, lambda: os._exit(3)).start()
+    dist.destroy_process_group()
+    os._exit(0)
+
+
+def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, channels: int = 1,
+           algo: str | None = "CollNetDirect", log_dir: str | None = None, timeout: float = 600,
+           port: int | None = None, extra_env: dict | None = None) -> dict:
+    """Run `world` ranks (child processes) and gather their reports.  The
+    caller must not have initialised the GPU."""
+    session = uuid.uuid4().hex[:10]
+    port = port or (20000 + os.getpid() % 20000)
+    if log_dir:
+        os.makedirs(log_dir, exist_ok=True)
+    import tempfile
+    out_dir = log_dir or tempfile.mkdtemp(prefix="sml_rccl_collnet_")
+    procs, files = [], []
+    for r in range(world):
+        env = dict(os.environ)
+        env.update(rank_env(r, world, 0 if same_gpu else r, session, channels, algo, log_dir))
+        env.pop("SWITCHML_NET_PLUGIN", None)
+        env.update(extra_env or {})
+        env["PYTHONPATH"] = os.path.dirname(_HERE) + os.pathsep + env.get("PYTHONPATH", "")
+        cmd = [sys.executable, "-u", "-m", "switchml_amd.rccl_collnet", "--rank", str(r), "--world", str(world),
+               "--device", str(0 if same_gpu else r), "--port", str(port), "--numel", str(numel),
+               "--iters", str(iters)]
+        f = open(os.path.join(out_dir, f"rank{r}.out"), "w+")
+        files.append(f)
+        procs.append(subprocess.Popen(cmd, env=env, stdout=f, stderr=subprocess.STDOUT, text=True))
+    t0 = time.time()
+    t_end = t0 + timeout
+    last = t0
+    while any(p.poll() is None for p in procs):
+        if time.time() > t_end:
+            for q in procs:
+                q.kill()
+            break
+        if any(p.poll() not in (None, 0) for p in procs):
+            time.sleep(5)   # one rank failed: give the others a moment, then stop them
+            for q in procs:
+                if q.poll() is None:
+                    q.kill()
+            break
+        if time.time() - last > 10:
+            last = time.time()
+            tail = []
+            for f in files:
+                f.flush()
+                with open(f.name, errors="replace") as g:
+                    ls = [l for l in g.read().splitlines() if l.startswith("[rank")]
+                tail.append(ls[-1] if ls else "-")
+            print(f"[rccl_collnet] {time.time() - t0:.0f} s: " + " | ".join(tail), flush=True)
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    outs = []
+    for f in files:
+        with open(f.name, errors="replace") as g:
+            outs.append(g.read())
+        f.close()
+    ranks, tails = [], []
+    for o in outs:
+        res = [l for l in o.splitlines() if l.startswith("RESULT ")]
+        ranks.append(json.loads(res[-1][7:]) if res else None)
+        tails.append(o.strip().splitlines()[-12:])
+    rep = {"world": world, "same_gpu": same_gpu, "numel": numel, "channels": channels, "algo": algo,
+           "extra_env": extra_env or {},
+           "returncodes": [p.returncode for p in procs], "ranks": ranks}
+    if any(r is None for r in ranks) or any(p.returncode for p in procs):
+        rep["tails"] = tails
+    ok = all(r is not None for r in ranks)
+    rep["iallreduce_calls"] = [r["stats_end"]["iallreduce"] if r else None for r in ranks]
+    rep["ok"] = bool(ok and all(p.returncode == 0 for p in procs)
+                     and all(r["stats_after_first"]["iallreduce"] > r["stats_before"]["iallreduce"] for r in ranks)
+                     and all(r["int_exact"] and r["int_equal_direct"] and r["normal_within_bound"] for r in ranks))
+    return rep
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rank", type=int)
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--port", type=int, default=29655)
+    ap.add_argument("--numel", type=int, default=1 << 22)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--same-gpu", action="store_true")
+    ap.add_argument("--channels", type=int, default=1)
+    ap.add_argument("--algo", default="CollNetDirect",
+                    help="NCCL_ALGO for the ranks ('' = RCCL's tuner); RCCL 7.2 runs AllReduce on CollNet only "
+                         "as CollNetDirect (its CollNetChain has no threads: nothing reduces)")
+    ap.add_argument("--env", action="append", default=[], help="KEY=VALUE for the ranks (repeatable)")
+    ap.add_argument("--log-dir")
+    ap.add_argument("--out")
+    a = ap.parse_args(argv)
+    if a.rank is not None:
+        rank_main(a)
+        return 0
+    rep = launch(a.world, a.same_gpu, a.numel, a.iters, a.channels, a.algo or None, a.log_dir,
+                 extra_env=dict(kv.split("=", 1) for kv in a.env))
+    if a.log_dir:
+        lines = []
+        for f in sorted(os.listdir(a.log_dir)):
+            with open(os.path.join(a.log_dir, f), errors="replace") as fh:
+                lines += [f"{f}: {l.rstrip()}" for l in fh
+                          if any(k in l for k in ("SWITCHML", "SwitchML", "CollNet", "collnet", "Collnet", "NET/",
+                                                  "Plugin", "WARN", "Algo", "nNodes", "nodes"))]
+        rep["rccl_log"] = lines[:200]
+    s = json.dumps(rep, indent=1)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(s)
+    print(s)
+    return 0 if rep["ok"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

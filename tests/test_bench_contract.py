@@ -1,0 +1,82 @@
+"""bench.py's self-check: the timed buckets come from an
+integer-exact generator restated in bench.py (bench_bucket), and the planes
+the timed K1 launches leave are compared with oracle digests committed in
+tests/golden/digests_bench.json (made by tests/golden/make_bench_digests.py).
+CPU: the restatement equals oracle.splitmix_grad (any seed, any offset), and
+the committed N = 1 digest of bucket 0 is the oracle's.  GPU: the same
+generator on the device, and K1 over the first bench bucket hashing to the
+committed digest."""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+DIGESTS = os.path.join(ROOT, "tests", "golden", "digests_bench.json")
+
+
+@pytest.mark.parametrize("seed,off,n", [(4242, 0, 100_000), (4245, 123_457, 70_001), (0, 1 << 33, 5000),
+                                        (2 ** 40 + 3, 67_108_864 - 777, 2000)])
+def test_bench_generator_is_oracle_splitmix_grad(seed, off, n):
+    import torch
+    got = bench.bench_bucket(torch, seed, off, n, "cpu").numpy()
+    if off < (1 << 32):
+        ref = O.splitmix_grad(seed, off + n)[off:]
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    # restated in numpy at the global index directly (offsets past what fits in memory)
+    i = np.arange(off, off + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed * 0x9E3779B97F4A7C15 % 2 ** 64) + i * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(31))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(29))
+    mant = (z >> np.uint64(40)).astype(np.int64) - (1 << 23)
+    k = ((i >> np.uint64(8)) * np.uint64(7) + (z & np.uint64(1))) % np.uint64(16)
+    ref2 = np.ldexp(mant.astype(np.float32), -(24 + k.astype(np.int32))).astype(np.float32)
+    assert np.array_equal(got.view(np.uint32), ref2.view(np.uint32))
+
+
+def test_bench_digests_shape_and_bucket0():
+    with open(DIGESTS) as f:
+        d = json.load(f)
+    assert d["packet_numel"] == 256 and d["buckets"] == 4 and d["seed0"] == bench.BENCH_SEED0
+    assert len(d["bucket_T1"]) == 4
+    assert sorted(d["job"]) == ["T2", "T4", "T8"]
+    for G in (2, 4, 8):
+        assert [len(r) for r in d["job"][f"T{G}"]] == [G] * 4
+    # T = 4 slice 0 of the job IS the N = 1 bucket (same seed, elements [0, 2^26))
+    assert d["job"]["T4"][0][0] == d["bucket_T1"][0]
+    x = O.splitmix_grad(d["seed0"], d["bucket_numel"])
+    e, q = O.exponents(x, 256), O.quantize(x, 256, 1)
+    assert hashlib.sha256(e.tobytes()).hexdigest() == d["bucket_T1"][0]["exps"]
+    assert hashlib.sha256(q.tobytes()).hexdigest() == d["bucket_T1"][0]["payload"]
+    assert bench.expected_digests(0, 1, 0, d["bucket_numel"], 256, 4) == d["bucket_T1"]
+    assert bench.expected_digests(d["job_numel"], 8, 5, 0, 256, 4) == [d["job"]["T8"][b][5] for b in range(4)]
+    assert bench.expected_digests(0, 1, 0, d["bucket_numel"], 64, 4) is None
+
+
+@pytest.mark.gpu
+def test_bench_bucket_on_gpu_hashes_to_digest(cuda):
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
+    import switchml_amd as sw
+    with open(DIGESTS) as f:
+        d = json.load(f)
+    small = bench.bench_bucket(torch, 4243, 1000, 300_000, cuda).cpu().numpy()
+    assert np.array_equal(small.view(np.uint32), O.splitmix_grad(4243, 301_000)[1000:].view(np.uint32))
+    N = d["bucket_numel"]
+    for b in (0, 3):
+        x = bench.bench_bucket(torch, d["seed0"] + b, 0, N, cuda)
+        B = sw.num_blocks(N, 256)
+        pl = torch.empty(B * 256, dtype=torch.int32, device=cuda)
+        ex = torch.empty(B, dtype=torch.int8, device=cuda)
+        sw.quantize_pack(x, 256, 1, payload=pl, exps_out=ex)
+        torch.cuda.synchronize()
+        assert bench.planes_sha256(torch, ex, pl, N, 256) == d["bucket_T1"][b]

@@ -27,7 +27,7 @@ def test_exports_every_header_symbol(sw):
 
 def test_abi_version_and_status_strings(sw):
     L = sw.lib()
-    assert L.sml_abi_version() == 1
+    assert L.sml_abi_version() == 2
     for code, name in [(0, b"SML_OK"), (1, b"SML_ERR_INVALID_ARG"), (2, b"SML_ERR_UNSUPPORTED"),
                        (3, b"SML_ERR_ALIGNMENT"), (4, b"SML_ERR_HIP")]:
         assert L.sml_status_string(code) == name

@@ -7,10 +7,9 @@ the Job).  CPU: the table, the bypass PPP (no GPU) and the uint8 widening;
 GPU: device and host buffers through the HIP quantizer, bit-exact vs the
 oracle's dummy-backend packet loop.
 
-A live RCCL CollNet run needs a multi-node CollNet topology (RCCL disables
-CollNet below NCCL_COLLNET_NODE_THRESHOLD nodes), so RCCL itself loading the
-plugin is not exercised here (tools/rccl_plugin_probe.py checks that RCCL
-resolves both exported tables)."""
+RCCL itself calling the table (every rank its own CollNet "node" through
+NCCL_HOSTID, the xgmi in-node switch as backend) is
+tests/test_rccl_collnet.py; here the table is driven by hand."""
 import ctypes
 import os
 import subprocess
@@ -215,29 +214,21 @@ print(json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("with_underlying", [False, True])
-def test_net_table_chains_to_underlying_plugin(tmp_path, with_underlying):
+def test_net_table_forwards_to_underlying_plugin(tmp_path):
     """ncclNetPlugin_v6 (reference: switchml_plugin.cc:37, NCCL_PLUGIN_SYMBOL
-    beside the CollNet table): without SWITCHML_NET_PLUGIN its init fails
-    cleanly (ncclInternalError, so RCCL falls back to its internal nets);
-    with one, every call is forwarded to the underlying plugin."""
+    beside the CollNet table) with SWITCHML_NET_PLUGIN set: every call is
+    forwarded to that underlying plugin."""
     fake = tmp_path / "libfake_net.so"
     src = tmp_path / "fake_net.c"
     src.write_text(FAKE_NET)
     subprocess.run(["gcc", "-shared", "-fPIC", "-O1", "-o", str(fake), str(src)], check=True)
     code = NET_DRIVER.format(root=ROOT, tests=os.path.join(ROOT, "tests"), fake=str(fake))
-    env = dict(os.environ)
-    env.pop("SWITCHML_NET_PLUGIN", None)
-    if with_underlying:
-        env["SWITCHML_NET_PLUGIN"] = str(fake)
+    env = dict(os.environ, SWITCHML_NET_PLUGIN=str(fake))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     import json
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["name"] == "SWITCHML"
-    if not with_underlying:
-        assert out["init"] == 3          # ncclInternalError: no underlying net
-        return
     assert out["init"] == 0
     assert out["devices"] == [0, 3] and out["props_bad"] == 4
     assert out["listen"] == 0 and out["handle"] == "FAKE"
@@ -246,6 +237,140 @@ def test_net_table_chains_to_underlying_plugin(tmp_path, with_underlying):
     calls = out["fake_calls"]
     for i in (1, 2, 3, 4, 5, 6, 7, 9, 10, 13, 14, 15, 16):
         assert calls[i] >= 1, (i, calls)
+
+
+# The built-in TCP net (plugins/rccl_collnet/socket_net.h), driven the way
+# RCCL's net transport drives a v6 net: listen -> handle to the peer ->
+# connect / accept (non-blocking: NULL comm means "call again") -> regMr ->
+# isend / irecv -> test until done -> close.
+SOCKET_DRIVER = r"""
+import ctypes, json, os, sys, time
+import numpy as np
+sys.path[:0] = [{root!r}, {tests!r}]
+from test_collnet_plugin import NetV6, PLUGIN, LOGGER, vp
+t = NetV6.in_dll(ctypes.CDLL(PLUGIN), "ncclNetPlugin_v6")
+P = ctypes.POINTER
+F = lambda name, *types: ctypes.CFUNCTYPE(ctypes.c_int, *types)(getattr(t, name))
+init, devices = F("init", LOGGER), F("devices", P(ctypes.c_int))
+props = F("getProperties", ctypes.c_int, vp)
+listen = F("listen", ctypes.c_int, vp, P(vp)); connect = F("connect", ctypes.c_int, vp, P(vp))
+accept = F("accept", vp, P(vp)); regmr = F("regMr", vp, vp, ctypes.c_int, ctypes.c_int, P(vp))
+dereg = F("deregMr", vp, vp)
+isend = F("isend", vp, vp, ctypes.c_int, ctypes.c_int, vp, P(vp))
+irecv = F("irecv", vp, ctypes.c_int, P(vp), P(ctypes.c_int), P(ctypes.c_int), P(vp), P(vp))
+iflush = F("iflush", vp, ctypes.c_int, P(vp), P(ctypes.c_int), P(vp), P(vp))
+test = F("test", vp, P(ctypes.c_int), P(ctypes.c_int))
+close_s, close_r, close_l = F("closeSend", vp), F("closeRecv", vp), F("closeListen", vp)
+keep_logger = LOGGER(lambda *a: None)   # the library calls it later (warnings)
+out = {{"init": init(keep_logger)}}
+n = ctypes.c_int(); devices(ctypes.byref(n)); out["ndev"] = n.value
+class Props(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("pciPath", ctypes.c_char_p), ("guid", ctypes.c_uint64),
+                ("ptrSupport", ctypes.c_int), ("speed", ctypes.c_int), ("port", ctypes.c_int),
+                ("latency", ctypes.c_float), ("maxComms", ctypes.c_int), ("maxRecvs", ctypes.c_int)]
+pr = Props(); out["props"] = props(0, ctypes.cast(ctypes.pointer(pr), vp))
+out["pname"], out["ptr"], out["maxRecvs"] = pr.name.decode(), pr.ptrSupport, pr.maxRecvs
+out["pci_null"] = pr.pciPath is None
+
+def pair():
+    h = (ctypes.c_char * 128)(); lc, sc, rc = vp(), vp(), vp()
+    assert listen(0, ctypes.cast(h, vp), ctypes.byref(lc)) == 0
+    assert accept(lc, ctypes.byref(rc)) == 0 and not rc.value      # nobody connected yet: call again
+    assert connect(0, ctypes.cast(h, vp), ctypes.byref(sc)) == 0 and sc.value
+    for _ in range(10000):
+        assert accept(lc, ctypes.byref(rc)) == 0
+        if rc.value: break
+        time.sleep(0.0005)
+    assert rc.value
+    return lc, sc, rc
+
+def wait(req):
+    d, sz = ctypes.c_int(0), ctypes.c_int(-1)
+    while not d.value:
+        rc = test(req, ctypes.byref(d), ctypes.byref(sz))
+        if rc: return ("err", rc)
+    return sz.value
+
+lc, sc, rc = pair()
+mh = vp(); out["regmr_host"] = regmr(sc, None, 0, 1, ctypes.byref(mh)); out["regmr_cuda"] = regmr(sc, None, 0, 2, ctypes.byref(vp()))
+rng = np.random.default_rng(7)
+sizes = [0, 1, 7, 4096, 65536 + 3, 8 << 20, 123457]
+msgs = [rng.integers(0, 256, s, dtype=np.uint8) for s in sizes]
+bufs = [np.full(s + 100, 0xAB, dtype=np.uint8) for s in sizes]
+sreqs, rreqs = [], []
+for i, (m, b) in enumerate(zip(msgs, bufs)):        # all posted before any test: FIFO matching
+    q = vp(); assert isend(sc, m.ctypes.data_as(vp), m.size, i, mh, ctypes.byref(q)) == 0 and q.value; sreqs.append(q)
+    q = vp(); d = (vp * 1)(b.ctypes.data); s = (ctypes.c_int * 1)(b.size); tg = (ctypes.c_int * 1)(i)
+    assert irecv(rc, 1, d, s, tg, (vp * 1)(None), ctypes.byref(q)) == 0 and q.value; rreqs.append(q)
+got = []
+for i in range(len(sizes)):    # drive both sides like the proxy: poll every request
+    done_s = done_r = None
+    while done_s is None or done_r is None:
+        for which, q in (("s", sreqs[i]), ("r", rreqs[i])):
+            if (which == "s" and done_s is not None) or (which == "r" and done_r is not None): continue
+            d, sz = ctypes.c_int(0), ctypes.c_int(-1)
+            assert test(q, ctypes.byref(d), ctypes.byref(sz)) == 0
+            if d.value:
+                if which == "s": done_s = sz.value
+                else: done_r = sz.value
+    got.append([done_s, done_r])
+out["sizes"] = got
+out["payload_ok"] = all(bool(np.array_equal(b[:m.size], m)) and bool((b[m.size:] == 0xAB).all())
+                        for m, b in zip(msgs, bufs))
+fq = vp(); out["iflush"] = [iflush(rc, 1, (vp * 1)(None), (ctypes.c_int * 1)(0), (vp * 1)(None), ctypes.byref(fq)), fq.value]
+# a receive smaller than the message: an error, not a silent truncation
+big = np.zeros(64, np.uint8); small = np.zeros(16, np.uint8)
+q = vp(); isend(sc, big.ctypes.data_as(vp), 64, 0, mh, ctypes.byref(q))
+r2 = vp(); irecv(rc, 1, (vp * 1)(small.ctypes.data), (ctypes.c_int * 1)(16), (ctypes.c_int * 1)(0), (vp * 1)(None), ctypes.byref(r2))
+out["truncated"] = wait(r2)
+dereg(sc, mh)
+out["close"] = [close_s(sc), close_r(rc), close_l(lc)]
+# a connector with another handle's nonce is dropped, the right one accepted
+h1 = (ctypes.c_char * 128)(); h2 = (ctypes.c_char * 128)(); l1, l2 = vp(), vp()
+listen(0, ctypes.cast(h1, vp), ctypes.byref(l1)); listen(0, ctypes.cast(h2, vp), ctypes.byref(l2))
+forged = bytearray(bytes(h2)); forged[8:14] = bytes(h1)[8:14]       # l1's address, l2's nonce
+fh = (ctypes.c_char * 128).from_buffer_copy(bytes(forged)); s_bad, s_ok, r1 = vp(), vp(), vp()
+connect(0, ctypes.cast(fh, vp), ctypes.byref(s_bad)); connect(0, ctypes.cast(h1, vp), ctypes.byref(s_ok))
+for _ in range(10000):
+    accept(l1, ctypes.byref(r1))
+    if r1.value: break
+    time.sleep(0.0005)
+x = np.arange(10, dtype=np.uint8); y = np.zeros(10, np.uint8)
+q1, q2 = vp(), vp()
+isend(s_ok, x.ctypes.data_as(vp), 10, 0, None, ctypes.byref(q1))
+irecv(r1, 1, (vp * 1)(y.ctypes.data), (ctypes.c_int * 1)(10), (ctypes.c_int * 1)(0), (vp * 1)(None), ctypes.byref(q2))
+out["nonce_check"] = [wait(q1), wait(q2), bool((x == y).all())]
+out["bad_handle"] = connect(0, ctypes.cast((ctypes.c_char * 128)(), vp), ctypes.byref(vp()))
+print(json.dumps(out))
+"""
+
+
+def test_builtin_socket_net():
+    """Without SWITCHML_NET_PLUGIN the library's own TCP net serves RCCL
+    (so RCCL keeps the paired CollNet table): non-blocking accept, FIFO
+    matching of posted sends and receives across sizes 0 B .. 8 MiB, receive
+    sizes reported by test(), no bytes past the message touched, a
+    too-small receive fails, a connection presenting another handle's nonce
+    is dropped, host pointers only."""
+    code = SOCKET_DRIVER.format(root=ROOT, tests=os.path.join(ROOT, "tests"))
+    env = dict(os.environ)
+    env.pop("SWITCHML_NET_PLUGIN", None)
+    env["SWITCHML_NET_IFADDR"] = "127.0.0.1"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["init"] == 0 and out["ndev"] == 1 and out["props"] == 0
+    assert out["pname"] == "SWITCHML" and out["ptr"] == 1 and out["maxRecvs"] == 1 and out["pci_null"]
+    assert out["regmr_host"] == 0 and out["regmr_cuda"] != 0
+    sizes = [0, 1, 7, 4096, 65536 + 3, 8 << 20, 123457]
+    assert out["sizes"] == [[s, s] for s in sizes]
+    assert out["payload_ok"]
+    assert out["iflush"] == [0, None]
+    assert out["truncated"] == ["err", 3]
+    assert out["close"] == [0, 0, 0]
+    assert out["nonce_check"] == [10, 10, True]
+    assert out["bad_handle"] == 4
 
 
 RESNET50_BUCKETS = [6_553_600, 6_553_600, 6_553_600, 5_896_232]   # 25 MiB DDP buckets of 25,557,032 params

@@ -1,0 +1,152 @@
+"""Per-packet calls in bursts (sml_preprocess_burst / sml_postprocess_burst,
+csrc/sml_packets.hip): the reference's PreprocessSingle / PostprocessSingle
+(ppp.cc:69-192, 194-299) for a DPDK-style rx burst and the tx burst it
+refills (dpdk_worker_thread.cc:276-345, dpdk_worker_thread_utils.inc:134,177).
+
+The driver here is the reference's dummy packet loop (dummy_worker_thread.cc:
+86-177) with its ring of b packet slots — in pinned host memory (a NIC's
+buffer pool) and in HBM — run burst by burst; packets inside a burst in
+shuffled order.  Every packet as sent (exponent byte for p < B, the n real
+payload words for p >= b) is captured after its burst and compared with the
+oracle's packet-loop capture (orc_dummy_packet_stream), the output with the
+oracle's output, bit for bit; the stale tail words of a partial last block
+must be left as they were.  Plus INT32 slices and the argument checks."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+
+def sw():
+    import switchml_amd as s
+    s.lib()
+    return s
+
+
+def run_bursts(x, P, W, b_max, ring_place, cuda, rng, burst_cap=64):
+    """The dummy packet loop, burst by burst, through the C-ABI; returns
+    (captured packet exps, captured packet payloads, output, b)."""
+    import torch
+    s = sw()
+    n = x.size
+    B = O.num_blocks(n, P)
+    b = min(B, b_max)
+    total = B + b
+    xd = torch.from_numpy(x).to(cuda)
+    out = torch.full((n,), float("nan"), device=cuda)
+    recv = torch.zeros(B, dtype=torch.int8, device=cuda)
+    SENT = 0x5A5A5A5A                        # the slots' bytes before any packet was built
+    if ring_place == "device":
+        ring = torch.full((b * P,), SENT, dtype=torch.int64, device=cuda).to(torch.int32)
+        extra = torch.zeros(b * 2, dtype=torch.uint8, device=cuda)
+    else:
+        ring = torch.full((b * P,), SENT, dtype=torch.int64).to(torch.int32).pin_memory()
+        extra = torch.zeros(b * 2, dtype=torch.uint8).pin_memory()
+    rbase, ebase = ring.data_ptr(), extra.data_ptr()
+    cap_e = np.zeros(total, dtype=np.int8)
+    cap_p = np.zeros((total, P), dtype=np.uint32)
+    stream = torch.cuda.current_stream(cuda)
+
+    def bursts(ids, pre):
+        ids = list(ids)
+        rng.shuffle(ids)                       # a burst's packets in any order
+        for i0 in range(0, len(ids), burst_cap):
+            part = ids[i0:i0 + burst_cap]
+            slots = [q % b for q in part]
+            bt = s.packet_burst(xd, out, P, W, b, recv, part, [rbase + sl * P * 4 for sl in slots],
+                                [ebase + sl * 2 for sl in slots])
+            (s.preprocess_burst if pre else s.postprocess_burst)(bt, stream)
+        torch.cuda.synchronize()
+
+    def snapshot():
+        return ring.cpu().numpy().view(np.uint32).reshape(b, P).copy()
+
+    def capture(ids, before):
+        rh = snapshot()
+        eh = extra.cpu().numpy()
+        for q in ids:
+            sl = q % b
+            cap_e[q] = eh[sl * 2].astype(np.int8) if q < B else 0
+            if q >= b:
+                m = min(P, n - (q - b) * P)
+                cap_p[q, :m] = rh[sl, :m]
+                # a partial block's tail keeps the slot's stale words (ppp.cc:102-109)
+                assert np.array_equal(rh[sl, m:], before[sl, m:]), "stale tail overwritten"
+
+    prev = snapshot()
+    bursts(range(b), True)
+    capture(range(b), prev)
+    for p0 in range(0, total, b):
+        w = min(b, total - p0)
+        torch.cuda.synchronize()
+        rh = ring.view(torch.int32)
+        # ProcessPacket x W (dummy_backend.cc:72-84) on the window's slots
+        if W != 1:
+            s.loopback_aggregate(rh[: w * P], W)
+        torch.cuda.synchronize()
+        bursts(range(p0, p0 + w), False)
+        nxt = [q + b for q in range(p0, p0 + w) if q + b < total]
+        prev = snapshot()
+        bursts(nxt, True)
+        capture(nxt, prev)
+    return cap_e, cap_p, out.cpu().numpy(), b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,W,n,b_max,ring,cap", [
+    (256, 1, 40_000, 64, "device", 64),
+    (256, 3, 100_003, 64, "pinned", 64),
+    (64, 2, 12_345, 50, "pinned", 17),
+    (1024, 8, 70_001, 16, "device", 64),
+    (128, 1, 777, 64, "device", 5),        # B < b_max: b = B
+    (512, 3, 513, 64, "pinned", 64),
+])
+def test_burst_loop_matches_oracle_packet_stream(cuda, P, W, n, b_max, ring, cap):
+    rng = np.random.default_rng(P + W + n)
+    x = O.splitmix_normal(n % 97, n) * np.float32(2.0 ** (W - 2))
+    if n > 1000:
+        x[100:140] = 0.0                             # an all-zero-ish stretch, special values
+        x[5] = np.float32(2.5)
+        x[6] = np.float32(-2.5)
+    pe, pp, ref_out, b = O.dummy_packet_stream(x, P=P, batch_max=b_max, num_workers=W)
+    ce, cp, out, b2 = run_bursts(x, P, W, b_max, ring, cuda, rng, cap)
+    assert b == b2
+    assert np.array_equal(ce, pe)
+    assert np.array_equal(cp, pp.view(np.uint32))
+    assert np.array_equal(out.view(np.uint32), ref_out.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_burst_int32_and_argument_checks(cuda):
+    import torch
+    s = sw()
+    P, n = 256, 5_000
+    xi = np.random.default_rng(3).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+    xd = torch.from_numpy(xi).to(cuda)
+    outd = torch.zeros_like(xd)
+    B = O.num_blocks(n, P)
+    pk = torch.zeros(B * P, dtype=torch.int32, device=cuda)
+    ids = list(range(B))
+    bt = s.packet_burst(xd, outd, P, 1, 0, None, ids, [pk.data_ptr() + q * P * 4 for q in ids], [0] * B)
+    s.preprocess_burst(bt)
+    s.postprocess_burst(bt)
+    torch.cuda.synchronize()
+    assert np.array_equal(pk.cpu().numpy().view(np.uint32)[:n], O.bswap32(xi))
+    assert np.array_equal(outd.cpu().numpy(), xi)
+    # a float burst holding q and q + b, a duplicate id, an id past B + b, > MAX_BURST packets
+    x = torch.randn(10_000, device=cuda)
+    o = torch.empty_like(x)
+    Bf = O.num_blocks(10_000, P)
+    recv = torch.zeros(Bf, dtype=torch.int8, device=cuda)
+    ring = torch.zeros(64 * P, dtype=torch.int32, device=cuda)
+    ex = torch.zeros(128, dtype=torch.uint8, device=cuda)
+    for bad in ([3, 3 + 8], [4, 4], [Bf + 8]):
+        bt = s.packet_burst(x, o, P, 1, 8, recv, bad, [ring.data_ptr()] * len(bad), [ex.data_ptr()] * len(bad))
+        with pytest.raises(s.SwitchMLError):
+            s.preprocess_burst(bt)
+    bt = s.packet_burst(x, o, P, 1, 8, recv, [0], [ring.data_ptr()], [ex.data_ptr()])
+    bt.count = 65
+    with pytest.raises(s.SwitchMLError):
+        s.postprocess_burst(bt)

@@ -177,3 +177,64 @@ def test_xgmi_config_validation():
         with pytest.raises(C.ContextError):
             C.start(C.make_config(bandwidth=0, **kw))
         assert C.state() != C.RUNNING
+
+
+def _failing_worker(rank, W, session, fail_rank, q):
+    """Worker `fail_rank` injects a fault on worker thread 0 of every job
+    (backend.dummy.fail_worker_thread); the session is poisoned, so every
+    worker's job fails — none hangs on a barrier, none reports FINISHED —
+    and the jobs after it fail too (no out-of-phase barriers)."""
+    try:
+        _paths()
+        import time
+        from switchml_amd import client as C
+        kw = dict(fail_worker_thread=0) if rank == fail_rank else {}
+        C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=2, packet_numel=256,
+                              max_outstanding_packets=128, mode="bulk", bandwidth=0, device=0, session=session,
+                              timeout_ms=30000, **kw))
+        t0 = time.time()
+        sts = []
+        for j in range(3):
+            x = torch.from_numpy(worker_bucket(rank, 200_000, j)).cuda()
+            job = C.allreduce_async(x)
+            C.wait_for_all_jobs()
+            sts.append(job.status())
+        took = time.time() - t0
+        C.stop()
+        q.put((rank, {"statuses": sts, "seconds": took}, ""))
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, None, traceback.format_exc()[-2000:]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_xgmi_failure_poisons_session(cuda, fail_rank):
+    from switchml_amd import client as C
+    session = "fail-" + uuid.uuid4().hex
+    for rank, res, err in _run(_failing_worker, 2, (session, fail_rank)):
+        assert res is not None, (rank, err)
+        assert res["statuses"] == [C.JOB_FAILED] * 3, (rank, res)
+        assert res["seconds"] < 20, (rank, res)    # failed fast: no barrier timeout waited out
+    assert not os.path.exists(f"/dev/shm/switchml-{session}")
+
+
+@pytest.mark.gpu
+def test_xgmi_replaces_stale_segment(cuda):
+    """A segment left by a crashed run (its worker 0 gone, its barrier counts
+    and attach count stale) is replaced by the next run's worker 0 instead of
+    being joined."""
+    import subprocess
+    import sys
+    session = "stale-" + uuid.uuid4().hex
+    p = subprocess.run([sys.executable, "-c", "import os; print(os.getpid())"], capture_output=True, text=True)
+    dead_pid = int(p.stdout)          # a process that has exited
+    path = f"/dev/shm/switchml-{session}"
+    with open(path, "wb") as f:      # magic "SMLX", W=T=1, stale counters, creator = the dead process
+        import struct
+        hdr = struct.pack("<IIIIQiIII", 0x534D4C58, 2, 1, 256, 1 << 20, dead_pid, 0, 2, 0)
+        f.write(hdr + b"\0" * (1 << 16))
+    for rank, res, err in _run(_client_worker, 2, (1, 256, session, 8192 * 4)):
+        assert res is not None, (rank, err)
+        assert all(res), (rank, res)
+    assert not os.path.exists(path)
