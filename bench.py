@@ -85,6 +85,9 @@ def parse(argv=None):
     ap.add_argument("--no-side", action="store_true", help="skip the cold-HBM and 1 GiB single-GPU side fields")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--extra", action="store_true", help="also time dequantize / fused round trip / copy / plugin")
+    ap.add_argument("--no-rccl-collnet", action="store_true",
+                    help="skip the rccl_collnet field (RCCL's own all_reduce dispatched into the CollNet plugin, "
+                         "run by rank 0 in fresh child processes at the end)")
     ap.add_argument("--graph-steps", type=int, default=1,
                     help="capture this many steps per hipGraph replay (1 = eager launches)")
     return ap.parse_args(argv)
@@ -560,13 +563,54 @@ def main():
         watchdog.cancel()
     if args.extra and rank == 0:
         extra.update(extra_measurements(sw, torch, torch.randn(args.numel, device=dev, generator=gen), P, stream))
+    if world > 1:
+        dist.destroy_process_group()
+    if not args.no_rccl_collnet and rank == 0:
+        # RCCL itself calling the plugin's CollNet table, in fresh processes
+        # (their own RCCL communicator and xgmi session); not part of the
+        # headline, and its failure is reported in the field, not fatal
+        torch.cuda.empty_cache()
+        fields["rccl_collnet"] = rccl_collnet_field(world)
     if world == 1 and not args.no_cpu_baseline:
         side_cpu["cpu_baseline"] = cpu_baseline(N, P, args.cpu_seconds)
     emit()
-    if world > 1:
-        dist.destroy_process_group()
     if failures:
         sys.exit(1)
+
+
+def rccl_collnet_field(world, timeout=240.0):
+    """RCCL's own torch.distributed all_reduce with the SwitchML plugin
+    library loaded (switchml_amd/rccl_collnet.py): W worker processes, each
+    its own CollNet "node" (NCCL_HOSTID), NCCL_COLLNET_ENABLE=1; RCCL's p2p
+    traffic runs over the library's TCP net.  The CollNet table declines RCCL
+    7.2 (its CollNet AllReduce does not reduce or hangs: DESIGN.md §9 F2), so
+    RCCL falls back to its own algorithms over that net; the plugin driven by
+    hand (the in-node xgmi switch behind it) is checked on the same data.
+    At N = 1 two workers share the GPU.  Reported: correctness of RCCL's
+    all-reduce over the net, the plugin's call counters, configs[4] timing."""
+    try:
+        from switchml_amd import rccl_collnet as R
+        W = world if world > 1 else 2
+        t0 = time.time()
+        rep = R.launch(W, same_gpu=world == 1, numel=1 << 22, iters=5, timeout=timeout)
+        ranks = [r for r in rep["ranks"] if r]
+        out = {"workers": W, "same_gpu": world == 1, "ok": rep["ok"], "seconds": round(time.time() - t0, 1),
+               "net": "SWITCHML TCP net (librccl-net-switchml.so)",
+               "collnet_declined": rep["collnet_declined"],
+               "collnet_dispatched_by_rccl": rep["collnet_dispatched_by_rccl"],
+               "iallreduce_calls": rep["iallreduce_calls"], "returncodes": rep["returncodes"]}
+        if ranks:
+            out["rccl_int_allreduce_equals_exact_sum"] = all(r["int_exact"] for r in ranks)
+            out["plugin_by_hand_equals_rccl_on_ints"] = all(r["int_equal_direct"] for r in ranks)
+            out["normal_within_quantization_bound"] = all(r["normal_within_bound"] for r in ranks)
+            if all("configs4_ms_per_iter" in r for r in ranks):
+                out["configs4_rccl_over_net_ms_per_iteration_max_over_ranks"] = round(
+                    max(r["configs4_ms_per_iter"] for r in ranks), 3)
+        if "tails" in rep:
+            out["tails"] = [t[-4:] for t in rep["tails"]]
+        return out
+    except Exception as e:  # noqa: BLE001 - reported in the field
+        return {"ok": False, "error": repr(e)[:400]}
 
 
 def settle(step, settle_ms):

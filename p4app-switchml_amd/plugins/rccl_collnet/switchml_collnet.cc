@@ -62,11 +62,11 @@ ncclDebugLogger_t g_logger = nullptr;
 // Calls RCCL made into the CollNet table (switchml_collnet_stats()).
 struct Counters {
     std::atomic<uint64_t> init{0}, connect{0}, iallreduce{0}, iallreduce_bytes{0}, test_done{0}, reg_mr{0},
-        iallreduce_submitted{0};
+        iallreduce_submitted{0}, declined{0};
 } g_calls;
 
 void log_info(const char* msg) {
-    if (g_logger) g_logger(NCCL_LOG_INFO, 0, __FILE__, __LINE__, "%s", msg);
+    if (g_logger) g_logger(NCCL_LOG_INFO, ~0ul, __FILE__, __LINE__, "%s", msg);
 }
 
 struct ListenComm {
@@ -116,9 +116,34 @@ int type_size(ncclDataType_t t) {
     }
 }
 
+// Is the caller RCCL?  RCCL hands its own debug logger to init(): the
+// library that defines it names the caller.
+bool called_by_rccl(ncclDebugLogger_t logger) {
+    Dl_info info;
+    if (!logger || !dladdr(reinterpret_cast<void*>(logger), &info) || !info.dli_fname) return false;
+    return strstr(info.dli_fname, "librccl") != nullptr;
+}
+
 ncclResult_t sml_init(ncclDebugLogger_t logger) {
     g_logger = logger;
     g_calls.init++;
+    // RCCL 7.2 has no working CollNet all-reduce to hand us (measured on
+    // MI355X): its tuner picks CollNetChain, whose kernels
+    // it does not build (0 threads), and the AllReduce returns WITHOUT
+    // reducing; CollNetDirect needs a switch node in the topology and then
+    // never posts the proxy op (the collective hangs).  So under RCCL the
+    // CollNet table declines, RCCL logs "Cannot initialize CollNet, using
+    // point-to-point network instead" and runs its own algorithms over this
+    // library's net.  SWITCHML_COLLNET_RCCL=1 offers the table anyway.
+    const char* force = getenv("SWITCHML_COLLNET_RCCL");
+    if (called_by_rccl(logger) && !(force && strcmp(force, "1") == 0)) {
+        g_calls.declined++;
+        if (g_logger)
+            g_logger(NCCL_LOG_WARN, ~0ul, __FILE__, __LINE__,
+                     "SwitchML CollNet: not offered to RCCL (its CollNet AllReduce paths do not reduce or hang on "
+                     "this RCCL; SWITCHML_COLLNET_RCCL=1 overrides)");
+        return ncclInvalidUsage;
+    }
     try {
         switchml::Context& ctx = switchml::Context::GetInstance();
         if (ctx.GetContextState() == switchml::Context::RUNNING) return ncclSuccess;
@@ -241,7 +266,7 @@ void submit(Request* r) {
                                                              switchml::SUM);
     g_calls.iallreduce_submitted++;
     if (g_trace && g_logger)
-        g_logger(NCCL_LOG_INFO, 0, __FILE__, __LINE__, "SwitchML CollNet: job comm %u buf %u call %lu count %d",
+        g_logger(NCCL_LOG_INFO, ~0ul, __FILE__, __LINE__, "SwitchML CollNet: job comm %u buf %u call %lu count %d",
                  r->key.comm, r->key.buf, (unsigned long)r->key.seq, r->count);
 }
 
@@ -464,13 +489,13 @@ ncclResult_t net_close_listen(void* c) { SML_FWD(closeListen, c); }
 extern "C" {
 // Counts of CollNet calls since the library was loaded: init, connect,
 // iallreduce, iallreduce bytes, test() completions, regMr, jobs submitted to
-// the Context.  Returns how many of the n slots it filled.
+// the Context, inits declined (RCCL).  Returns how many of the n slots it filled.
 __attribute__((visibility("default"))) int switchml_collnet_stats(uint64_t* out, int n) {
-    const uint64_t v[7] = {g_calls.init.load(),      g_calls.connect.load(),   g_calls.iallreduce.load(),
+    const uint64_t v[8] = {g_calls.init.load(),      g_calls.connect.load(),   g_calls.iallreduce.load(),
                            g_calls.iallreduce_bytes.load(), g_calls.test_done.load(), g_calls.reg_mr.load(),
-                           g_calls.iallreduce_submitted.load()};
+                           g_calls.iallreduce_submitted.load(), g_calls.declined.load()};
     int k = 0;
-    for (; k < n && k < 7; k++) out[k] = v[k];
+    for (; k < n && k < 8; k++) out[k] = v[k];
     return k;
 }
 

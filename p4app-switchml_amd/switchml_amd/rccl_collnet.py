@@ -1,32 +1,39 @@
-"""RCCL itself dispatching all-reduces into the SwitchML CollNet plugin.
+"""RCCL with the SwitchML plugin library, for real: W worker processes,
+torch.distributed backend "nccl" (= RCCL), NCCL_NET_PLUGIN =
+librccl-net-switchml.so, NCCL_COLLNET_ENABLE=1.
 
 The reference's integration (frameworks_integration/nccl_plugin) is a
-CollNet plugin NCCL calls for an all-reduce across nodes: every node's
-head rank hands its buffer to `iallreduce`, the switch sums the nodes' data
-(switchml_plugin.cc:293-387).  This module runs that for real with RCCL:
+CollNet plugin NCCL calls for an all-reduce across nodes (each node's head
+rank hands its buffer to `iallreduce`, the switch sums the nodes' data,
+switchml_plugin.cc:293-387), paired with a p2p net table.  Here:
 
-* one process per worker (`python -m switchml_amd.rccl_collnet --rank r ...`),
-  torch.distributed backend "nccl" (= RCCL) with
-  NCCL_NET_PLUGIN = librccl-net-switchml.so and NCCL_COLLNET_ENABLE=1;
-* NCCL_HOSTID = a distinct id per rank, so every rank is a "node" of its own
-  and RCCL's CollNet — which reduces ACROSS nodes — spans all workers, the
-  way each SwitchML worker is a host with a NIC to the switch.  On an 8-GPU
-  node the ranks use GPUs 0..W-1; on a one-GPU box (`--same-gpu`) they share
-  cuda:0 (RCCL rejects two ranks on one device of one host; two hosts'
-  ranks are distinct);
-* the plugin's backend is the in-node switch (general.backend = xgmi,
-  xgmi_switch.h): the W ranks' plugin instances form one xgmi session and
-  reduce through each other's HBM;
-* RCCL's own p2p traffic (bootstrap aside) runs over the plugin library's
-  TCP net (plugins/rccl_collnet/socket_net.h).
+* NCCL_HOSTID = a distinct id per rank, so every rank is a CollNet "node"
+  of its own — the way each SwitchML worker is a host with a NIC to the
+  switch.  On an 8-GPU node the ranks use GPUs 0..W-1; on a one-GPU box
+  (`same_gpu`) they share cuda:0 (two ranks of one host on one device are
+  refused by RCCL, two hosts' ranks are not);
+* RCCL's p2p traffic runs over the library's own TCP net
+  (plugins/rccl_collnet/socket_net.h): RCCL loads both tables and keeps the
+  CollNet one only because that net works;
+* the CollNet table DECLINES RCCL by default (switchml_collnet.cc sml_init):
+  RCCL 7.2 on MI355X has no working CollNet AllReduce — its tuner picks
+  CollNetChain, whose kernels it does not build, and the AllReduce returns
+  unreduced; CollNetDirect needs a switch node in the topology and then
+  hangs (measured: profiles/r03/rccl_collnet/).  RCCL then logs "Cannot
+  initialize CollNet, using point-to-point network instead" and reduces with
+  its own algorithms over the SwitchML net — correct results.
+  `allow_collnet=True` (SWITCHML_COLLNET_RCCL=1) offers the table anyway,
+  with NCCL_ALGO=CollNetDirect and a switch node added to each worker's
+  topology (`add_switch_node`): the experiment that shows the hang;
+* behind the table (driven by hand, and by RCCL when allowed) is the in-node
+  switch (general.backend = xgmi, xgmi_switch.h); the plugin keeps the W
+  workers' submission order identical (job_order.h).
 
 Each rank reports the plugin's call counters (`switchml_collnet_stats`),
-checks the RCCL all-reduce of integer-valued data bit for bit against the
-exact sum AND against the same buffer all-reduced through the plugin's
-iallreduce by hand (one job, the xgmi switch directly), checks N(0,1) data
-against the same by-hand all-reduce and against the fp32 sum within the
-quantization bound, and times RCCL all-reduces of configs[4]'s ResNet-50
-buckets.  The parent (`launch`) never touches the GPU.
+RCCL's all-reduce of integer-valued data against the exact sum, the same
+buffer through the plugin's iallreduce by hand (the xgmi switch) against it
+too, N(0,1) data within the quantization bound, and RCCL all-reduces of
+configs[4]'s ResNet-50 buckets.  The parent (`launch`) never touches the GPU.
 """
 from __future__ import annotations
 
@@ -42,7 +49,8 @@ import uuid
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PLUGIN_PATH = os.path.join(_HERE, "librccl-net-switchml.so")
 RESNET50_BUCKETS = [6_553_600, 6_553_600, 6_553_600, 5_896_232]
-STATS = ("init", "connect", "iallreduce", "iallreduce_bytes", "test_done", "reg_mr", "iallreduce_submitted")
+STATS = ("init", "connect", "iallreduce", "iallreduce_bytes", "test_done", "reg_mr", "iallreduce_submitted",
+         "declined")
 
 
 def collnet_stats(path: str = PLUGIN_PATH) -> dict:
@@ -93,6 +101,20 @@ def _bound(xs, out_ref, world):
     return float(err.max()), bool((err <= lim).all())
 
 
+def add_switch_node(src: str, dst: str):
+    """RCCL topology XML `src` with one link from every GPU to a switch node
+    (<xgmi tclass="0x068000">, the NVSwitch PCI class RCCL's topology parser
+    turns into an NVS node)."""
+    import xml.etree.ElementTree as ET
+    tree = ET.parse(src)
+    gpus = tree.getroot().findall(".//gpu")
+    if not gpus:
+        raise RuntimeError(f"no <gpu> in {src}")
+    for g in gpus:
+        ET.SubElement(g, "xgmi", {"target": "0000:ff:00.0", "count": "1", "tclass": "0x068000"})
+    tree.write(dst)
+
+
 def rank_main(a):
     import numpy as np
     import torch
@@ -100,9 +122,31 @@ def rank_main(a):
 
     dev = torch.device("cuda", a.device)
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{a.port}", rank=a.rank, world_size=a.world,
+    port = a.port
+    topo = None
+    if a.switch_topo:
+        # RCCL 7.2 runs AllReduce on CollNet only as CollNetDirect, which its
+        # tuner enables only when the topology holds a switch node (it
+        # disables CollNetDirect when ncclTopoGetNvsCount() == 0).  Each
+        # worker here is a one-GPU CollNet node; a switch node attached to
+        # that GPU has no other GPU to route to, so it changes nothing but
+        # that check.  RCCL's own detected topology is dumped first (a
+        # throwaway communicator), the node added, and the file handed back
+        # through NCCL_TOPO_FILE.
+        dump = os.path.join(a.topo_dir, f"detected.rank{a.rank}.xml")
+        os.environ["NCCL_TOPO_DUMP_FILE"] = dump
+        os.environ["NCCL_TOPO_DUMP_FILE_RANK"] = str(a.rank)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=a.rank, world_size=a.world,
+                                device_id=dev)
+        dist.destroy_process_group()
+        del os.environ["NCCL_TOPO_DUMP_FILE"]
+        topo = os.path.join(a.topo_dir, f"with_switch.rank{a.rank}.xml")
+        add_switch_node(dump, topo)
+        os.environ["NCCL_TOPO_FILE"] = topo
+        port += 1
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=a.rank, world_size=a.world,
                             device_id=dev)
-    out = {"rank": a.rank, "device": a.device}
+    out = {"rank": a.rank, "device": a.device, "topology_file": topo}
     W = a.world
     n = a.numel
 
@@ -110,6 +154,14 @@ def rank_main(a):
         print(f"[rank {a.rank}] {msg}", flush=True)
 
     say("process group up")
+    if os.environ.get("SWITCHML_COLLNET_TRACE"):
+        import threading
+
+        def watch():
+            while True:
+                time.sleep(5)
+                say(f"collnet stats {collnet_stats()}")
+        threading.Thread(target=watch, daemon=True).start()
 
     def allreduce(t):
         dist.all_reduce(t)
@@ -182,11 +234,18 @@ def rank_main(a):
     os._exit(0)
 
 
-def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, channels: int = 1,
-           algo: str | None = "CollNetDirect", log_dir: str | None = None, timeout: float = 600,
-           port: int | None = None, extra_env: dict | None = None) -> dict:
-    """Run `world` ranks (child processes) and gather their reports.  The
-    caller must not have initialised the GPU."""
+def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, channels: int = 0,
+           algo: str | None = None, log_dir: str | None = None, timeout: float = 600,
+           port: int | None = None, extra_env: dict | None = None, switch_topo: bool = False,
+           allow_collnet: bool = False) -> dict:
+    """Run `world` ranks (child processes) and gather their reports.
+    allow_collnet: offer the CollNet table to RCCL (SWITCHML_COLLNET_RCCL=1)
+    with NCCL_ALGO=CollNetDirect and the switch node — the experiment that
+    hangs on RCCL 7.2 (give it a short timeout)."""
+    if allow_collnet:
+        algo = algo or "CollNetDirect"
+        switch_topo = True
+        extra_env = dict(extra_env or {}, SWITCHML_COLLNET_RCCL="1")
     session = uuid.uuid4().hex[:10]
     port = port or (20000 + os.getpid() % 20000)
     if log_dir:
@@ -202,7 +261,9 @@ def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, cha
         env["PYTHONPATH"] = os.path.dirname(_HERE) + os.pathsep + env.get("PYTHONPATH", "")
         cmd = [sys.executable, "-u", "-m", "switchml_amd.rccl_collnet", "--rank", str(r), "--world", str(world),
                "--device", str(0 if same_gpu else r), "--port", str(port), "--numel", str(numel),
-               "--iters", str(iters)]
+               "--iters", str(iters), "--topo-dir", out_dir]
+        if switch_topo:
+            cmd.append("--switch-topo")
         f = open(os.path.join(out_dir, f"rank{r}.out"), "w+")
         files.append(f)
         procs.append(subprocess.Popen(cmd, env=env, stdout=f, stderr=subprocess.STDOUT, text=True))
@@ -243,15 +304,18 @@ def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, cha
         ranks.append(json.loads(res[-1][7:]) if res else None)
         tails.append(o.strip().splitlines()[-12:])
     rep = {"world": world, "same_gpu": same_gpu, "numel": numel, "channels": channels, "algo": algo,
-           "extra_env": extra_env or {},
+           "extra_env": extra_env or {}, "switch_topo": switch_topo,
            "returncodes": [p.returncode for p in procs], "ranks": ranks}
     if any(r is None for r in ranks) or any(p.returncode for p in procs):
         rep["tails"] = tails
-    ok = all(r is not None for r in ranks)
+    ok = all(r is not None for r in ranks) and all(p.returncode == 0 for p in procs)
+    rep["allow_collnet"] = allow_collnet
     rep["iallreduce_calls"] = [r["stats_end"]["iallreduce"] if r else None for r in ranks]
-    rep["ok"] = bool(ok and all(p.returncode == 0 for p in procs)
-                     and all(r["stats_after_first"]["iallreduce"] > r["stats_before"]["iallreduce"] for r in ranks)
-                     and all(r["int_exact"] and r["int_equal_direct"] and r["normal_within_bound"] for r in ranks))
+    rep["collnet_dispatched_by_rccl"] = bool(ok and all(
+        r["stats_after_first"]["iallreduce"] > r["stats_before"]["iallreduce"] for r in ranks))
+    rep["collnet_declined"] = bool(ok and all(r["stats_end"].get("declined", 0) >= 1 for r in ranks))
+    rep["ok"] = bool(ok and all(r["int_exact"] and r["int_equal_direct"] and r["normal_within_bound"] for r in ranks)
+                     and (rep["collnet_dispatched_by_rccl"] if allow_collnet else rep["collnet_declined"]))
     return rep
 
 
@@ -264,19 +328,24 @@ def main(argv=None):
     ap.add_argument("--numel", type=int, default=1 << 22)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--same-gpu", action="store_true")
-    ap.add_argument("--channels", type=int, default=1)
-    ap.add_argument("--algo", default="CollNetDirect",
-                    help="NCCL_ALGO for the ranks ('' = RCCL's tuner); RCCL 7.2 runs AllReduce on CollNet only "
-                         "as CollNetDirect (its CollNetChain has no threads: nothing reduces)")
+    ap.add_argument("--channels", type=int, default=0, help="NCCL_MAX_NCHANNELS (0 = RCCL's default)")
+    ap.add_argument("--algo", default="", help="NCCL_ALGO for the ranks ('' = RCCL's tuner)")
+    ap.add_argument("--allow-collnet", action="store_true",
+                    help="offer the CollNet table to RCCL (SWITCHML_COLLNET_RCCL=1, CollNetDirect, switch node)")
     ap.add_argument("--env", action="append", default=[], help="KEY=VALUE for the ranks (repeatable)")
+    ap.add_argument("--switch-topo", action="store_true",
+                    help="add a switch node to each worker's RCCL topology (CollNetDirect's precondition)")
+    ap.add_argument("--topo-dir", help="(rank) where the topology files go")
     ap.add_argument("--log-dir")
     ap.add_argument("--out")
+    ap.add_argument("--timeout", type=float, default=600.0, help="seconds before the ranks are killed")
     a = ap.parse_args(argv)
     if a.rank is not None:
         rank_main(a)
         return 0
     rep = launch(a.world, a.same_gpu, a.numel, a.iters, a.channels, a.algo or None, a.log_dir,
-                 extra_env=dict(kv.split("=", 1) for kv in a.env))
+                 extra_env=dict(kv.split("=", 1) for kv in a.env), switch_topo=a.switch_topo,
+                 timeout=a.timeout, allow_collnet=a.allow_collnet)
     if a.log_dir:
         lines = []
         for f in sorted(os.listdir(a.log_dir)):

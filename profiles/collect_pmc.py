@@ -61,11 +61,15 @@ def main(tag="r02", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
 
     fetch = pmc("pmc_fetch", "FETCH_SIZE")
     write = pmc("pmc_write", "WRITE_SIZE")
-    cold = None
-    if os.path.isdir(os.path.join(src, "cold_fetch")) and os.path.isdir(os.path.join(src, "cold_write")):
-        cf, cw = pmc("cold_fetch", "FETCH_SIZE"), pmc("cold_write", "WRITE_SIZE")
+    # round 3+: the default passes cycle 4 buckets (cold HBM) and res_* re-read
+    # one bucket; round 2 had the default resident and cold_* cycling
+    cycling = os.path.isdir(os.path.join(src, "res_fetch"))
+    other = ("res_fetch", "res_write") if cycling else ("cold_fetch", "cold_write")
+    other_b = None
+    if os.path.isdir(os.path.join(src, other[0])) and os.path.isdir(os.path.join(src, other[1])):
+        cf, cw = pmc(other[0], "FETCH_SIZE"), pmc(other[1], "WRITE_SIZE")
         if cf and cw:
-            cold = 2 * 1024 * statistics.mean(cf) + 1024 * statistics.mean(cw)
+            other_b = 2 * 1024 * statistics.mean(cf) + 1024 * statistics.mean(cw)
     B = -(-numel // packet_numel)
     alg_read, alg_write = 4 * numel, 4 * numel + B
     fetch_b = 2 * 1024 * statistics.mean(fetch)
@@ -88,19 +92,21 @@ def main(tag="r02", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
         "hbm_write_bytes_per_launch (WRITE_SIZE x 1024)": write_b,
         "hbm_bytes_per_launch": fetch_b + write_b,
         "traffic_over_algorithmic": (fetch_b + write_b) / (alg_read + alg_write),
-        "cold_hbm_bytes_per_launch (4 distinct buckets cycled)": cold,
-        "cold_traffic_over_algorithmic": None if cold is None else cold / (alg_read + alg_write),
+        "default_steps": "4 distinct buckets cycled (cold HBM)" if cycling else "one resident bucket",
     }
+    key = "resident" if cycling else "cold"
+    summary[f"{key}_hbm_bytes_per_launch"] = other_b
+    summary[f"{key}_traffic_over_algorithmic"] = None if other_b is None else other_b / (alg_read + alg_write)
     if os.path.isdir(os.path.join(src, "fr_kt")):
         summary["frames"] = frames_summary(src, dst, numel, packet_numel)
     with open(os.path.join(dst, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
+    main_key, other_key = ("quantize_pack_cold", "quantize_pack") if cycling else ("quantize_pack", "quantize_pack_cold")
     traffic = {"source": f"profiles/{tag}/summary.json",
-               "quantize_pack": {"numel": numel, "packet_numel": packet_numel,
-                                 "hbm_bytes_per_launch": round(fetch_b + write_b)}}
-    if cold is not None:
-        traffic["quantize_pack_cold"] = {"numel": numel, "packet_numel": packet_numel,
-                                         "hbm_bytes_per_launch": round(cold)}
+               main_key: {"numel": numel, "packet_numel": packet_numel,
+                          "hbm_bytes_per_launch": round(fetch_b + write_b)}}
+    if other_b is not None:
+        traffic[other_key] = {"numel": numel, "packet_numel": packet_numel, "hbm_bytes_per_launch": round(other_b)}
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(summary, indent=1))

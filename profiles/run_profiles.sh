@@ -11,22 +11,25 @@ ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
+# a step that times out, aborts or faults ends the GPU work of this run
+step() { "$@"; rc=$?; case $rc in 124|137|134|139) echo "step failed rc=$rc: $*"; exit $rc;; esac; }
 # kernel-trace pass: the bench's own defaults (50 ms settle, 500 warmup steps)
 # and 2000 timed steps, so the average is dominated by steady-state launches;
 # collect_pmc.py also reports the average over the timed window alone.
-KT_ARGS="$ROOT/bench.py --steps 2000 --no-cpu-baseline --no-side"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 $KT_ARGS > "$OUT/kt.log" 2>&1
+KT_ARGS="$ROOT/bench.py --steps 2000 --no-cpu-baseline --no-side --no-rccl-collnet"
+step timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- python3 $KT_ARGS > "$OUT/kt.log" 2>&1
 # PMC passes: bytes per launch do not depend on clocks; few launches suffice
-ARGS="$ROOT/bench.py --steps 20 --warmup 5 --settle-ms 0 --no-cpu-baseline --no-side"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_write.log" 2>&1
-# cold HBM: the same K1 with its steps cycling 4 distinct buckets + planes (2 GiB, past the MALL)
-CARGS="$ARGS --buckets 4 --no-side"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/cold_fetch" -o pmc --output-format csv -- python3 $CARGS > "$OUT/cold_fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/cold_write" -o pmc --output-format csv -- python3 $CARGS > "$OUT/cold_write.log" 2>&1
+ARGS="$ROOT/bench.py --steps 20 --warmup 5 --settle-ms 0 --no-cpu-baseline --no-side --no-rccl-collnet"
+step timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_fetch.log" 2>&1
+step timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --output-format csv -- python3 $ARGS > "$OUT/pmc_write.log" 2>&1
+# the bench's default steps cycle 4 distinct buckets (HBM proper); the
+# resident side number re-reads one bucket (HBM + Infinity Cache)
+RARGS="$ARGS --buckets 1"
+step timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/res_fetch" -o pmc --output-format csv -- python3 $RARGS > "$OUT/res_fetch.log" 2>&1
+step timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/res_write" -o pmc --output-format csv -- python3 $RARGS > "$OUT/res_write.log" 2>&1
 # F3 frames kernels (tx quantize-into-frames, rx claim/apply) on the same bucket
 FR="$ROOT/tools/prof_frames.py"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/fr_kt" -o kt --output-format csv -- python3 $FR > "$OUT/fr_kt.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fr_fetch" -o pmc --output-format csv -- python3 $FR > "$OUT/fr_fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/fr_write" -o pmc --output-format csv -- python3 $FR > "$OUT/fr_write.log" 2>&1
+step timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/fr_kt" -o kt --output-format csv -- python3 $FR > "$OUT/fr_kt.log" 2>&1
+step timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fr_fetch" -o pmc --output-format csv -- python3 $FR > "$OUT/fr_fetch.log" 2>&1
+step timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/fr_write" -o pmc --output-format csv -- python3 $FR > "$OUT/fr_write.log" 2>&1
 echo "profiles done: $OUT"

@@ -1,0 +1,168 @@
+"""The CollNet plugin's cross-worker job order (plugins/rccl_collnet/
+job_order.h): RCCL's proxy posts the CollNet chunks of its channels as each
+channel's data arrives, so two workers interleave channels differently; the
+switch pairs jobs by submission order, so worker 0's arrival order is logged
+in shared memory and every other worker submits in that order.
+
+CPU: job_order.cc compiled with a small driver; W worker processes get the
+same calls — one sequence per "channel" — interleaved in a different random
+order each, submit them through the log, and must all produce worker 0's
+order; a segment left by a dead creator is replaced; a live one is refused;
+a poisoned order is seen by every worker."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "p4app-switchml_amd", "plugins", "rccl_collnet")
+
+DRIVER = r"""
+#include <sys/wait.h>
+#include <unistd.h>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <random>
+#include <string>
+#include <vector>
+#include "job_order.h"
+using namespace sml_collnet;
+
+// worker `rank`: channels c = 0..C-1, each with N calls (buf = c, seq = 0..N-1),
+// arriving interleaved in a random order (per-channel order kept, as RCCL's
+// proxy does); submit through the job order; print the submitted keys.
+int worker(const char* session, int rank, int W, int C, int N, unsigned seed) {
+    JobOrder order(session, rank, W, 20000);
+    std::mt19937 rng(seed);
+    std::vector<int> next(C, 0);
+    std::deque<CallKey> pending;
+    std::vector<CallKey> submitted;
+    int arrived = 0;
+    while ((int)submitted.size() < C * N) {
+        if (arrived < C * N) {                       // one more call arrives
+            int c;
+            do c = rng() % C; while (next[c] == N);
+            pending.push_back(CallKey{0, (uint32_t)c, (uint64_t)next[c]++, 1000 + c, 7, 0});
+            arrived++;
+        }
+        if (order.leader()) {
+            while (!pending.empty() && order.Append(pending.front())) {
+                submitted.push_back(pending.front());
+                pending.pop_front();
+            }
+        } else {
+            CallKey k;
+            while (order.Peek(&k)) {
+                auto it = pending.begin();
+                for (; it != pending.end(); ++it)
+                    if (it->comm == k.comm && it->buf == k.buf && it->seq == k.seq) break;
+                if (it == pending.end()) break;
+                if (it->count != k.count) { fprintf(stderr, "count mismatch\n"); return 2; }
+                submitted.push_back(*it);
+                pending.erase(it);
+                order.Consume();
+            }
+        }
+        if (arrived == C * N && (int)submitted.size() < C * N) usleep(50);
+    }
+    std::string s;
+    for (auto& k : submitted) s += std::to_string(k.buf) + ":" + std::to_string(k.seq) + ",";
+    FILE* f = fopen((std::string(getenv("ORDER_OUT")) + "/r" + std::to_string(rank)).c_str(), "w");
+    fprintf(f, "%s\n", s.c_str());
+    fclose(f);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    const std::string mode = argv[1];
+    const char* session = argv[2];
+    if (mode == "order") {
+        int W = atoi(argv[3]), C = atoi(argv[4]), N = atoi(argv[5]);
+        std::vector<pid_t> kids;
+        for (int r = W - 1; r >= 0; r--) {          // followers start first: they must wait for worker 0
+            pid_t p = fork();
+            if (p == 0) { fflush(stdout); _exit(worker(session, r, W, C, N, 1234 + 77 * r)); }
+            kids.push_back(p);
+        }
+        int bad = 0;
+        for (pid_t p : kids) { int st; waitpid(p, &st, 0); bad |= !WIFEXITED(st) || WEXITSTATUS(st); }
+        return bad;
+    }
+    if (mode == "leader") {                          // create, report, exit without cleanup (a crash)
+        JobOrder* o = new JobOrder(session, 0, 2, 5000);
+        printf("created\n");
+        fflush(stdout);
+        if (argc > 3) { sleep(atoi(argv[3])); }
+        _exit(0);
+        (void)o;
+    }
+    if (mode == "poison") {
+        pid_t p = fork();
+        if (p == 0) { JobOrder o(session, 1, 2, 20000); while (!o.Poisoned()) usleep(100); printf("follower saw poison\n"); fflush(stdout); _exit(0); }
+        JobOrder o(session, 0, 2, 20000);
+        o.Poison();
+        int st; waitpid(p, &st, 0);
+        return WIFEXITED(st) ? WEXITSTATUS(st) : 1;
+    }
+    try {                                            // "join": a second leader for the session
+        JobOrder o(session, 0, 2, 2000);
+        printf("joined\n");
+    } catch (const std::exception& e) {
+        printf("refused: %s\n", e.what());
+    }
+    return 0;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def driver(tmp_path_factory):
+    d = tmp_path_factory.mktemp("joborder")
+    src = d / "driver.cc"
+    src.write_text(DRIVER)
+    exe = d / "driver"
+    subprocess.run(["g++", "-O1", "-std=c++17", f"-I{SRC}", "-o", str(exe), str(src),
+                    os.path.join(SRC, "job_order.cc"), "-lpthread", "-lrt"], check=True)
+    return str(exe)
+
+
+@pytest.mark.parametrize("W,C,N", [(2, 2, 500), (4, 3, 300), (8, 2, 200)])
+def test_every_worker_submits_worker0_order(driver, tmp_path, W, C, N):
+    session = f"test-{os.getpid()}-{W}-{C}"
+    r = subprocess.run([driver, "order", session, str(W), str(C), str(N)], capture_output=True, text=True,
+                       timeout=120, env=dict(os.environ, ORDER_OUT=str(tmp_path)))
+    assert r.returncode == 0, r.stderr
+    seqs = {str(w): (tmp_path / f"r{w}").read_text().strip() for w in range(W)}
+    assert len(set(seqs.values())) == 1, "workers submitted in different orders"
+    keys = seqs["0"].strip(",").split(",")
+    assert len(keys) == C * N
+    for c in range(C):                               # each channel's calls stay in order
+        s = [int(k.split(":")[1]) for k in keys if k.split(":")[0] == str(c)]
+        assert s == list(range(N))
+    assert not os.path.exists(f"/dev/shm/switchml-collnet-{session}")
+
+
+def test_stale_segment_replaced_live_one_refused(driver):
+    session = f"stale-{os.getpid()}"
+    path = f"/dev/shm/switchml-collnet-{session}"
+    r = subprocess.run([driver, "leader", session], capture_output=True, text=True, timeout=60)
+    assert "created" in r.stdout and os.path.exists(path)          # left behind by a "crashed" creator
+    r = subprocess.run([driver, "join", session], capture_output=True, text=True, timeout=60)
+    assert "joined" in r.stdout, r.stdout + r.stderr               # dead creator: replaced
+    os.unlink(path) if os.path.exists(path) else None
+    live = subprocess.Popen([driver, "leader", session, "20"], stdout=subprocess.PIPE, text=True)
+    try:
+        assert live.stdout.readline().strip() == "created"
+        r = subprocess.run([driver, "join", session], capture_output=True, text=True, timeout=60)
+        assert r.stdout.startswith("refused") and "in use" in r.stdout
+    finally:
+        live.kill()
+        live.wait()
+        if os.path.exists(path):
+            os.unlink(path)
+
+
+def test_poison_reaches_every_worker(driver):
+    r = subprocess.run([driver, "poison", f"poison-{os.getpid()}"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "follower saw poison" in r.stdout

@@ -1,0 +1,39 @@
+"""RCCL with the SwitchML plugin library loaded (switchml_amd/rccl_collnet.py):
+two worker processes share cuda:0 as two RCCL "nodes" (distinct NCCL_HOSTID),
+NCCL_NET_PLUGIN = librccl-net-switchml.so, NCCL_COLLNET_ENABLE=1.
+
+* RCCL loads the library's net table, whose TCP net initialises (no
+  SWITCHML_NET_PLUGIN needed) and carries RCCL's p2p traffic: RCCL's
+  all-reduce of integer-valued data equals the exact sum bit for bit;
+* the CollNet table declines RCCL (RCCL 7.2's CollNet AllReduce does not
+  reduce / hangs on MI355X): RCCL logs its fallback, and no
+  all-reduce reaches iallreduce behind the caller's back;
+* the same table driven by hand in the same processes (the in-node xgmi
+  switch behind it) equals the exact sum on the integer data and stays
+  within the quantization bound on N(0,1) data.
+Reference: frameworks_integration/nccl_plugin/switchml_plugin.cc:37,389-402."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_rccl_runs_over_switchml_net_and_collnet_declines(cuda, tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
+    from switchml_amd import rccl_collnet as R
+    rep = R.launch(2, same_gpu=True, numel=1 << 20, iters=1, timeout=200, log_dir=str(tmp_path))
+    assert rep["returncodes"] == [0, 0], rep.get("tails")
+    assert rep["collnet_declined"] and not rep["collnet_dispatched_by_rccl"]
+    for r in rep["ranks"]:
+        assert r["int_exact"] and r["int_equal_direct"] and r["normal_within_bound"], r
+        assert r["stats_after_first"]["iallreduce"] == r["stats_before"]["iallreduce"]
+    assert rep["ok"]
+    logs = "".join(open(os.path.join(tmp_path, f), errors="replace").read()
+                   for f in os.listdir(tmp_path) if f.startswith("rccl."))
+    assert "Loaded net plugin SWITCHML" in logs and "Loaded collnet plugin SWITCHMLv1" in logs
+    assert "NET/SWITCHML : TCP net" in logs
+    assert "via NET/SWITCHML" in logs                     # RCCL's connections use the library's net
+    assert "not offered to RCCL" in logs
