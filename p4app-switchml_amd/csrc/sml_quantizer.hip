@@ -396,14 +396,20 @@ static void launch_quant_p(uint32_t P, uint32_t U, bool nts, dim3 grid, hipStrea
 // 2-slice tiles are level on cold HBM and lose up to 11 % resident.
 static std::atomic<uint32_t> g_quant_slices{4};
 
-// Payload planes of at least this many bytes take non-temporal stores
-// (sml_set_payload_nt_threshold; UINT64_MAX = never, 0 = always).  Measured,
-// one bucket re-read every step (profiles/r02c/ab_store_size*.json): up to
-// 256 MiB default-policy stores win (7.13 vs 6.35 TB/s at 256 MiB: the
-// planes stay in the 256 MiB Infinity Cache); from 288 MiB on, where they
-// cannot, non-temporal stores win by 5 % (6.33-6.41 vs 6.01-6.11 TB/s at
-// 288 MiB-1 GiB).  So: non-temporal past the Infinity Cache's size.
-static std::atomic<uint64_t> g_nt_threshold{(256ull << 20) + 1};
+// Payload planes (and K4 / round-trip fp32 outputs) of at least this many
+// bytes take non-temporal stores (sml_set_payload_nt_threshold; UINT64_MAX =
+// never, 0 = always).  Measured on cold HBM — steps cycling distinct buckets,
+// the pattern of a real job where a plane is written once and handed on
+// (profiles/r03/ab_cold_policy*.json, interleaved medians): non-temporal
+// stores win at 64 / 128 / 256 MiB planes for K1 (+4.1 / +3.5 / +4.6 %), K4
+// (+5.6 / +6.3 / +4.5 %) and the fused round trip (+4.2 / +3.1 / +3.5 %).
+// Default-policy stores win only when ONE plane is rewritten step after step
+// (it then stays in the 256 MiB Infinity Cache: K1 7.13 vs 6.31 TB/s at
+// 256 MiB, 6.54 vs 6.09 at 128 MiB; level at 64 MiB).  So planes from a
+// quarter of the Infinity Cache on stream non-temporally; smaller ones (a
+// framework's 25 MiB gradient buckets) keep the default policy, so their
+// next reader can find them in the cache.  Bytes are identical either way.
+static std::atomic<uint64_t> g_nt_threshold{64ull << 20};
 
 static uint32_t quant_slices(uint32_t P) {
     const uint32_t need = P > 256 ? P / 256 : 1;

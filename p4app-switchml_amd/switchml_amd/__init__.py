@@ -206,9 +206,9 @@ def set_grid_limit(max_workgroups: int) -> int:
 
 
 def set_payload_nt_threshold(nbytes: int) -> int:
-    """Payload planes of at least `nbytes` bytes take non-temporal stores in
-    K1/K3 (default: larger than the 256 MiB Infinity Cache; 2**64-1 = never,
-    0 = always); returns the previous threshold."""
+    """Payload planes (and K4 / round-trip outputs) of at least `nbytes`
+    bytes take non-temporal stores (default 64 MiB, a quarter of the Infinity
+    Cache; 2**64-1 = never, 0 = always); returns the previous threshold."""
     return int(lib().sml_set_payload_nt_threshold(nbytes))
 
 

@@ -103,6 +103,7 @@ def test_quantize_tile_slices_invariant(sw, P):
     W, n = 3, 200_003
     x_np = O.splitmix_normal(P + 5, n + 1)
     xd = torch.from_numpy(x_np).cuda()
+    orig = sw.set_payload_nt_threshold(2 ** 64 - 1)       # the library default, restored below
     try:
         for off in (0, 1):
             xs, xn = xd[off:off + n], x_np[off:off + n]
@@ -127,19 +128,20 @@ def test_quantize_tile_slices_invariant(sw, P):
                     assert np.array_equal(rne.cpu().numpy().view(np.uint32), want_rne), tag
     finally:
         sw.set_quantize_tile_slices(0)
-        sw.set_payload_nt_threshold((256 << 20) + 1)
+        sw.set_payload_nt_threshold(orig)
 
 
 @pytest.mark.parametrize("P", [64, 256, 1024])
 def test_output_store_policy_invariant(sw, P):
     """K1, K4 and the fused round trip with their output planes written
-    non-temporally (sml_set_payload_nt_threshold(0): what planes larger than
-    the Infinity Cache get) and with default-policy stores: the same bytes
+    non-temporally (sml_set_payload_nt_threshold(0): what planes of 64 MiB
+    and more get) and with default-policy stores: the same bytes
     as the oracle, aligned and 4-byte-offset slices."""
     import torch
     W, n = 3, 300_007
     x_np = O.splitmix_normal(P + 77, n + 1)
     xd = torch.from_numpy(x_np).cuda()
+    orig = sw.set_payload_nt_threshold(2 ** 64 - 1)       # the library default, restored below
     try:
         for off in (0, 1):
             xs, xn = xd[off:off + n], x_np[off:off + n]
@@ -159,4 +161,4 @@ def test_output_store_policy_invariant(sw, P):
                 assert np.array_equal(out.cpu().numpy().view(np.uint32), dq.view(np.uint32)), (off, nt)
                 assert np.array_equal(rt.cpu().numpy().view(np.uint32), dq.view(np.uint32)), (off, nt)
     finally:
-        sw.set_payload_nt_threshold((256 << 20) + 1)
+        sw.set_payload_nt_threshold(orig)
