@@ -516,6 +516,7 @@ def main():
             side["resident"] = bucket_measure(sw, torch, args.numel, P, stream, nbuf=1)
         else:
             side["cold_hbm"] = bucket_measure(sw, torch, args.numel, P, stream, nbuf=4)
+        side["copy_ceiling"] = copy_ceiling(sw, torch, args.numel, stream, nbuf=nb, k1_ms=kern_ms_max)
         side["configs3_1gpu"] = job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev)
     if world > 1 and not args.no_side:
         side["weak_256MiB_per_gpu"] = weak_measure(sw, torch, dist, args.numel, P, stream, dev, world)
@@ -570,7 +571,7 @@ def main():
         # (their own RCCL communicator and xgmi session); not part of the
         # headline, and its failure is reported in the field, not fatal
         torch.cuda.empty_cache()
-        fields["rccl_collnet"] = rccl_collnet_field(world)
+        fields["rccl_collnet"] = rccl_collnet_field(world, same_gpu=world == 1 or rehearse)
     if world == 1 and not args.no_cpu_baseline:
         side_cpu["cpu_baseline"] = cpu_baseline(N, P, args.cpu_seconds)
     emit()
@@ -578,7 +579,7 @@ def main():
         sys.exit(1)
 
 
-def rccl_collnet_field(world, timeout=240.0):
+def rccl_collnet_field(world, same_gpu=False, timeout=240.0):
     """RCCL's own torch.distributed all_reduce with the SwitchML plugin
     library loaded (switchml_amd/rccl_collnet.py): W worker processes, each
     its own CollNet "node" (NCCL_HOSTID), NCCL_COLLNET_ENABLE=1; RCCL's p2p
@@ -592,9 +593,9 @@ def rccl_collnet_field(world, timeout=240.0):
         from switchml_amd import rccl_collnet as R
         W = world if world > 1 else 2
         t0 = time.time()
-        rep = R.launch(W, same_gpu=world == 1, numel=1 << 22, iters=5, timeout=timeout)
+        rep = R.launch(W, same_gpu=same_gpu, numel=1 << 22, iters=5, timeout=timeout)
         ranks = [r for r in rep["ranks"] if r]
-        out = {"workers": W, "same_gpu": world == 1, "ok": rep["ok"], "seconds": round(time.time() - t0, 1),
+        out = {"workers": W, "same_gpu": same_gpu, "ok": rep["ok"], "seconds": round(time.time() - t0, 1),
                "net": "SWITCHML TCP net (librccl-net-switchml.so)",
                "collnet_declined": rep["collnet_declined"],
                "collnet_dispatched_by_rccl": rep["collnet_dispatched_by_rccl"],
@@ -664,6 +665,33 @@ def bucket_measure(sw, torch, N, P, stream, nbuf=4, reps=200):
     return {"buckets": nbuf, "bucket_MiB": N * 4 >> 20, "kernel_ms": round(t * 1e3, 5),
             "achieved_GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
             "note": note}
+
+
+def copy_ceiling(sw, torch, N, stream, nbuf=4, reps=200, k1_ms=None):
+    """The practical HBM ceiling for K1's access pattern: sml_stream_copy (the
+    same 1024-element tiles, XCD order and 16-B non-temporal accesses, no
+    arithmetic) moving the same 4N read + 4N written bytes, its steps cycling
+    the same number of distinct buckets as the headline."""
+    g = torch.Generator(device=stream.device)
+    g.manual_seed(99)
+    xs = [torch.randn(N, device=stream.device, generator=g) for _ in range(nbuf)]
+    ys = [torch.empty_like(x) for x in xs]
+    i = [0]
+
+    def fn():
+        k = i[0]
+        i[0] = (k + 1) % nbuf
+        sw.stream_copy(xs[k], ys[k], stream=stream)
+
+    settle(fn, 30.0)
+    t = time_launches(torch, fn, stream, reps)
+    out = {"buckets": nbuf, "kernel_ms": round(t * 1e3, 5), "GBps": round(8 * N / t / 1e9, 1),
+           "frac_of_peak": round(8 * N / t / 1e9 / HBM_PEAK_GBPS, 4)}
+    if k1_ms:
+        out["k1_time_over_copy_time"] = round(k1_ms / (t * 1e3), 4)
+    out["note"] = ("a plain non-temporal copy of the same bytes in K1's tile shape, steps cycling the same buckets: "
+                   "what the HBM delivers to this access pattern")
+    return out
 
 
 def job_measure(sw, torch, job_numel, P, stream, dev, reps=50):

@@ -87,6 +87,23 @@ def rank_env(rank: int, world: int, device: int, session: str, channels: int, al
     return env
 
 
+def worker_env(parent: dict, rank: int, world: int, device: int, session: str, channels: int = 0,
+               algo: str | None = None, log_dir: str | None = None, extra_env: dict | None = None) -> dict:
+    """A worker's environment: the parent's, minus what a launcher put there
+    for ITS ranks — under torch.distributed.run, TORCHELASTIC_USE_AGENT_STORE
+    makes every rank of a tcp:// rendezvous a store client with no server (a
+    silent hang), and RANK / WORLD_SIZE / MASTER_* name the wrong group —
+    plus rank_env and `extra_env`."""
+    env = {k: v for k, v in parent.items()
+           if not k.startswith(("TORCHELASTIC_", "ROLE_", "GROUP_"))
+           and k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                         "SWITCHML_NET_PLUGIN")}
+    env.update(rank_env(rank, world, device, session, channels, algo, log_dir))
+    env.update(extra_env or {})
+    env["PYTHONPATH"] = os.path.dirname(_HERE) + os.pathsep + env.get("PYTHONPATH", "")
+    return env
+
+
 def _bound(xs, out_ref, world):
     """|out - sum x| <= per-element quantization bound, with the global block
     exponent e (max over workers): each worker rounds to 2^(e-31) * W units
@@ -254,11 +271,7 @@ def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, cha
     out_dir = log_dir or tempfile.mkdtemp(prefix="sml_rccl_collnet_")
     procs, files = [], []
     for r in range(world):
-        env = dict(os.environ)
-        env.update(rank_env(r, world, 0 if same_gpu else r, session, channels, algo, log_dir))
-        env.pop("SWITCHML_NET_PLUGIN", None)
-        env.update(extra_env or {})
-        env["PYTHONPATH"] = os.path.dirname(_HERE) + os.pathsep + env.get("PYTHONPATH", "")
+        env = worker_env(os.environ, r, world, 0 if same_gpu else r, session, channels, algo, log_dir, extra_env)
         cmd = [sys.executable, "-u", "-m", "switchml_amd.rccl_collnet", "--rank", str(r), "--world", str(world),
                "--device", str(0 if same_gpu else r), "--port", str(port), "--numel", str(numel),
                "--iters", str(iters), "--topo-dir", out_dir]

@@ -37,3 +37,22 @@ def test_rccl_runs_over_switchml_net_and_collnet_declines(cuda, tmp_path):
     assert "NET/SWITCHML : TCP net" in logs
     assert "via NET/SWITCHML" in logs                     # RCCL's connections use the library's net
     assert "not offered to RCCL" in logs
+
+
+def test_worker_env_drops_launcher_state():
+    """Workers started from a torch.distributed.run rank must not inherit its
+    agent-store rendezvous (a tcp:// init would wait for a store server that
+    never starts) or its RANK / WORLD_SIZE / MASTER_*."""
+    sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
+    from switchml_amd import rccl_collnet as R
+    parent = {"TORCHELASTIC_USE_AGENT_STORE": "True", "TORCHELASTIC_RESTART_COUNT": "0", "RANK": "3",
+              "WORLD_SIZE": "8", "LOCAL_RANK": "3", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29500",
+              "GROUP_RANK": "0", "SWITCHML_NET_PLUGIN": "/x.so", "PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    env = R.worker_env(parent, 1, 2, 1, "s1", extra_env={"FOO": "1"})
+    for k in ("TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_RESTART_COUNT", "RANK", "WORLD_SIZE", "LOCAL_RANK",
+              "MASTER_ADDR", "MASTER_PORT", "GROUP_RANK", "SWITCHML_NET_PLUGIN"):
+        assert k not in env, k
+    assert env["PATH"] == "/usr/bin" and env["FOO"] == "1"
+    assert env["NCCL_NET_PLUGIN"].endswith("librccl-net-switchml.so") and env["NCCL_COLLNET_ENABLE"] == "1"
+    assert env["NCCL_HOSTID"] == "switchml-worker-s1-1"
+    assert "rank = 1" in env["SWITCHML_CONFIG_INI"] and "device = 1" in env["SWITCHML_CONFIG_INI"]
