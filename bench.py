@@ -26,7 +26,11 @@ each checked (bit-equal to each other, and within the quantization bound of
 an fp32 all-reduce of the same buckets) and set against its xGMI bound; and
 configs4_plugin: the ResNet-50 buckets through the CollNet plugin table on an
 N-rank communicator over the xgmi backend (device and pinned host buffers).
-A failed check or an exception exits non-zero.
+The exit status is 1 only when the headline's own check fails (the timed
+planes differ from the committed digests) or the headline cannot be
+measured; a failed or timed-out diagnostic field (switch paths, plugin,
+rccl_collnet) is reported in the line under "diagnostic_failures" and in its
+own field, so one experimental path cannot void the measured headline.
 
 Units: value / roofline.achieved = ALGORITHMIC bytes per second: 4N read
 (fp32 in) + 4N written (int32 payload) + B written (int8 exponents),
@@ -436,6 +440,7 @@ def main():
     del xs, pls, exs, x, payload, exps
 
     failures = [] if ok else ["self_check: " + check_note]
+    diag_failures = []          # diagnostic fields: reported, not fatal (module docstring)
     side, fields, extra = {}, {}, {}
 
     def emit():
@@ -508,6 +513,8 @@ def main():
             line["cpu_baseline"] = side_cpu["cpu_baseline"]
         if failures:
             line["failures"] = failures
+        if diag_failures:
+            line["diagnostic_failures"] = diag_failures
         print(json.dumps(line), flush=True)
 
     side_cpu = {}
@@ -532,11 +539,11 @@ def main():
         # switch) is where a hang could happen; past the deadline the run
         # reports what it has, with the failure, and every rank exits 1.
         def on_timeout():
-            failures.append(f"timeout: the switch / plugin phase exceeded {args.exchange_timeout:g} s")
+            diag_failures.append(f"timeout: the switch / plugin phase exceeded {args.exchange_timeout:g} s")
             try:
                 emit()
             finally:
-                os._exit(1)
+                os._exit(1 if failures else 0)
         watchdog = threading.Timer(args.exchange_timeout, on_timeout)
         watchdog.daemon = True
         watchdog.start()
@@ -548,7 +555,7 @@ def main():
         for k in ("switchsim", "p2p_switch", "xgmi_switch"):
             f = fields.get(k, {})
             if "error" in f or not f.get("verified", False):
-                failures.append(f"{k}: {f.get('error', 'not verified')}")
+                diag_failures.append(f"{k}: {f.get('error', 'not verified')}")
     if world > 1 and not args.no_plugin:
         # configs[4] on every GPU at once: each rank hands the ResNet-50 buckets
         # to its own plugin instance, on an N-rank communicator whose backend
@@ -556,10 +563,10 @@ def main():
         try:
             fields["configs4_plugin"] = plugin_measure_ranks(torch, dist, dev, world)
             if not fields["configs4_plugin"]["placements_agree_all_ranks"]:
-                failures.append("configs4_plugin: device and pinned-host results differ")
+                diag_failures.append("configs4_plugin: device and pinned-host results differ")
         except Exception as e:  # noqa: BLE001
             fields["configs4_plugin"] = {"error": repr(e)[:400]}
-            failures.append(f"configs4_plugin: {fields['configs4_plugin']['error']}")
+            diag_failures.append(f"configs4_plugin: {fields['configs4_plugin']['error']}")
     if watchdog is not None:
         watchdog.cancel()
     if args.extra and rank == 0:
@@ -572,6 +579,8 @@ def main():
         # headline, and its failure is reported in the field, not fatal
         torch.cuda.empty_cache()
         fields["rccl_collnet"] = rccl_collnet_field(world, same_gpu=world == 1 or rehearse)
+        if not fields["rccl_collnet"].get("ok", False):
+            diag_failures.append("rccl_collnet: " + fields["rccl_collnet"].get("error", "not ok"))
     if world == 1 and not args.no_cpu_baseline:
         side_cpu["cpu_baseline"] = cpu_baseline(N, P, args.cpu_seconds)
     emit()
@@ -579,7 +588,7 @@ def main():
         sys.exit(1)
 
 
-def rccl_collnet_field(world, same_gpu=False, timeout=240.0):
+def rccl_collnet_field(world, same_gpu=False, timeout=120.0):
     """RCCL's own torch.distributed all_reduce with the SwitchML plugin
     library loaded (switchml_amd/rccl_collnet.py): W worker processes, each
     its own CollNet "node" (NCCL_HOSTID), NCCL_COLLNET_ENABLE=1; RCCL's p2p
@@ -587,11 +596,14 @@ def rccl_collnet_field(world, same_gpu=False, timeout=240.0):
     7.2 (its CollNet AllReduce does not reduce or hangs: DESIGN.md §9 F2), so
     RCCL falls back to its own algorithms over that net; the plugin driven by
     hand (the in-node xgmi switch behind it) is checked on the same data.
-    At N = 1 two workers share the GPU.  Reported: correctness of RCCL's
-    all-reduce over the net, the plugin's call counters, configs[4] timing."""
+    Two workers at every N (GPUs 0 and 1 when the node has them; at N = 1
+    they share the GPU): the field shows RCCL running over the plugin's net
+    and the table's decision, and is kept short so the driver's N = 8 run is
+    not spent on it.  Reported: correctness of RCCL's all-reduce over the
+    net, the plugin's call counters, configs[4] timing."""
     try:
         from switchml_amd import rccl_collnet as R
-        W = world if world > 1 else 2
+        W = 2
         t0 = time.time()
         rep = R.launch(W, same_gpu=same_gpu, numel=1 << 22, iters=5, timeout=timeout)
         ranks = [r for r in rep["ranks"] if r]
