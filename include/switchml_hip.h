@@ -243,6 +243,22 @@ typedef struct {
 sml_status_t sml_preprocess_burst(const sml_packet_burst* burst, void* stream);
 sml_status_t sml_postprocess_burst(const sml_packet_burst* burst, void* stream);
 
+/* The receive loop's two calls on one buffer in ONE launch: for every
+ * RECEIVED packet q of the burst, PostprocessSingle(q) and then — when packet
+ * q + b exists (q + b < B + b for FLOAT32, q + b < B for INT32; b =
+ * batch_num_ltus, the packet window, for both types here) —
+ * PreprocessSingle(q + b) into the same entries[i] / extras[i]: DpdkWorkerThread's
+ * receive loop, PostprocessSingle then ReusePacket (dpdk_worker_thread.cc:
+ * 300-345, dpdk_worker_thread_utils.inc:134,177), and DummyWorkerThread's
+ * loop trip (dummy_worker_thread.cc:106-163).  Bit-identical to
+ * sml_postprocess_burst followed by sml_preprocess_burst of the ids q + b.
+ * With SML_FLAG_PROCESS_PACKET the dummy backend's ProcessPacket (all P words
+ * x num_workers, wrapping, exponent unchanged; dummy_backend.cc:72-84) is
+ * applied to each packet first, and all P words are written back (the words
+ * the preprocess does not rewrite keep the processed values). */
+#define SML_FLAG_PROCESS_PACKET 0x8u
+sml_status_t sml_exchange_burst(const sml_packet_burst* burst, void* stream);
+
 /* Plane sharing for the peer-to-peer switch: export the allocation holding
  * d_ptr as an IPC handle of sml_ipc_handle_bytes() bytes plus d_ptr's byte
  * offset inside it; open a peer's handle in this process (returns the

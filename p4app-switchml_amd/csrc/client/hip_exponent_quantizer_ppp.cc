@@ -42,6 +42,7 @@ void HipExponentQuantizerPPP::check(int status, const char* what) const {
 uint64_t HipExponentQuantizerPPP::SetupJobSlice(JobSlice* job_slice) {
     // ppp.cc:54-62
     job_slice_ = job_slice;
+    pool_probe_ = nullptr;
     const uint64_t bytes = job_slice->slice.numel * DataTypeSize(job_slice->slice.data_type);
     total_main_num_ltus_ = (bytes + ltu_size_ - 1) / ltu_size_;
     batch_num_ltus_ = std::min<uint64_t>(total_main_num_ltus_, batch_max_num_ltus_);
@@ -192,28 +193,48 @@ void HipExponentQuantizerPPP::PostprocessSingle(uint64_t ltu_id, void* entries_p
 // go to the kernel in place (pinned host memory at its device address — the
 // same offset applies to every buffer of the pool); pageable memory takes the
 // per-packet path, which stages.
-void HipExponentQuantizerPPP::burst(bool pre, uint32_t n, const uint64_t* ltu_ids, void* const* entries,
+void HipExponentQuantizerPPP::burst(BurstKind kind, uint32_t n, const uint64_t* ltu_ids, void* const* entries,
                                    void* const* extras) {
     if (n == 0) return;
     const Tensor& s = job_slice_->slice;
+    const bool flt = s.data_type == FLOAT32;
+    const uint64_t total = total_main_num_ltus_ + (flt ? batch_num_ltus_ : 0);
     ensure_single_buffers();
-    const PacketMem m = packet_mem(entries[0]);
+    // one pool per slice: the query is cached for the slice (SetupJobSlice resets it)
+    if (entries[0] != pool_probe_) {
+        pool_probe_ = entries[0];
+        const PacketMem pm = packet_mem(entries[0]);
+        pool_dev_ = pm.dev;
+        pool_host_ = pm.host;
+    }
+    const PacketMem m{pool_dev_, pool_host_};
     if (!m.dev) {
-        for (uint32_t i = 0; i < n; i++)
-            pre ? PreprocessSingle(ltu_ids[i], entries[i], extras ? extras[i] : nullptr)
-                : PostprocessSingle(ltu_ids[i], entries[i], extras ? extras[i] : nullptr);
+        if (kind == BurstKind::kProcessExchange)
+            throw SwitchMLFatal("ProcessPostprocessReuseBurst: packet buffers must be device-addressable");
+        for (uint32_t i = 0; i < n; i++) {
+            void* x = extras ? extras[i] : nullptr;
+            if (kind != BurstKind::kPre) PostprocessSingle(ltu_ids[i], entries[i], x);
+            if (kind == BurstKind::kPre) PreprocessSingle(ltu_ids[i], entries[i], x);
+            else if (kind == BurstKind::kExchange && ltu_ids[i] + batch_num_ltus_ < total)
+                PreprocessSingle(ltu_ids[i] + batch_num_ltus_, entries[i], x);
+        }
         return;
     }
     const intptr_t delta = static_cast<char*>(m.dev) - static_cast<char*>(entries[0]);
+    const bool exchange = kind == BurstKind::kExchange || kind == BurstKind::kProcessExchange;
     sml_packet_burst b{};
     b.in = static_cast<const float*>(s.in_ptr);
     b.out = static_cast<float*>(s.out_ptr);
     b.numel = s.numel;
     b.packet_numel = (uint32_t)ltu_numel_;
     b.num_workers = config_.general_.num_workers;
-    b.data_type = s.data_type == FLOAT32 ? SML_FLOAT32 : SML_INT32;
-    b.batch_num_ltus = s.data_type == FLOAT32 ? batch_num_ltus_ : 0;
+    b.data_type = flt ? SML_FLOAT32 : SML_INT32;
+    // the exchange needs the window for INT32 too (the next packet is q + b)
+    b.batch_num_ltus = flt || exchange ? batch_num_ltus_ : 0;
     b.recv_exps = d_recv_exps_;
+    b.flags = kind == BurstKind::kProcessExchange ? SML_FLAG_PROCESS_PACKET : 0u;
+    const char* what = kind == BurstKind::kPre ? "sml_preprocess_burst"
+                       : kind == BurstKind::kPost ? "sml_postprocess_burst" : "sml_exchange_burst";
     for (uint32_t i0 = 0; i0 < n; i0 += SML_MAX_BURST) {
         b.count = std::min<uint32_t>(SML_MAX_BURST, n - i0);
         for (uint32_t i = 0; i < b.count; i++) {
@@ -221,20 +242,34 @@ void HipExponentQuantizerPPP::burst(bool pre, uint32_t n, const uint64_t* ltu_id
             b.entries[i] = static_cast<char*>(entries[i0 + i]) + delta;
             b.extras[i] = extras && extras[i0 + i] ? static_cast<char*>(extras[i0 + i]) + delta : nullptr;
         }
-        check(pre ? sml_preprocess_burst(&b, stream_) : sml_postprocess_burst(&b, stream_),
-              pre ? "sml_preprocess_burst" : "sml_postprocess_burst");
+        check(kind == BurstKind::kPre ? sml_preprocess_burst(&b, stream_)
+              : kind == BurstKind::kPost ? sml_postprocess_burst(&b, stream_) : sml_exchange_burst(&b, stream_),
+              what);
     }
     if (m.host || !stream_ordered_) hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 
 void HipExponentQuantizerPPP::PreprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries,
                                               void* const* extras) {
-    burst(true, n, ltu_ids, entries, extras);
+    burst(BurstKind::kPre, n, ltu_ids, entries, extras);
 }
 
 void HipExponentQuantizerPPP::PostprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries,
                                                void* const* extras) {
-    burst(false, n, ltu_ids, entries, extras);
+    burst(BurstKind::kPost, n, ltu_ids, entries, extras);
+}
+
+void HipExponentQuantizerPPP::PostprocessReuseBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries,
+                                                    void* const* extras, uint64_t batch, uint64_t total_ltus) {
+    const bool flt = job_slice_->slice.data_type == FLOAT32;
+    if (batch != batch_num_ltus_ || total_ltus != total_main_num_ltus_ + (flt ? batch_num_ltus_ : 0))
+        throw SwitchMLFatal("PostprocessReuseBurst: batch / total_ltus differ from the slice's b / B (+ b)");
+    burst(BurstKind::kExchange, n, ltu_ids, entries, extras);
+}
+
+void HipExponentQuantizerPPP::ProcessPostprocessReuseBurst(uint32_t n, const uint64_t* ltu_ids,
+                                                           void* const* entries, void* const* extras) {
+    burst(BurstKind::kProcessExchange, n, ltu_ids, entries, extras);
 }
 
 void HipExponentQuantizerPPP::ExponentsBulk(void* exps_plane) {

@@ -37,6 +37,15 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     // (HBM or pinned host memory); pageable ones take the per-packet path.
     void PreprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras) override;
     void PostprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras) override;
+    // One launch per SML_MAX_BURST received packets (sml_exchange_burst);
+    // batch / total_ltus must be this slice's b and B (+ b for FLOAT32).
+    void PostprocessReuseBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras,
+                               uint64_t batch, uint64_t total_ltus) override;
+    // The same with the dummy backend's ProcessPacket (x num_workers,
+    // dummy_backend.cc:72-84) applied to each packet first, in the same launch:
+    // the loopback backend's device ring runs a whole ring pass as one launch.
+    void ProcessPostprocessReuseBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries,
+                                      void* const* extras);
 
     // A per-LTU / burst call returns with its packet complete, as the
     // reference's does (the caller hands a packet to the NIC next).  A caller
@@ -56,7 +65,8 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
   private:
     void check(int status, const char* what) const;
     void ensure_single_buffers();
-    void burst(bool pre, uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras);
+    enum class BurstKind { kPre, kPost, kExchange, kProcessExchange };
+    void burst(BurstKind kind, uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras);
 
     JobSlice* job_slice_ = nullptr;
     uint64_t total_main_num_ltus_ = 0;  // B
@@ -70,6 +80,11 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     int32_t* d_stage_ = nullptr;
     int8_t* d_stage_exp_ = nullptr;
     bool stream_ordered_ = false;
+    // where the slice's packet pool lives (burst calls): the first buffer
+    // pointer seen, and its packet_mem() answer
+    void* pool_probe_ = nullptr;
+    void* pool_dev_ = nullptr;
+    bool pool_host_ = true;
 };
 
 }  // namespace switchml

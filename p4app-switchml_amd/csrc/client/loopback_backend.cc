@@ -118,15 +118,17 @@ void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerStat
     // The reference handles one packet per loop trip: packet p comes back,
     // ProcessPacket, PostprocessSingle(p), PreprocessSingle(p + b) into the
     // same ring slot.  Slots are independent, so the packets of one pass over
-    // the ring (slots s0 .. s0 + w - 1, w <= b) go as bursts — the way a DPDK
-    // worker handles an rx burst and refills a tx burst — with the same calls
-    // per slot in the same order: ProcessPacket(window), PostprocessBurst,
-    // PreprocessBurst.  A device ring stays stream-ordered (no host sync per
-    // burst); a host ring completes each burst before the CPU touches it.
+    // the ring (slots s0 .. s0 + w - 1, w <= b) go as one burst — the way a
+    // DPDK worker handles an rx burst and refills its mbufs — with the same
+    // calls per slot in the same order: PostprocessReuseBurst (post of p, pre
+    // of p + b into the slot).  An HBM ring runs the whole trip, ProcessPacket
+    // included, as ONE launch per pass and stays stream-ordered (no host sync);
+    // a host ring completes each burst before the CPU touches it.
     const uint16_t W = cfg.general_.num_workers;
     const bool dev_ring = where == "device";
+    const bool proc = cfg.backend_.dummy.process_packets;
     ppp.SetStreamOrdered(dev_ring);
-    std::vector<uint64_t> ids(b), nids(b);
+    std::vector<uint64_t> ids(b);
     std::vector<void*> ents(b), exs(b);
     for (uint64_t p = 0; p < b; p++) {
         ids[p] = p;
@@ -136,18 +138,15 @@ void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerStat
     ppp.PreprocessBurst((uint32_t)b, ids.data(), ents.data(), exs.data());
     for (uint64_t p0 = 0; p0 < total; p0 += b) {
         const uint64_t w = std::min<uint64_t>(b, total - p0);   // p0 % b == 0: slots 0 .. w - 1
-        if (cfg.backend_.dummy.process_packets && dev_ring)
-            sml_ok(sml_loopback_aggregate(ring, w * P, W, 0, ppp.stream()), "sml_loopback_aggregate");
-        else if (cfg.backend_.dummy.process_packets)
+        for (uint64_t s = 0; s < w; s++) ids[s] = p0 + s;
+        if (proc && dev_ring) {
+            ppp.ProcessPostprocessReuseBurst((uint32_t)w, ids.data(), ents.data(), exs.data());
+            continue;
+        }
+        if (proc)
             for (uint64_t i = 0; i < w * P; i++)
                 ring[i] = (int32_t)__builtin_bswap32(__builtin_bswap32((uint32_t)ring[i]) * (uint32_t)W);
-        uint32_t nn = 0;
-        for (uint64_t s = 0; s < w; s++) {
-            ids[s] = p0 + s;
-            if (p0 + s + b < total) nids[nn++] = p0 + s + b;
-        }
-        ppp.PostprocessBurst((uint32_t)w, ids.data(), ents.data(), exs.data());
-        ppp.PreprocessBurst(nn, nids.data(), ents.data(), exs.data());   // slots 0 .. nn - 1
+        ppp.PostprocessReuseBurst((uint32_t)w, ids.data(), ents.data(), exs.data(), b, total);
     }
     ppp.SetStreamOrdered(false);
 }

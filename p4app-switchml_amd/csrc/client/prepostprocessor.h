@@ -66,6 +66,22 @@ class PrePostProcessor {
     virtual void PostprocessBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras) {
         for (uint32_t i = 0; i < n; i++) PostprocessSingle(ltu_ids[i], entries[i], extras ? extras[i] : nullptr);
     }
+    // The receive loop's two calls on one buffer: for every received packet
+    // q = ltu_ids[i], PostprocessSingle(q) and then, when q + batch <
+    // total_ltus, PreprocessSingle(q + batch) into the same entries[i] /
+    // extras[i] — DpdkWorkerThread's PostprocessSingle + ReusePacket
+    // (dpdk_worker_thread.cc:300-345, dpdk_worker_thread_utils.inc:134,177) and
+    // DummyWorkerThread's loop trip (dummy_worker_thread.cc:106-163).
+    // total_ltus = B, plus b when NeedsExtraBatch().  This default is that
+    // loop; the HIP PPP runs it as one launch per burst.
+    virtual void PostprocessReuseBurst(uint32_t n, const uint64_t* ltu_ids, void* const* entries,
+                                       void* const* extras, uint64_t batch, uint64_t total_ltus) {
+        for (uint32_t i = 0; i < n; i++) {
+            void* x = extras ? extras[i] : nullptr;
+            PostprocessSingle(ltu_ids[i], entries[i], x);
+            if (ltu_ids[i] + batch < total_ltus) PreprocessSingle(ltu_ids[i] + batch, entries[i], x);
+        }
+    }
 
     Numel ltu_size() const { return ltu_size_; }
 

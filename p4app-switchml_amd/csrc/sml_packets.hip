@@ -25,7 +25,11 @@
 // 262-298).  Bit-identical to calling the per-packet entry points in order;
 // the only ordering the reference's loop guarantees — packet q + b is
 // preprocessed after packet q is postprocessed — is the caller's, across
-// bursts (a burst holding both q and q + b is refused).
+// bursts (a burst holding both q and q + b is refused), or the exchange
+// burst's, which does both for a received packet in one wave (post of q,
+// then pre of q + b into the same buffer: one launch per rx burst).
+#include <algorithm>
+
 #include "sml_host.h"
 
 namespace sml {
@@ -124,8 +128,134 @@ __global__ __launch_bounds__(kBlockThreads) void k_postprocess_burst(sml_packet_
     if (q < B && lane == 0) a.recv_exps[q] = *static_cast<const int8_t*>(a.extras[i]);
 }
 
-// Host checks shared by both entry points.
-static sml_status_t check_burst(const sml_packet_burst* a) {
+// One wave per RECEIVED packet q, the DPDK receive loop's two calls on one
+// mbuf in one launch (dpdk_worker_thread.cc:300-345: PostprocessSingle of the
+// packet, then ReusePacket -> PreprocessSingle of pkt_id + b into the same
+// buffer, dpdk_worker_thread_utils.inc:134,177), optionally preceded by the
+// dummy backend's ProcessPacket (x W on all P words, dummy_backend.cc:72-84):
+//   FLOAT32  post: q >= b: block q - b dequantized with recv_exps[q - b];
+//                  q < B: the packet's exponent byte -> recv_exps[q]
+//            pre (q < B, i.e. q + b < B + b): block q quantized with that same
+//                  received exponent (its n real words; a partial block's tail
+//                  keeps the packet's words), exponent of block q + b into
+//                  byte 0 of the extra slot when q + b < B
+//   INT32    post: block q byte-swapped into out; pre (q + b < B): block q + b
+//                  byte-swapped into the buffer (b = the packet window)
+// Every load of the packet is waited for before its buffer is written: the
+// reads and the writes of one buffer may cross PCIe (pinned mbufs), where a
+// posted write may overtake an outstanding read.
+template <int P, bool RNE, bool PROC>
+__global__ __launch_bounds__(kBlockThreads) void k_exchange_burst(sml_packet_burst a) {
+    constexpr int U = P > 256 ? P / 256 : 1;
+    constexpr int kLanes = P >= 256 ? kWave : P / 4;
+    const uint32_t i = blockIdx.x * kWavesPerBlock + wave_index();
+    if (i >= a.count) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool act = lane < kLanes;
+    const uint64_t q = a.pkt_ids[i];
+    const uint64_t B = (a.numel + P - 1) / P;
+    const uint64_t b = a.batch_num_ltus;
+    const bool flt = a.data_type == SML_FLOAT32;
+    auto real = [&](uint64_t k) -> uint64_t { return a.numel - k * P < P ? a.numel - k * P : P; };
+    uint32_t* ent = static_cast<uint32_t*>(a.entries[i]);
+    const int8_t* ext = static_cast<const int8_t*>(a.extras[i]);
+
+    // what each half touches: post reads words [0, n_post) of the packet
+    // (all P under PROC), pre rewrites words [0, n_pre)
+    const bool post_pay = flt ? q >= b : true;
+    const uint64_t n_post = !post_pay ? 0 : real(flt ? q - b : q);
+    const bool pre = flt ? q < B : q + b < B;
+    const uint64_t n_pre = !pre ? 0 : real(flt ? q : q + b);
+    const bool pre_exp = flt && q + b < B;
+    const uint64_t n_read = PROC ? P : n_post;
+
+    // ---- every load up front
+    uint32_t w[U][4];
+    f4 xq[U], xe[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const uint64_t j = (uint64_t)u * 256 + lane * 4 + t;
+            w[u][t] = act && j < n_read ? ent[j] : 0u;
+        }
+        const uint64_t j = (uint64_t)u * 256 + lane * 4;
+        if (flt) {
+            xq[u] = act && pre ? load4_guarded(a.in + q * P + j, j, n_pre) : mkf4(0, 0, 0, 0);
+            xe[u] = act && pre_exp ? load4_guarded(a.in + (q + b) * P + j, j, real(q + b)) : mkf4(0, 0, 0, 0);
+        } else {
+            const float* src = a.in + (q + b) * P + j;   // int32 words, read as raw bits
+            xq[u] = act && pre ? load4_guarded(src, j, n_pre) : mkf4(0, 0, 0, 0);
+        }
+    }
+    const int e_recv = flt && q < B ? (int)*ext : 0;     // the packet's (aggregated) exponent byte
+    const int e_post = flt && q >= b ? (int)a.recv_exps[q - b] : 0;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+    // ---- ProcessPacket, postprocess
+    const uint32_t W = a.num_workers;
+    if constexpr (PROC) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) w[u][t] = bswap(bswap(w[u][t]) * W);
+    }
+    if (post_pay) {
+        const uint64_t k = flt ? q - b : q;
+        const float s = flt ? scale_for(W, e_post) : 0.0f;
+        uint32_t* out = reinterpret_cast<uint32_t*>(a.out) + k * P;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint64_t j = (uint64_t)u * 256 + lane * 4 + t;
+                if (act && j < n_post)
+                    out[j] = flt ? __float_as_uint(dequantize1(bswap(w[u][t]), s)) : bswap(w[u][t]);
+            }
+    }
+    if (flt && q < B && lane == 0) a.recv_exps[q] = (int8_t)e_recv;
+
+    // ---- preprocess of q + b into the same buffer
+    if (pre) {
+        const float s = flt ? scale_for(W, e_recv) : 0.0f;
+        const uint64_t body = n_pre / 16 * 16;              // VCL=1: RNE on the 16-aligned body
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t j = (uint64_t)u * 256 + lane * 4;
+            u4 v;
+            if (flt) {
+                v = quantize4<RNE>(xq[u], s, j, body);
+            } else {
+                v = mku4(__float_as_uint(xq[u].x), __float_as_uint(xq[u].y), __float_as_uint(xq[u].z),
+                         __float_as_uint(xq[u].w));
+            }
+            const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                if (act && j + t < n_pre) w[u][t] = bswap(vv[t]);
+        }
+    }
+    // the buffer's words: the new packet's, or (PROC) the processed ones
+    const uint64_t n_write = PROC ? P : n_pre;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const uint64_t j = (uint64_t)u * 256 + lane * 4 + t;
+            if (act && j < n_write) ent[j] = w[u][t];
+        }
+    if (pre_exp) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int u = 0; u < U; u++) m = umax(m, max4(xe[u]));
+        m = group_max<256>(m);                              // idle lanes hold 0
+        if (lane == 0) *static_cast<int8_t*>(a.extras[i]) = (int8_t)exponent_of(m);
+    }
+}
+
+// Host checks shared by the entry points.  `window`: the exchange burst's
+// packet window b applies to INT32 slices too (the next packet is q + b).
+static sml_status_t check_burst(const sml_packet_burst* a, bool window = false) {
     if (!a) return SML_ERR_INVALID_ARG;
     if (!valid_packet(a->packet_numel)) return SML_ERR_UNSUPPORTED;
     if (a->count > SML_MAX_BURST || a->num_workers == 0) return SML_ERR_INVALID_ARG;
@@ -135,15 +265,28 @@ static sml_status_t check_burst(const sml_packet_burst* a) {
     const uint64_t P = a->packet_numel;
     const uint64_t B = sml_num_blocks(a->numel, (uint32_t)P);
     const bool flt = a->data_type == SML_FLOAT32;
-    const uint64_t b = flt ? a->batch_num_ltus : 0;
-    if (flt && (!a->recv_exps || b > B)) return SML_ERR_INVALID_ARG;
+    const uint64_t b = flt || window ? a->batch_num_ltus : 0;
+    if ((flt || window) && b > B) return SML_ERR_INVALID_ARG;
+    if (window && b == 0) return SML_ERR_INVALID_ARG;
+    if (flt && !a->recv_exps) return SML_ERR_INVALID_ARG;
+    const uint64_t total = flt ? B + b : B;
+    bool run = true;   // ids q0, q0 + 1, ... (a ring pass): distinct, and q0 + b is not among them if count <= b
     for (uint32_t i = 0; i < a->count; i++) {
         const uint64_t q = a->pkt_ids[i];
-        if (q >= B + b || !a->entries[i] || (flt && q < B && !a->extras[i])) return SML_ERR_INVALID_ARG;
-        for (uint32_t j = 0; j < i; j++)   // distinct, and never q and q + b together
-            if (a->pkt_ids[j] == q || (b && (a->pkt_ids[j] == q + b || a->pkt_ids[j] + b == q)))
-                return SML_ERR_INVALID_ARG;
+        if (q >= total || !a->entries[i] || (flt && q < B && !a->extras[i])) return SML_ERR_INVALID_ARG;
+        if (window && flt && q + b < B && !a->extras[i]) return SML_ERR_INVALID_ARG;
+        run = run && q == a->pkt_ids[0] + i;
     }
+    if (run && (b == 0 || a->count <= b)) return SML_OK;
+    // any other order: distinct, and never q and q + b together (sorted copy)
+    uint64_t ids[SML_MAX_BURST];
+    std::copy(a->pkt_ids, a->pkt_ids + a->count, ids);
+    std::sort(ids, ids + a->count);
+    for (uint32_t i = 1; i < a->count; i++)
+        if (ids[i] == ids[i - 1]) return SML_ERR_INVALID_ARG;
+    if (b)
+        for (uint32_t i = 0; i < a->count; i++)
+            if (std::binary_search(ids, ids + a->count, ids[i] + b)) return SML_ERR_INVALID_ARG;
     return SML_OK;
 }
 
@@ -189,6 +332,34 @@ sml_status_t sml_postprocess_burst(const sml_packet_burst* burst, void* stream) 
         case 512: k_postprocess_burst<512><<<grid, kBlockThreads, 0, s>>>(a); break;
         default: k_postprocess_burst<1024><<<grid, kBlockThreads, 0, s>>>(a); break;
     }
+    return launch_check();
+}
+
+sml_status_t sml_exchange_burst(const sml_packet_burst* burst, void* stream) {
+    sml_status_t st = check_burst(burst, true);
+    if (st != SML_OK || burst->count == 0) return st;
+    if (!burst->in || !burst->out) return SML_ERR_INVALID_ARG;
+    const sml_packet_burst& a = *burst;
+    const dim3 grid((a.count + kWavesPerBlock - 1) / kWavesPerBlock);
+    const hipStream_t s = (hipStream_t)stream;
+    const bool rne = (a.flags & SML_FLAG_ROUND_RNE) != 0;
+    const bool proc = (a.flags & SML_FLAG_PROCESS_PACKET) != 0;
+#define SML_XCH(PN)                                                                                \
+    if (proc) {                                                                                    \
+        if (rne) k_exchange_burst<PN, true, true><<<grid, kBlockThreads, 0, s>>>(a);               \
+        else k_exchange_burst<PN, false, true><<<grid, kBlockThreads, 0, s>>>(a);                  \
+    } else {                                                                                       \
+        if (rne) k_exchange_burst<PN, true, false><<<grid, kBlockThreads, 0, s>>>(a);              \
+        else k_exchange_burst<PN, false, false><<<grid, kBlockThreads, 0, s>>>(a);                 \
+    }
+    switch (a.packet_numel) {
+        case 64: SML_XCH(64) break;
+        case 128: SML_XCH(128) break;
+        case 256: SML_XCH(256) break;
+        case 512: SML_XCH(512) break;
+        default: SML_XCH(1024) break;
+    }
+#undef SML_XCH
     return launch_check();
 }
 

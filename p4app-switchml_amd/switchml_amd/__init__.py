@@ -26,6 +26,7 @@ SML_ERR_HIP = 4
 FLAG_PAYLOAD_LE = 0x1
 FLAG_ROUND_RNE = 0x2
 FLAG_PEER_PLANES = 0x4   # inputs written by other GPUs: acquire first (sml_release_to_peers on the writer)
+FLAG_PROCESS_PACKET = 0x8   # sml_exchange_burst: the dummy backend's ProcessPacket (x W) on each packet first
 
 PACKET_NUMELS = (64, 128, 256, 512, 1024)
 
@@ -148,6 +149,8 @@ def lib():
     L.sml_preprocess_burst.argtypes = [ctypes.POINTER(PacketBurst), vp]
     L.sml_postprocess_burst.restype = i32
     L.sml_postprocess_burst.argtypes = [ctypes.POINTER(PacketBurst), vp]
+    L.sml_exchange_burst.restype = i32
+    L.sml_exchange_burst.argtypes = [ctypes.POINTER(PacketBurst), vp]
     L.sml_ipc_handle_bytes.restype = u32
     L.sml_ipc_get_handle.restype = i32
     L.sml_ipc_get_handle.argtypes = [vp, vp, ctypes.POINTER(u64)]
@@ -481,6 +484,14 @@ def preprocess_burst(burst: PacketBurst, stream=None, like=None):
 def postprocess_burst(burst: PacketBurst, stream=None, like=None):
     """sml_postprocess_burst: PostprocessSingle for every packet of the burst."""
     _check("sml_postprocess_burst", lib().sml_postprocess_burst(ctypes.byref(burst), _stream(stream, like)))
+
+
+def exchange_burst(burst: PacketBurst, stream=None, like=None):
+    """sml_exchange_burst: for every received packet q, PostprocessSingle(q)
+    then PreprocessSingle(q + b) into the same buffer (the DPDK receive loop's
+    post + ReusePacket) in one launch; FLAG_PROCESS_PACKET applies the dummy
+    backend's ProcessPacket (x W) first."""
+    _check("sml_exchange_burst", lib().sml_exchange_burst(ctypes.byref(burst), _stream(stream, like)))
 
 
 def release_to_peers(stream=None, device=None):

@@ -150,3 +150,139 @@ def test_burst_int32_and_argument_checks(cuda):
     bt.count = 65
     with pytest.raises(s.SwitchMLError):
         s.postprocess_burst(bt)
+
+
+def run_exchange(x, P, W, b_max, ring_place, cuda, rng, burst_cap=64, proc_in_kernel=True):
+    """The same packet loop with one sml_exchange_burst per pass (post of p
+    and pre of p + b into the slot, in one launch — DPDK's receive loop +
+    ReusePacket); ProcessPacket x W inside it (FLAG_PROCESS_PACKET) or as a
+    separate K5 launch first."""
+    import torch
+    s = sw()
+    n = x.size
+    B = O.num_blocks(n, P)
+    b = min(B, b_max)
+    total = B + b
+    xd = torch.from_numpy(x).to(cuda)
+    out = torch.full((n,), float("nan"), device=cuda)
+    recv = torch.zeros(B, dtype=torch.int8, device=cuda)
+    SENT = 0x5A5A5A5A
+    if ring_place == "device":
+        ring = torch.full((b * P,), SENT, dtype=torch.int64, device=cuda).to(torch.int32)
+        extra = torch.zeros(b * 2, dtype=torch.uint8, device=cuda)
+    else:
+        ring = torch.full((b * P,), SENT, dtype=torch.int64).to(torch.int32).pin_memory()
+        extra = torch.zeros(b * 2, dtype=torch.uint8).pin_memory()
+    rbase, ebase = ring.data_ptr(), extra.data_ptr()
+    cap_e = np.zeros(total, dtype=np.int8)
+    cap_p = np.zeros((total, P), dtype=np.uint32)
+    stream = torch.cuda.current_stream(cuda)
+
+    def snapshot():
+        return ring.cpu().numpy().view(np.uint32).reshape(b, P).copy()
+
+    def processed(words):
+        return O.bswap32((O.bswap32(words).astype(np.uint64) * W % (1 << 32)).astype(np.uint32))
+
+    def capture(ids, before):
+        rh = snapshot()
+        eh = extra.cpu().numpy()
+        for q in ids:
+            sl = q % b
+            cap_e[q] = eh[sl * 2].astype(np.int8) if q < B else 0
+            if q >= b:
+                m = min(P, n - (q - b) * P)
+                cap_p[q, :m] = rh[sl, :m]
+                assert np.array_equal(rh[sl, m:], before[sl, m:]), "tail words not as ProcessPacket left them"
+
+    ids0 = list(range(b))
+    prev = snapshot()
+    for i0 in range(0, b, burst_cap):
+        part = ids0[i0:i0 + burst_cap]
+        s.preprocess_burst(s.packet_burst(xd, out, P, W, b, recv, part, [rbase + q * P * 4 for q in part],
+                                          [ebase + q * 2 for q in part]), stream)
+    torch.cuda.synchronize()
+    capture(ids0, prev)
+    for p0 in range(0, total, b):
+        w = min(b, total - p0)
+        if W != 1 and not proc_in_kernel:
+            s.loopback_aggregate(ring.view(torch.int32)[: w * P], W)
+        torch.cuda.synchronize()
+        before = snapshot()
+        if proc_in_kernel:
+            before = processed(before)
+        ids = list(range(p0, p0 + w))
+        rng.shuffle(ids)
+        for i0 in range(0, w, burst_cap):
+            part = ids[i0:i0 + burst_cap]
+            slots = [q % b for q in part]
+            bt = s.packet_burst(xd, out, P, W, b, recv, part, [rbase + sl * P * 4 for sl in slots],
+                                [ebase + sl * 2 for sl in slots],
+                                flags=s.FLAG_PROCESS_PACKET if proc_in_kernel else 0)
+            s.exchange_burst(bt, stream)
+        torch.cuda.synchronize()
+        capture([q + b for q in range(p0, p0 + w) if q + b < total], before)
+    return cap_e, cap_p, out.cpu().numpy(), b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,W,n,b_max,ring,cap,proc", [
+    (256, 1, 40_000, 64, "device", 64, True),
+    (256, 3, 100_003, 64, "device", 64, True),
+    (256, 3, 100_003, 64, "pinned", 64, False),
+    (64, 2, 12_345, 50, "pinned", 17, True),
+    (1024, 8, 70_001, 16, "device", 64, False),
+    (1024, 5, 70_001, 16, "pinned", 7, True),
+    (128, 1, 777, 64, "device", 5, True),          # B < b_max: b = B
+    (512, 3, 513, 64, "pinned", 64, False),
+])
+def test_exchange_loop_matches_oracle_packet_stream(cuda, P, W, n, b_max, ring, cap, proc):
+    rng = np.random.default_rng(P * 7 + W + n)
+    x = O.splitmix_normal(n % 89, n) * np.float32(2.0 ** (W - 2))
+    if n > 1000:
+        x[100:140] = 0.0
+        x[5] = np.float32(2.5)
+        x[6] = np.float32(-2.5)
+    pe, pp, ref_out, b = O.dummy_packet_stream(x, P=P, batch_max=b_max, num_workers=W)
+    ce, cp, out, b2 = run_exchange(x, P, W, b_max, ring, cuda, rng, cap, proc)
+    assert b == b2
+    assert np.array_equal(ce, pe)
+    assert np.array_equal(cp, pp.view(np.uint32))
+    assert np.array_equal(out.view(np.uint32), ref_out.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ring", ["device", "pinned"])
+def test_exchange_int32_window_and_argument_checks(cuda, ring):
+    import torch
+    s = sw()
+    P, n, b = 256, 20_000, 8
+    xi = np.random.default_rng(5).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+    xd = torch.from_numpy(xi).to(cuda)
+    outd = torch.zeros_like(xd)
+    B = O.num_blocks(n, P)
+    slots = torch.zeros(b * P, dtype=torch.int32, device=cuda if ring == "device" else "cpu")
+    if ring == "pinned":
+        slots = slots.pin_memory()
+    base = slots.data_ptr()
+    # INT32: packet q carries block q; the first b packets, then every received
+    # packet q is post'ed and its buffer refilled with block q + b
+    first = list(range(b))
+    s.preprocess_burst(s.packet_burst(xd, outd, P, 1, 0, None, first, [base + q * P * 4 for q in first], [0] * b))
+    for p0 in range(0, B, b):
+        ids = list(range(p0, min(p0 + b, B)))
+        s.exchange_burst(s.packet_burst(xd, outd, P, 1, b, None, ids, [base + (q % b) * P * 4 for q in ids],
+                                        [0] * len(ids)))
+    torch.cuda.synchronize()
+    assert np.array_equal(outd.cpu().numpy(), xi)
+    # refused: window 0, q and q + b in one burst, an id past B + b (FLOAT32)
+    x = torch.randn(10_000, device=cuda)
+    o = torch.empty_like(x)
+    Bf = O.num_blocks(10_000, P)
+    recv = torch.zeros(Bf, dtype=torch.int8, device=cuda)
+    rg = torch.zeros(64 * P, dtype=torch.int32, device=cuda)
+    ex = torch.zeros(128, dtype=torch.uint8, device=cuda)
+    for bw, bad in ((0, [1]), (8, [3, 11]), (8, [Bf + 8])):
+        bt = s.packet_burst(x, o, P, 1, bw, recv, bad, [rg.data_ptr()] * len(bad), [ex.data_ptr()] * len(bad))
+        with pytest.raises(s.SwitchMLError):
+            s.exchange_burst(bt)

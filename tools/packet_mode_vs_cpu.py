@@ -4,8 +4,9 @@ same box.
 
 GPU: bin/allreduce_benchmark in packet mode — the loopback backend driving
 the HIP PPP through its per-LTU interface (PreprocessSingle/PostprocessSingle
-semantics, in bursts of one ring pass: csrc/client/loopback_backend.cc
-run_packet_loop) — 64 MiB fp32, T = 4 worker threads, W = 2, device ring.
+semantics, one exchange burst per ring pass: csrc/client/loopback_backend.cc
+run_packet_loop) — 64 MiB fp32, T = 4 worker threads, W = 2, device ring and
+pinned host ring.
 CPU: the oracle's restatement of the reference's DummyWorkerThread loop with
 the reference's default build (VCL=1), T = 4 threads, the same job (pre +
 ProcessPacket + post for every packet: the whole round trip), and the
@@ -30,16 +31,26 @@ def median(v):
 
 
 def gpu_packet_mode(numel, T, W, jobs=7):
+    """packet: HBM ring, one exchange launch per ring pass (ProcessPacket +
+    post + pre); packet_pinned_ring: the ring in pinned host memory (a NIC's
+    mbuf pool: ProcessPacket on the CPU, one exchange launch per pass, read
+    and written over PCIe, host sync per burst)."""
+    import tempfile
     exe = os.path.join(ROOT, "p4app-switchml_amd", "bin", "allreduce_benchmark")
     res = {}
-    for mode in ("packet", "bulk", "fused"):
+    with tempfile.NamedTemporaryFile("w", suffix=".cfg", delete=False) as f:
+        f.write("[backend.hip]\npacket_ring = pinned\n")
+        pinned_cfg = f.name
+    for name, mode, extra in (("packet", "packet", []), ("packet_pinned_ring", "packet", ["--config", pinned_cfg]),
+                              ("bulk", "bulk", []), ("fused", "fused", [])):
         r = subprocess.run([exe, "--tensor-numel", str(numel), "--tensor-type", "float", "--num-workers", str(W),
                             "--num-worker-threads", str(T), "--bandwidth", "0", "--device", "gpu", "--mode", mode,
-                            "--num-jobs", str(jobs), "--num-warmup-jobs", "2", "--verify", "true"],
+                            "--num-jobs", str(jobs), "--num-warmup-jobs", "2", "--verify", "true"] + extra,
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0 and "Data verified successfully" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
         ns = [int(m) for m in re.findall(r"Duration: #(\d+)# ns", r.stdout)]
-        res[mode] = {"median_ms": median(ns) / 1e6, "jobs": len(ns)}
+        res[name] = {"median_ms": median(ns) / 1e6, "jobs": len(ns)}
+    os.unlink(pinned_cfg)
     return res
 
 
@@ -72,9 +83,12 @@ def main():
            "gpu_allreduce_benchmark": g, "cpu_reference_vcl1_T4": c,
            "packet_mode_vs_cpu_roundtrip": round(c["roundtrip"]["median_ms"] / g["packet"]["median_ms"], 3),
            "packet_mode_vs_cpu_preprocess_only": round(c["preprocess_only"]["median_ms"] / g["packet"]["median_ms"], 3),
-           "note": ("GPU packet mode = the whole all-reduce (per-packet pre + ProcessPacket + post through the "
-                    "HIP PPP's burst calls, device ring); CPU = the oracle's restatement of the reference's "
-                    "VCL=1 per-packet loop on this host, same job")}
+           "pinned_ring_vs_cpu_roundtrip": round(c["roundtrip"]["median_ms"] /
+                                                 g["packet_pinned_ring"]["median_ms"], 3),
+           "note": ("GPU packet mode = the whole all-reduce (per-packet ProcessPacket + post + pre through the "
+                    "HIP PPP's exchange bursts: PostprocessReuseBurst, one launch per pass over the b-slot ring; "
+                    "device ring, and a pinned host ring like a NIC's mbuf pool); CPU = the oracle's restatement "
+                    "of the reference's VCL=1 per-packet loop on this host, same job")}
     s = json.dumps(out, indent=1)
     print(s)
     if len(sys.argv) > 1:
