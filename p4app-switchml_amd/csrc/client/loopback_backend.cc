@@ -112,8 +112,9 @@ void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerStat
         extra = static_cast<uint8_t*>(ws.hring_extra.get(b * 2, pin));
         std::memset(ring, 0, b * P * 4);
     }
-    // ProcessPacket (every entry of the packet x W) on the CPU for a host ring,
-    // as dummy_backend.cc:72-84 does, on the device for an HBM ring.
+    // ProcessPacket (every entry of the packet x W, dummy_backend.cc:72-84) on
+    // the device for a device-addressable ring (HBM or pinned host memory, in
+    // the same launch as the PPP's calls), on the CPU for a pageable one.
     //
     // The reference handles one packet per loop trip: packet p comes back,
     // ProcessPacket, PostprocessSingle(p), PreprocessSingle(p + b) into the
@@ -121,9 +122,10 @@ void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerStat
     // the ring (slots s0 .. s0 + w - 1, w <= b) go as one burst — the way a
     // DPDK worker handles an rx burst and refills its mbufs — with the same
     // calls per slot in the same order: PostprocessReuseBurst (post of p, pre
-    // of p + b into the slot).  An HBM ring runs the whole trip, ProcessPacket
-    // included, as ONE launch per pass and stays stream-ordered (no host sync);
-    // a host ring completes each burst before the CPU touches it.
+    // of p + b into the slot).  A device-addressable ring runs the whole trip,
+    // ProcessPacket included, as ONE launch per pass; the HBM ring stays
+    // stream-ordered (no host sync), a host ring completes each burst before
+    // the call returns (the packets would go to the NIC next).
     const uint16_t W = cfg.general_.num_workers;
     const bool dev_ring = where == "device";
     const bool proc = cfg.backend_.dummy.process_packets;
@@ -139,7 +141,7 @@ void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerStat
     for (uint64_t p0 = 0; p0 < total; p0 += b) {
         const uint64_t w = std::min<uint64_t>(b, total - p0);   // p0 % b == 0: slots 0 .. w - 1
         for (uint64_t s = 0; s < w; s++) ids[s] = p0 + s;
-        if (proc && dev_ring) {
+        if (proc && where != "pageable") {
             ppp.ProcessPostprocessReuseBurst((uint32_t)w, ids.data(), ents.data(), exs.data());
             continue;
         }
