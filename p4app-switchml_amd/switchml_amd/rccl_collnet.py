@@ -302,7 +302,7 @@ def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, cha
                 with open(f.name, errors="replace") as g:
                     ls = [l for l in g.read().splitlines() if l.startswith("[rank")]
                 tail.append(ls[-1] if ls else "-")
-            print(f"[rccl_collnet] {time.time() - t0:.0f} s: " + " | ".join(tail), flush=True)
+            print(f"[rccl_collnet] {time.time() - t0:.0f} s: " + " | ".join(tail), file=sys.stderr, flush=True)
         time.sleep(0.2)
     for p in procs:
         p.wait()
