@@ -286,3 +286,74 @@ def test_exchange_int32_window_and_argument_checks(cuda, ring):
         bt = s.packet_burst(x, o, P, 1, bw, recv, bad, [rg.data_ptr()] * len(bad), [ex.data_ptr()] * len(bad))
         with pytest.raises(s.SwitchMLError):
             s.exchange_burst(bt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,W,n,b_max,ring,seed", [
+    (256, 2, 60_001, 64, "device", 1),
+    (256, 3, 33_333, 32, "pinned", 2),
+    (1024, 8, 50_000, 16, "device", 3),
+    (64, 1, 9_999, 48, "pinned", 4),
+])
+def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring, seed):
+    """DummyBackend::ReceiveBurst delivers a RANDOM subset of the pending
+    packets in random order (dummy_backend.cc:99-118: k = rand() % (pending +
+    1), each a random pending index), ProcessPacket (x W) on receipt; the
+    worker then post-processes each received packet and refills its slot with
+    packet p + b (dummy_worker_thread.cc:125-170).  The same loop here, every
+    receive burst one sml_exchange_burst with FLAG_PROCESS_PACKET: each packet
+    as sent and the output equal the oracle's in-order packet stream bit for
+    bit (slots are independent, so the delivery order cannot change a byte)."""
+    import torch
+    s = sw()
+    rng = np.random.default_rng(seed)
+    x = O.splitmix_normal(seed + 11, n) * np.float32(2.0 ** (seed - 2))
+    pe, pp, ref_out, b = O.dummy_packet_stream(x, P=P, batch_max=b_max, num_workers=W)
+    B = O.num_blocks(n, P)
+    total = B + b
+    xd = torch.from_numpy(x).to(cuda)
+    out = torch.full((n,), float("nan"), device=cuda)
+    recv = torch.zeros(B, dtype=torch.int8, device=cuda)
+    if ring == "device":
+        rg = torch.zeros(b * P, dtype=torch.int32, device=cuda)
+        ex = torch.zeros(b * 2, dtype=torch.uint8, device=cuda)
+    else:
+        rg = torch.zeros(b * P, dtype=torch.int32).pin_memory()
+        ex = torch.zeros(b * 2, dtype=torch.uint8).pin_memory()
+    rbase, ebase = rg.data_ptr(), ex.data_ptr()
+    stream = torch.cuda.current_stream(cuda)
+
+    def capture(ids):
+        rh = rg.cpu().numpy().view(np.uint32).reshape(b, P)
+        eh = ex.cpu().numpy()
+        for q in ids:
+            sl = q % b
+            if q < B:
+                assert eh[sl * 2].astype(np.int8) == pe[q], f"exponent of packet {q}"
+            if q >= b:
+                m = min(P, n - (q - b) * P)
+                assert np.array_equal(rh[sl, :m], pp[q, :m].view(np.uint32)), f"payload of packet {q}"
+
+    first = list(range(b))
+    s.preprocess_burst(s.packet_burst(xd, out, P, W, b, recv, first, [rbase + q * P * 4 for q in first],
+                                      [ebase + q * 2 for q in first]), stream)
+    torch.cuda.synchronize()
+    capture(first)
+    pending, received = list(first), 0
+    while received < total:
+        k = int(rng.integers(0, len(pending) + 1))
+        got = []
+        for _ in range(k):
+            got.append(pending.pop(int(rng.integers(0, len(pending)))))
+        if not got:
+            continue
+        received += len(got)
+        bt = s.packet_burst(xd, out, P, W, b, recv, got, [rbase + (q % b) * P * 4 for q in got],
+                            [ebase + (q % b) * 2 for q in got], flags=s.FLAG_PROCESS_PACKET)
+        s.exchange_burst(bt, stream)
+        torch.cuda.synchronize()
+        nxt = [q + b for q in got if q + b < total]
+        capture(nxt)
+        pending.extend(nxt)
+    assert not pending
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref_out.view(np.uint32))
