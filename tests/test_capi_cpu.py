@@ -73,6 +73,47 @@ def test_argument_validation_without_gpu(sw):
     assert L.sml_loopback_aggregate(pay, 6, 2, 0, None) == sw.SML_ERR_ALIGNMENT
 
 
+def test_burst_validation_without_gpu(sw):
+    """sml_{pre,post}process_burst / sml_exchange_burst refuse a malformed
+    burst before any HIP call: too many packets, an id past B (+ b), a
+    duplicate id, q and q + b together, a zero window for the exchange, a
+    missing extra slot for a FLOAT32 packet that carries an exponent."""
+    L = sw.lib()
+    x = (ctypes.c_float * 4096)()
+    o = (ctypes.c_float * 4096)()
+    recv = (ctypes.c_int8 * 16)()
+    ring = (ctypes.c_int32 * 256)()
+    extra = (ctypes.c_uint8 * 2)()
+
+    def burst(ids, b=4, with_extra=True, count=None):
+        bt = sw.PacketBurst()
+        bt.in_ = ctypes.addressof(x)
+        bt.out = ctypes.addressof(o)
+        bt.numel = 4096
+        bt.packet_numel = 256                  # B = 16
+        bt.num_workers = 1
+        bt.data_type = 0
+        bt.batch_num_ltus = b
+        bt.recv_exps = ctypes.addressof(recv)
+        bt.count = len(ids) if count is None else count
+        for i, q in enumerate(ids):
+            bt.pkt_ids[i] = q
+            bt.entries[i] = ctypes.addressof(ring)
+            bt.extras[i] = ctypes.addressof(extra) if with_extra else None
+        return ctypes.byref(bt)
+
+    bad = sw.SML_ERR_INVALID_ARG
+    for fn in (L.sml_preprocess_burst, L.sml_postprocess_burst, L.sml_exchange_burst):
+        assert fn(burst([0], count=65), None) == bad           # > SML_MAX_BURST
+        assert fn(burst([20]), None) == bad                    # q >= B + b
+        assert fn(burst([3, 3]), None) == bad                  # duplicate
+        assert fn(burst([5, 1]), None) == bad                  # q and q + b (any order)
+        assert fn(burst([2], with_extra=False), None) == bad   # q < B needs its extra slot
+        assert fn(burst([]), None) == sw.SML_OK                # nothing to do
+    assert L.sml_exchange_burst(burst([1], b=0), None) == bad  # the exchange needs its window
+    assert L.sml_exchange_burst(burst([1], b=17), None) == bad  # b > B
+
+
 def test_grid_limit_knob(sw):
     prev = sw.set_grid_limit(1024)
     assert sw.set_grid_limit(prev) == 1024
