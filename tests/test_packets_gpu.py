@@ -303,7 +303,10 @@ def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring,
     packet p + b (dummy_worker_thread.cc:125-170).  The same loop here, every
     receive burst one sml_exchange_burst with FLAG_PROCESS_PACKET: each packet
     as sent and the output equal the oracle's in-order packet stream bit for
-    bit (slots are independent, so the delivery order cannot change a byte)."""
+    bit (slots are independent, so the delivery order cannot change a byte).
+    Before every receive, up to three outstanding packets are re-built into
+    spare buffers, as the DPDK timeout path re-sends them, and must equal the
+    packets in flight byte for byte."""
     import torch
     s = sw()
     rng = np.random.default_rng(seed)
@@ -339,8 +342,36 @@ def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring,
                                       [ebase + q * 2 for q in first]), stream)
     torch.cuda.synchronize()
     capture(first)
+    # the DPDK timer path re-builds a packet that timed out (ResendPacketCallback
+    # -> BuildPacket -> PreprocessSingle(pkt_id), dpdk_worker_thread_utils.inc:
+    # 225-265) into a fresh mbuf: the PPP is a pure function of (block, scale),
+    # so the resent bytes must equal the outstanding packet's
+    if ring == "device":
+        spare = torch.zeros(3 * P, dtype=torch.int32, device=cuda)
+        spare_x = torch.zeros(6, dtype=torch.uint8, device=cuda)
+    else:
+        spare = torch.zeros(3 * P, dtype=torch.int32).pin_memory()
+        spare_x = torch.zeros(6, dtype=torch.uint8).pin_memory()
+
+    def resend_matches(ids):
+        s.preprocess_burst(s.packet_burst(xd, out, P, W, b, recv, ids,
+                                          [spare.data_ptr() + i * P * 4 for i in range(len(ids))],
+                                          [spare_x.data_ptr() + i * 2 for i in range(len(ids))]), stream)
+        torch.cuda.synchronize()
+        rh = rg.cpu().numpy().view(np.uint32).reshape(b, P)
+        sh = spare.cpu().numpy().view(np.uint32).reshape(3, P)
+        eh, sx = ex.cpu().numpy(), spare_x.cpu().numpy()
+        for i, q in enumerate(ids):
+            if q < B:
+                assert sx[i * 2] == eh[(q % b) * 2], f"resent exponent of packet {q}"
+            if q >= b:
+                m = min(P, n - (q - b) * P)
+                assert np.array_equal(sh[i, :m], rh[q % b, :m]), f"resent payload of packet {q}"
+
     pending, received = list(first), 0
     while received < total:
+        if pending:
+            resend_matches([int(q) for q in rng.choice(pending, size=min(3, len(pending)), replace=False)])
         k = int(rng.integers(0, len(pending) + 1))
         got = []
         for _ in range(k):
