@@ -259,6 +259,36 @@ sml_status_t sml_postprocess_burst(const sml_packet_burst* burst, void* stream);
 #define SML_FLAG_PROCESS_PACKET 0x8u
 sml_status_t sml_exchange_burst(const sml_packet_burst* burst, void* stream);
 
+/* A persistent burst server, for packet buffers in HOST memory (a NIC's
+ * mbuf pool in pinned memory): there a burst launch costs a launch, PCIe
+ * round trips and a host synchronisation, ≈ 20 µs per burst (DESIGN.md §9
+ * F1).  The server is one resident workgroup that polls a doorbell in
+ * coherent, device-mapped host memory.  sml_burst_server_submit() writes the
+ * burst, rings the doorbell and returns once the burst is complete (it spins
+ * on the completion word the server publishes with a system-scope release):
+ * the same bytes as sml_preprocess_burst (op SML_BURST_PRE),
+ * sml_postprocess_burst (SML_BURST_POST) or sml_exchange_burst
+ * (SML_BURST_EXCHANGE, SML_FLAG_PROCESS_PACKET honoured), a wave per packet.
+ * The server starts with the first submit, leaves its loop after `idle_ms`
+ * (0 = 100) without a burst, or on sml_burst_server_stop(), and is restarted
+ * by the next submit; destroy stops it and frees it.  While it runs it
+ * occupies one CU and a device-wide synchronisation waits for it, so a
+ * caller stops it between job slices.
+ * packet_numel and SML_FLAG_ROUND_RNE are fixed per server (a burst with
+ * other values is refused); one server per calling thread; the current
+ * device is the server's. */
+typedef struct sml_burst_server sml_burst_server;
+#define SML_BURST_PRE 0u
+#define SML_BURST_POST 1u
+#define SML_BURST_EXCHANGE 2u
+sml_status_t sml_burst_server_create(uint32_t packet_numel, uint32_t flags, uint32_t idle_ms,
+                                     sml_burst_server** server_out);
+sml_status_t sml_burst_server_submit(sml_burst_server* server, uint32_t op, const sml_packet_burst* burst);
+/* Leave the loop now and wait for it (the next submit restarts the server);
+ * the server's memory and stream are kept for that. */
+sml_status_t sml_burst_server_stop(sml_burst_server* server);
+sml_status_t sml_burst_server_destroy(sml_burst_server* server);
+
 /* Plane sharing for the peer-to-peer switch: export the allocation holding
  * d_ptr as an IPC handle of sml_ipc_handle_bytes() bytes plus d_ptr's byte
  * offset inside it; open a peer's handle in this process (returns the

@@ -78,6 +78,7 @@ bool Config::LoadFromString(const std::string& ini) {
         else if (full == "backend.xgmi.timeout_ms") backend_.xgmi.timeout_ms = parse_uint<uint64_t>(full, val, ~0ull);
         else if (full == "backend.hip.mode") backend_.hip.mode = val;
         else if (full == "backend.hip.packet_ring") backend_.hip.packet_ring = val;
+        else if (full == "backend.hip.burst_server") backend_.hip.burst_server = parse_bool(val);
         else if (full == "backend.hip.batch_jobs") backend_.hip.batch_jobs = parse_uint<uint32_t>(full, val, 0xffffffffull);
         else if (full == "backend.hip.coalesce_us") backend_.hip.coalesce_us = parse_uint<uint32_t>(full, val, 1000000ull);
         else fprintf(stderr, "[switchml] ignoring config key '%s' (not used by this build)\n", full.c_str());
@@ -155,7 +156,9 @@ std::string Config::ToString() const {
       << "\nprocess_packets = " << (backend_.dummy.process_packets ? "true" : "false")
       << "\nfail_worker_thread = " << backend_.dummy.fail_worker_thread
       << "\n\n[backend.hip]\ndevice = " << backend_.hip.device << "\nmode = " << backend_.hip.mode
-      << "\npacket_ring = " << backend_.hip.packet_ring << "\nbatch_jobs = " << backend_.hip.batch_jobs
+      << "\npacket_ring = " << backend_.hip.packet_ring
+      << "\nburst_server = " << (backend_.hip.burst_server ? "true" : "false")
+      << "\nbatch_jobs = " << backend_.hip.batch_jobs
       << "\ncoalesce_us = " << backend_.hip.coalesce_us
       << "\n\n[backend.xgmi]\nsession = " << backend_.xgmi.session
       << "\nmax_slice_numel = " << backend_.xgmi.max_slice_numel << "\ntimeout_ms = " << backend_.xgmi.timeout_ms

@@ -48,6 +48,11 @@ struct HipBackendConfig {
     // "pinned" (page-locked host memory, a NIC's DMA buffers) or "pageable"
     // (plain malloc) — the per-LTU calls handle all three (staged or direct).
     std::string packet_ring = "device";
+    // Burst calls whose packet buffers are in host memory (pinned ring, a
+    // NIC's mbuf pool) go to a persistent burst server (sml_burst_server_*:
+    // one resident workgroup polling a doorbell) instead of one launch and a
+    // host synchronisation per burst; the server runs for the job slice.
+    bool burst_server = false;
     // mode = fused, loopback switch, no simulated wire: ONE worker thread
     // takes every slice of up to batch_jobs queued jobs (at most
     // SML_MAX_BATCH_SLICES slices) and runs them in one kernel launch

@@ -26,7 +26,8 @@ HipExponentQuantizerPPP::HipExponentQuantizerPPP(Config& config, WorkerTid worke
 }
 
 HipExponentQuantizerPPP::~HipExponentQuantizerPPP() {
-    CleanupJobSlice();
+    job_slice_ = nullptr;
+    if (server_) (void)sml_burst_server_destroy(server_);   // no throwing from a destructor
     if (d_recv_exps_) (void)hipFree(d_recv_exps_);
     if (d_stage_) (void)hipFree(d_stage_);
     if (d_stage_exp_) (void)hipFree(d_stage_exp_);
@@ -51,7 +52,14 @@ uint64_t HipExponentQuantizerPPP::SetupJobSlice(JobSlice* job_slice) {
 
 bool HipExponentQuantizerPPP::NeedsExtraBatch() { return job_slice_->slice.data_type == FLOAT32; }
 
-void HipExponentQuantizerPPP::CleanupJobSlice() { job_slice_ = nullptr; }
+void HipExponentQuantizerPPP::CleanupJobSlice() {
+    job_slice_ = nullptr;
+    server_synced_ = false;
+    // a resident server would hold up every device-wide synchronisation:
+    // it runs for one slice's packet loop only (its memory and stream stay)
+    if (server_ && sml_burst_server_stop(server_) != SML_OK)
+        throw SwitchMLFatal(std::string("sml_burst_server_stop: ") + sml_last_error());
+}
 
 void HipExponentQuantizerPPP::ensure_single_buffers() {
     if (!d_stage_) {
@@ -235,6 +243,16 @@ void HipExponentQuantizerPPP::burst(BurstKind kind, uint32_t n, const uint64_t* 
     b.flags = kind == BurstKind::kProcessExchange ? SML_FLAG_PROCESS_PACKET : 0u;
     const char* what = kind == BurstKind::kPre ? "sml_preprocess_burst"
                        : kind == BurstKind::kPost ? "sml_postprocess_burst" : "sml_exchange_burst";
+    const bool serve = m.host && config_.backend_.hip.burst_server;
+    if (serve && !server_) {
+        check(sml_burst_server_create((uint32_t)ltu_numel_, 0, 100, &server_), "sml_burst_server_create");
+    }
+    if (serve && !server_synced_) {   // the server has its own stream: the slice's staged input must be there
+        hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+        server_synced_ = true;
+    }
+    const uint32_t op = kind == BurstKind::kPre ? SML_BURST_PRE
+                        : kind == BurstKind::kPost ? SML_BURST_POST : SML_BURST_EXCHANGE;
     for (uint32_t i0 = 0; i0 < n; i0 += SML_MAX_BURST) {
         b.count = std::min<uint32_t>(SML_MAX_BURST, n - i0);
         for (uint32_t i = 0; i < b.count; i++) {
@@ -242,10 +260,15 @@ void HipExponentQuantizerPPP::burst(BurstKind kind, uint32_t n, const uint64_t* 
             b.entries[i] = static_cast<char*>(entries[i0 + i]) + delta;
             b.extras[i] = extras && extras[i0 + i] ? static_cast<char*>(extras[i0 + i]) + delta : nullptr;
         }
+        if (serve) {   // returns with the burst complete
+            check(sml_burst_server_submit(server_, op, &b), "sml_burst_server_submit");
+            continue;
+        }
         check(kind == BurstKind::kPre ? sml_preprocess_burst(&b, stream_)
               : kind == BurstKind::kPost ? sml_postprocess_burst(&b, stream_) : sml_exchange_burst(&b, stream_),
               what);
     }
+    if (serve) return;
     if (m.host || !stream_ordered_) hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
 }
 

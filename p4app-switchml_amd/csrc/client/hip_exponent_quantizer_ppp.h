@@ -18,6 +18,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "prepostprocessor.h"
+#include "switchml_hip.h"
 
 namespace switchml {
 
@@ -85,6 +86,9 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     void* pool_probe_ = nullptr;
     void* pool_dev_ = nullptr;
     bool pool_host_ = true;
+    // persistent burst server for host-memory packets (backend.hip.burst_server)
+    sml_burst_server* server_ = nullptr;
+    bool server_synced_ = false;   // stream_ drained before the slice's first server burst
 };
 
 }  // namespace switchml

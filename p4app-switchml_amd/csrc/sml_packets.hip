@@ -29,17 +29,16 @@
 // burst's, which does both for a received packet in one wave (post of q,
 // then pre of q + b into the same buffer: one launch per rx burst).
 #include <algorithm>
+#include <chrono>
 
 #include "sml_host.h"
 
 namespace sml {
 
 template <int P, bool RNE>
-__global__ __launch_bounds__(kBlockThreads) void k_preprocess_burst(sml_packet_burst a) {
+__device__ __forceinline__ void preprocess_one(const sml_packet_burst& a, uint32_t i) {
     constexpr int U = P > 256 ? P / 256 : 1;         // 256-element slices per packet
     constexpr int kLanes = P >= 256 ? kWave : P / 4; // lanes holding a slice
-    const uint32_t i = blockIdx.x * kWavesPerBlock + wave_index();
-    if (i >= a.count) return;
     const int lane = threadIdx.x & (kWave - 1);
     const bool act = lane < kLanes;
     const uint64_t q = a.pkt_ids[i];
@@ -90,11 +89,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_preprocess_burst(sml_packet_b
 }
 
 template <int P>
-__global__ __launch_bounds__(kBlockThreads) void k_postprocess_burst(sml_packet_burst a) {
+__device__ __forceinline__ void postprocess_one(const sml_packet_burst& a, uint32_t i) {
     constexpr int U = P > 256 ? P / 256 : 1;
     constexpr int kLanes = P >= 256 ? kWave : P / 4;
-    const uint32_t i = blockIdx.x * kWavesPerBlock + wave_index();
-    if (i >= a.count) return;
     const int lane = threadIdx.x & (kWave - 1);
     const bool act = lane < kLanes;
     const uint64_t q = a.pkt_ids[i];
@@ -145,11 +142,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_postprocess_burst(sml_packet_
 // reads and the writes of one buffer may cross PCIe (pinned mbufs), where a
 // posted write may overtake an outstanding read.
 template <int P, bool RNE, bool PROC>
-__global__ __launch_bounds__(kBlockThreads) void k_exchange_burst(sml_packet_burst a) {
+__device__ __forceinline__ void exchange_one(const sml_packet_burst& a, uint32_t i) {
     constexpr int U = P > 256 ? P / 256 : 1;
     constexpr int kLanes = P >= 256 ? kWave : P / 4;
-    const uint32_t i = blockIdx.x * kWavesPerBlock + wave_index();
-    if (i >= a.count) return;
     const int lane = threadIdx.x & (kWave - 1);
     const bool act = lane < kLanes;
     const uint64_t q = a.pkt_ids[i];
@@ -251,6 +246,126 @@ __global__ __launch_bounds__(kBlockThreads) void k_exchange_burst(sml_packet_bur
         m = group_max<256>(m);                              // idle lanes hold 0
         if (lane == 0) *static_cast<int8_t*>(a.extras[i]) = (int8_t)exponent_of(m);
     }
+}
+
+// One launch per burst: a wave per packet.
+template <int P, bool RNE>
+__global__ __launch_bounds__(kBlockThreads) void k_preprocess_burst(sml_packet_burst a) {
+    const uint32_t i = blockIdx.x * kWavesPerBlock + wave_index();
+    if (i < a.count) preprocess_one<P, RNE>(a, i);
+}
+
+template <int P>
+__global__ __launch_bounds__(kBlockThreads) void k_postprocess_burst(sml_packet_burst a) {
+    const uint32_t i = blockIdx.x * kWavesPerBlock + wave_index();
+    if (i < a.count) postprocess_one<P>(a, i);
+}
+
+template <int P, bool RNE, bool PROC>
+__global__ __launch_bounds__(kBlockThreads) void k_exchange_burst(sml_packet_burst a) {
+    const uint32_t i = blockIdx.x * kWavesPerBlock + wave_index();
+    if (i < a.count) exchange_one<P, RNE, PROC>(a, i);
+}
+
+// ---- the persistent burst server (include/switchml_hip.h) ----------------
+// kServerGroups resident workgroups of 16 waves — one wave per packet of a
+// full burst — poll a doorbell in coherent, device-mapped host memory.  Per
+// burst, in every workgroup: thread 0 polls the doorbell with relaxed
+// system-scope loads and, once it moves, acquires at system scope (no stale
+// copy of the host-written descriptor or packets); a barrier orders the other
+// threads after it; the descriptor is copied into LDS with system-scope
+// loads; the waves run their packets (the same per-packet bodies as the
+// one-launch-per-burst kernels); a barrier orders every wave's stores before
+// thread 0, which releases them at system scope and arrives on a counter in
+// device memory.  The last workgroup to arrive resets the counter and
+// publishes the burst's sequence number with a system-scope release store;
+// the host submits the next burst only after that, so no workgroup can run
+// ahead into the next burst.  The loop ends on `stop` or after idle_ticks of
+// wall clock without a doorbell, so every wave reaches the exit on its own;
+// the host restarts a server that has been idle for half that long before
+// ringing it again, so a doorbell never races an idle exit.
+constexpr int kServerThreads = 1024;
+constexpr int kServerGroups = SML_MAX_BURST / (kServerThreads / kWave);   // 4
+
+struct alignas(64) ServerCtl {
+    uint64_t doorbell;         // host: sequence number of the last submitted burst
+    uint32_t op;               // host: SML_BURST_* of that burst
+    uint32_t stop;             // host: 1 = leave the loop
+    uint64_t pad0[6];
+    uint64_t done;             // device: sequence number of the last completed burst
+    uint32_t exited[kServerGroups];   // device: workgroup g has left its loop
+    uint64_t pad2[5];
+    sml_packet_burst burst;    // host: the submitted burst
+};
+
+// A system-scope load without acquire semantics: polling must not invalidate
+// the caches on every probe (an acquire load does); the one acquire fence
+// follows the probe that sees the doorbell.
+template <class T>
+__device__ __forceinline__ T sys_poll(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int P, bool RNE>
+__global__ __launch_bounds__(kServerThreads) void k_burst_server(ServerCtl* ctl, uint32_t* arrive,
+                                                                 uint64_t idle_ticks) {
+    __shared__ sml_packet_burst sa;
+    __shared__ uint64_t s_seq;
+    __shared__ int s_cmd;
+    constexpr uint32_t kWaves = kServerThreads / kWave;
+    constexpr uint32_t kAllWaves = kWaves * kServerGroups;
+    const uint32_t tid = threadIdx.x;
+    uint64_t seen = tid == 0 ? sys_poll(&ctl->done) : 0;
+    for (;;) {
+        if (tid == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            int cmd = -1;
+            uint64_t db = seen;
+            for (;;) {
+                if (sys_poll(&ctl->stop)) break;
+                db = sys_poll(&ctl->doorbell);
+                if (db != seen) {
+                    // acquire once, by the thread that saw the doorbell; the
+                    // barrier below orders every other thread after it
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                    cmd = (int)sys_poll(&ctl->op);
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_cmd = cmd;
+            s_seq = db;
+        }
+        __syncthreads();
+        const int cmd = s_cmd;
+        if (cmd < 0) break;
+        constexpr uint32_t kWords = sizeof(sml_packet_burst) / 4;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&ctl->burst);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(&sa);
+        for (uint32_t k = tid; k < kWords; k += kServerThreads)
+            dst[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();
+        const uint32_t n = sa.count;
+        const bool proc = (sa.flags & SML_FLAG_PROCESS_PACKET) != 0;
+        for (uint32_t i = blockIdx.x * kWaves + wave_index(); i < n; i += kAllWaves) {
+            if (cmd == SML_BURST_PRE) preprocess_one<P, RNE>(sa, i);
+            else if (cmd == SML_BURST_POST) postprocess_one<P>(sa, i);
+            else if (proc) exchange_one<P, RNE, true>(sa, i);
+            else exchange_one<P, RNE, false>(sa, i);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            seen = s_seq;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this workgroup's stores, system-wide
+            const uint32_t before = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (before == kServerGroups - 1) {              // the last one: every group's stores are released
+                __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctl->done, seen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+    if (tid == 0) __hip_atomic_store(&ctl->exited[blockIdx.x], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Host checks shared by the entry points.  `window`: the exchange burst's
@@ -361,6 +476,157 @@ sml_status_t sml_exchange_burst(const sml_packet_burst* burst, void* stream) {
     }
 #undef SML_XCH
     return launch_check();
+}
+
+}  // extern "C"
+
+struct sml_burst_server {
+    sml::ServerCtl* ctl = nullptr;    // host address (coherent, device-mapped)
+    sml::ServerCtl* dctl = nullptr;   // the same memory at its device address
+    uint32_t* arrive = nullptr;       // device memory: workgroups done with the current burst
+    hipStream_t stream = nullptr;
+    uint32_t packet_numel = 0;
+    bool rne = false;
+    uint64_t idle_ticks = 0;
+    std::chrono::milliseconds restart_after{50};   // half the server's idle time
+    uint64_t seq = 0;
+    bool launched = false;            // a kernel was launched and not yet joined
+    std::chrono::steady_clock::time_point last_activity;
+};
+
+namespace {
+
+uint64_t host_load(const volatile uint64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+
+bool any_exited(const sml_burst_server* s) {
+    for (int g = 0; g < sml::kServerGroups; g++)
+        if (__atomic_load_n(&s->ctl->exited[g], __ATOMIC_ACQUIRE)) return true;
+    return false;
+}
+
+// Stop a launched server (if any) and wait for every workgroup to leave.
+sml_status_t server_join(sml_burst_server* s) {
+    if (!s->launched) return SML_OK;
+    __atomic_store_n(&s->ctl->stop, 1u, __ATOMIC_RELEASE);
+    s->launched = false;
+    return sml::hip_check(hipStreamSynchronize(s->stream));
+}
+
+sml_status_t server_launch(sml_burst_server* s) {
+    sml_status_t st = server_join(s);
+    if (st != SML_OK) return st;
+    for (int g = 0; g < sml::kServerGroups; g++) __atomic_store_n(&s->ctl->exited[g], 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&s->ctl->stop, 0u, __ATOMIC_RELEASE);
+    st = sml::hip_check(hipMemsetAsync(s->arrive, 0, sizeof(uint32_t), s->stream));
+    if (st != SML_OK) return st;
+    const dim3 grid(sml::kServerGroups), block(sml::kServerThreads);
+#define SML_SRV(PN)                                                                                        \
+    if (s->rne) sml::k_burst_server<PN, true><<<grid, block, 0, s->stream>>>(s->dctl, s->arrive, s->idle_ticks); \
+    else sml::k_burst_server<PN, false><<<grid, block, 0, s->stream>>>(s->dctl, s->arrive, s->idle_ticks);
+    switch (s->packet_numel) {
+        case 64: SML_SRV(64) break;
+        case 128: SML_SRV(128) break;
+        case 256: SML_SRV(256) break;
+        case 512: SML_SRV(512) break;
+        default: SML_SRV(1024) break;
+    }
+#undef SML_SRV
+    st = sml::launch_check();
+    s->launched = st == SML_OK;
+    s->last_activity = std::chrono::steady_clock::now();
+    return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+sml_status_t sml_burst_server_create(uint32_t packet_numel, uint32_t flags, uint32_t idle_ms,
+                                     sml_burst_server** out) {
+    if (!out) return SML_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!sml::valid_packet(packet_numel)) return SML_ERR_UNSUPPORTED;
+    if (flags & ~SML_FLAG_ROUND_RNE) return SML_ERR_INVALID_ARG;
+    int dev = 0, rate_khz = 0;
+    sml_status_t st = sml::hip_check(hipGetDevice(&dev));
+    if (st == SML_OK) st = sml::hip_check(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev));
+    if (st != SML_OK) return st;
+    auto* s = new sml_burst_server;
+    const uint32_t ms = idle_ms ? idle_ms : 100;
+    s->packet_numel = packet_numel;
+    s->rne = (flags & SML_FLAG_ROUND_RNE) != 0;
+    s->idle_ticks = (uint64_t)(rate_khz > 0 ? rate_khz : 100000) * ms;
+    s->restart_after = std::chrono::milliseconds(ms / 2);
+    void* h = nullptr;
+    void* d = nullptr;
+    st = sml::hip_check(hipHostMalloc(&h, sizeof(sml::ServerCtl), hipHostMallocMapped | hipHostMallocCoherent));
+    if (st == SML_OK) {
+        memset(h, 0, sizeof(sml::ServerCtl));
+        st = sml::hip_check(hipHostGetDevicePointer(&d, h, 0));
+    }
+    if (st == SML_OK) st = sml::hip_check(hipMalloc(reinterpret_cast<void**>(&s->arrive), 64));
+    if (st == SML_OK) st = sml::hip_check(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    if (st != SML_OK) {
+        if (h) (void)hipHostFree(h);
+        if (s->arrive) (void)hipFree(s->arrive);
+        delete s;
+        return st;
+    }
+    s->ctl = static_cast<sml::ServerCtl*>(h);
+    s->dctl = static_cast<sml::ServerCtl*>(d);
+    *out = s;
+    return SML_OK;
+}
+
+sml_status_t sml_burst_server_submit(sml_burst_server* s, uint32_t op, const sml_packet_burst* burst) {
+    if (!s || op > SML_BURST_EXCHANGE) return SML_ERR_INVALID_ARG;
+    sml_status_t st = sml::check_burst(burst, op == SML_BURST_EXCHANGE);
+    if (st != SML_OK || burst->count == 0) return st;
+    if ((op != SML_BURST_POST && !burst->in) || (op != SML_BURST_PRE && !burst->out)) return SML_ERR_INVALID_ARG;
+    if (burst->packet_numel != s->packet_numel || ((burst->flags & SML_FLAG_ROUND_RNE) != 0) != s->rne)
+        return SML_ERR_INVALID_ARG;   // fixed per server
+    // not running, left its loop, or close to its idle exit: (re)start it, so
+    // the doorbell below never races an idle exit
+    if (!s->launched || any_exited(s) ||
+        std::chrono::steady_clock::now() - s->last_activity > s->restart_after) {
+        st = server_launch(s);
+        if (st != SML_OK) return st;
+    }
+    memcpy(&s->ctl->burst, burst, sizeof(sml_packet_burst));
+    __atomic_store_n(&s->ctl->op, op, __ATOMIC_RELEASE);
+    __atomic_store_n(&s->ctl->doorbell, ++s->seq, __ATOMIC_RELEASE);
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+    for (uint32_t spins = 0; host_load(&s->ctl->done) != s->seq; spins++) {
+        if ((spins & 255) != 255) continue;
+        if (any_exited(s) && host_load(&s->ctl->done) != s->seq) {
+            (void)server_join(s);
+            strncpy(sml::g_last_error, "burst server: a workgroup left its loop during a burst",
+                    sizeof(sml::g_last_error) - 1);
+            return SML_ERR_HIP;
+        }
+        if (std::chrono::steady_clock::now() > t_end) {
+            (void)server_join(s);
+            strncpy(sml::g_last_error, "burst server: no completion within 10 s", sizeof(sml::g_last_error) - 1);
+            return SML_ERR_HIP;
+        }
+    }
+    s->last_activity = std::chrono::steady_clock::now();
+    return SML_OK;
+}
+
+sml_status_t sml_burst_server_stop(sml_burst_server* s) {
+    if (!s) return SML_ERR_INVALID_ARG;
+    return server_join(s);
+}
+
+sml_status_t sml_burst_server_destroy(sml_burst_server* s) {
+    if (!s) return SML_OK;
+    const sml_status_t st = sml_burst_server_stop(s);
+    (void)hipStreamDestroy(s->stream);
+    (void)hipFree(s->arrive);
+    (void)hipHostFree(s->ctl);
+    delete s;
+    return st;
 }
 
 }  // extern "C"

@@ -151,6 +151,14 @@ def lib():
     L.sml_postprocess_burst.argtypes = [ctypes.POINTER(PacketBurst), vp]
     L.sml_exchange_burst.restype = i32
     L.sml_exchange_burst.argtypes = [ctypes.POINTER(PacketBurst), vp]
+    L.sml_burst_server_create.restype = i32
+    L.sml_burst_server_create.argtypes = [u32, u32, u32, ctypes.POINTER(vp)]
+    L.sml_burst_server_submit.restype = i32
+    L.sml_burst_server_submit.argtypes = [vp, u32, ctypes.POINTER(PacketBurst)]
+    L.sml_burst_server_destroy.restype = i32
+    L.sml_burst_server_destroy.argtypes = [vp]
+    L.sml_burst_server_stop.restype = i32
+    L.sml_burst_server_stop.argtypes = [vp]
     L.sml_ipc_handle_bytes.restype = u32
     L.sml_ipc_get_handle.restype = i32
     L.sml_ipc_get_handle.argtypes = [vp, vp, ctypes.POINTER(u64)]
@@ -492,6 +500,37 @@ def exchange_burst(burst: PacketBurst, stream=None, like=None):
     post + ReusePacket) in one launch; FLAG_PROCESS_PACKET applies the dummy
     backend's ProcessPacket (x W) first."""
     _check("sml_exchange_burst", lib().sml_exchange_burst(ctypes.byref(burst), _stream(stream, like)))
+
+
+BURST_PRE, BURST_POST, BURST_EXCHANGE = 0, 1, 2
+
+
+class BurstServer:
+    """sml_burst_server_*: a persistent workgroup that runs bursts submitted
+    through a doorbell in host memory (for packet buffers in pinned host
+    memory).  submit() returns with the burst complete; close() stops it."""
+
+    def __init__(self, packet_numel: int, flags: int = 0, idle_ms: int = 100):
+        self._h = ctypes.c_void_p()
+        _check("sml_burst_server_create", lib().sml_burst_server_create(packet_numel, flags, idle_ms,
+                                                                        ctypes.byref(self._h)))
+
+    def submit(self, op: int, burst: PacketBurst):
+        _check("sml_burst_server_submit", lib().sml_burst_server_submit(self._h, op, ctypes.byref(burst)))
+
+    def stop(self):
+        """Leave the loop now (the next submit restarts it)."""
+        _check("sml_burst_server_stop", lib().sml_burst_server_stop(self._h))
+
+    def close(self):
+        if self._h:
+            h, self._h = self._h, None
+            _check("sml_burst_server_destroy", lib().sml_burst_server_destroy(h))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().sml_burst_server_destroy(self._h)
+            self._h = None
 
 
 def release_to_peers(stream=None, device=None):

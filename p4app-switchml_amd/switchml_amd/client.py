@@ -62,7 +62,8 @@ def make_config(**kw) -> str:
         "rank", "num_workers", "num_worker_threads", "max_outstanding_packets", "packet_numel",
         "backend", "scheduler", "prepostprocessor", "instant_job_completion")}
     dummy = {k: v for k, v in kw.items() if k in ("bandwidth", "process_packets", "fail_worker_thread")}
-    hip = {k: v for k, v in kw.items() if k in ("device", "mode", "packet_ring", "batch_jobs", "coalesce_us")}
+    hip = {k: v for k, v in kw.items() if k in ("device", "mode", "packet_ring", "burst_server", "batch_jobs",
+                                                     "coalesce_us")}
     xgmi = {k: v for k, v in kw.items() if k in ("session", "max_slice_numel", "timeout_ms")}
     unknown = set(kw) - set(general) - set(dummy) - set(hip) - set(xgmi)
     if unknown:

@@ -114,6 +114,18 @@ def test_burst_validation_without_gpu(sw):
     assert L.sml_exchange_burst(burst([1], b=17), None) == bad  # b > B
 
 
+def test_burst_server_validation_without_gpu(sw):
+    """The burst server's entry points refuse bad arguments before any HIP
+    call: no server, an unsupported packet size, unknown flags."""
+    L = sw.lib()
+    h = ctypes.c_void_p()
+    assert L.sml_burst_server_create(100, 0, 0, ctypes.byref(h)) == sw.SML_ERR_UNSUPPORTED
+    assert L.sml_burst_server_create(256, 0x8, 0, ctypes.byref(h)) == sw.SML_ERR_INVALID_ARG
+    assert L.sml_burst_server_submit(None, 0, None) == sw.SML_ERR_INVALID_ARG
+    assert L.sml_burst_server_stop(None) == sw.SML_ERR_INVALID_ARG
+    assert L.sml_burst_server_destroy(None) == sw.SML_OK
+
+
 def test_grid_limit_knob(sw):
     prev = sw.set_grid_limit(1024)
     assert sw.set_grid_limit(prev) == 1024

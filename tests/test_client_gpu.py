@@ -54,17 +54,19 @@ def test_allreduce_float_host_tensors(C, mode, T, W, P):
     C.stop()
 
 
-@pytest.mark.parametrize("ring", ["device", "pinned", "pageable"])
+@pytest.mark.parametrize("ring", ["device", "pinned", "pageable", "pinned+server"])
 @pytest.mark.parametrize("T,W,P,n", [(2, 2, 256, 20_011), (1, 3, 64, 4_099), (3, 8, 1024, 30_001)])
 def test_packet_mode_ring_placements(C, ring, T, W, P, n):
     """The per-LTU PreprocessSingle / PostprocessSingle calls with the packet
     ring in HBM (kernels write / read the packets in place, stream-ordered),
-    in pinned host memory (kernels over PCIe, synchronous calls) and in
+    in pinned host memory (kernels over PCIe, synchronous calls; "+server":
+    through the persistent burst server, backend.hip.burst_server) and in
     pageable host memory (staged through HBM): the reference's packet stream
     (dummy_worker_thread.cc:86-177), bit-exact with the oracle, FLOAT32
     and INT32."""
+    place, server = ring.split("+")[0], ring.endswith("+server")
     C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, max_outstanding_packets=16 * T,
-                          mode="packet", packet_ring=ring, bandwidth=0))
+                          mode="packet", packet_ring=place, burst_server=server, bandwidth=0))
     x = O.splitmix_normal(n + W, n)
     ref = O.dummy_allreduce(x, P=P, max_outstanding_packets=16 * T, num_worker_threads=T, num_workers=W)
     out = np.empty_like(x)

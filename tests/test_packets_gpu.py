@@ -289,13 +289,16 @@ def test_exchange_int32_window_and_argument_checks(cuda, ring):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P,W,n,b_max,ring,seed", [
-    (256, 2, 60_001, 64, "device", 1),
-    (256, 3, 33_333, 32, "pinned", 2),
-    (1024, 8, 50_000, 16, "device", 3),
-    (64, 1, 9_999, 48, "pinned", 4),
+@pytest.mark.parametrize("P,W,n,b_max,ring,seed,server", [
+    (256, 2, 60_001, 64, "device", 1, False),
+    (256, 3, 33_333, 32, "pinned", 2, False),
+    (1024, 8, 50_000, 16, "device", 3, False),
+    (64, 1, 9_999, 48, "pinned", 4, False),
+    (256, 3, 33_333, 32, "pinned", 5, True),
+    (1024, 5, 50_000, 16, "pinned", 6, True),
+    (128, 2, 20_001, 64, "device", 7, True),
 ])
-def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring, seed):
+def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring, seed, server):
     """DummyBackend::ReceiveBurst delivers a RANDOM subset of the pending
     packets in random order (dummy_backend.cc:99-118: k = rand() % (pending +
     1), each a random pending index), ProcessPacket (x W) on receipt; the
@@ -306,7 +309,8 @@ def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring,
     bit (slots are independent, so the delivery order cannot change a byte).
     Before every receive, up to three outstanding packets are re-built into
     spare buffers, as the DPDK timeout path re-sends them, and must equal the
-    packets in flight byte for byte."""
+    packets in flight byte for byte.  `server`: every burst goes through the
+    persistent burst server (sml_burst_server_submit) instead of a launch."""
     import torch
     s = sw()
     rng = np.random.default_rng(seed)
@@ -325,6 +329,15 @@ def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring,
         ex = torch.zeros(b * 2, dtype=torch.uint8).pin_memory()
     rbase, ebase = rg.data_ptr(), ex.data_ptr()
     stream = torch.cuda.current_stream(cuda)
+    srv = s.BurstServer(P) if server else None
+
+    def run(op, bt):
+        if srv is not None:
+            srv.submit(op, bt)
+        elif op == s.BURST_PRE:
+            s.preprocess_burst(bt, stream)
+        else:
+            s.exchange_burst(bt, stream)
 
     def capture(ids):
         rh = rg.cpu().numpy().view(np.uint32).reshape(b, P)
@@ -338,8 +351,8 @@ def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring,
                 assert np.array_equal(rh[sl, :m], pp[q, :m].view(np.uint32)), f"payload of packet {q}"
 
     first = list(range(b))
-    s.preprocess_burst(s.packet_burst(xd, out, P, W, b, recv, first, [rbase + q * P * 4 for q in first],
-                                      [ebase + q * 2 for q in first]), stream)
+    run(s.BURST_PRE, s.packet_burst(xd, out, P, W, b, recv, first, [rbase + q * P * 4 for q in first],
+                                    [ebase + q * 2 for q in first]))
     torch.cuda.synchronize()
     capture(first)
     # the DPDK timer path re-builds a packet that timed out (ResendPacketCallback
@@ -354,9 +367,9 @@ def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring,
         spare_x = torch.zeros(6, dtype=torch.uint8).pin_memory()
 
     def resend_matches(ids):
-        s.preprocess_burst(s.packet_burst(xd, out, P, W, b, recv, ids,
-                                          [spare.data_ptr() + i * P * 4 for i in range(len(ids))],
-                                          [spare_x.data_ptr() + i * 2 for i in range(len(ids))]), stream)
+        run(s.BURST_PRE, s.packet_burst(xd, out, P, W, b, recv, ids,
+                                        [spare.data_ptr() + i * P * 4 for i in range(len(ids))],
+                                        [spare_x.data_ptr() + i * 2 for i in range(len(ids))]))
         torch.cuda.synchronize()
         rh = rg.cpu().numpy().view(np.uint32).reshape(b, P)
         sh = spare.cpu().numpy().view(np.uint32).reshape(3, P)
@@ -381,10 +394,54 @@ def test_exchange_random_delivery_like_dummy_backend(cuda, P, W, n, b_max, ring,
         received += len(got)
         bt = s.packet_burst(xd, out, P, W, b, recv, got, [rbase + (q % b) * P * 4 for q in got],
                             [ebase + (q % b) * 2 for q in got], flags=s.FLAG_PROCESS_PACKET)
-        s.exchange_burst(bt, stream)
+        run(s.BURST_EXCHANGE, bt)
         torch.cuda.synchronize()
         nxt = [q + b for q in got if q + b < total]
         capture(nxt)
         pending.extend(nxt)
     assert not pending
+    if srv is not None:
+        srv.close()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), ref_out.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_burst_server_idle_restart_and_refusals(cuda):
+    """The server leaves its loop after idle_ms without a doorbell and the next
+    submit starts another (the burst still completes, bit-exact); a burst with
+    another packet size or rounding mode than the server's is refused; close()
+    of a server that never ran, and twice, is fine."""
+    import time
+    import torch
+    s = sw()
+    P, W, n = 256, 2, 20_000
+    x = O.splitmix_normal(17, n)
+    xd = torch.from_numpy(x).to(cuda)
+    out = torch.zeros(n, device=cuda)
+    B = O.num_blocks(n, P)
+    b = 16
+    recv = torch.zeros(B, dtype=torch.int8, device=cuda)
+    ring = torch.zeros(b * P, dtype=torch.int32).pin_memory()
+    extra = torch.zeros(b * 2, dtype=torch.uint8).pin_memory()
+    s.BurstServer(P).close()                                   # never started
+    srv = s.BurstServer(P, idle_ms=20)
+    ids = list(range(b))
+    slots = [ring.data_ptr() + q * P * 4 for q in ids]
+    exs = [extra.data_ptr() + q * 2 for q in ids]
+    srv.submit(s.BURST_PRE, s.packet_burst(xd, out, P, W, b, recv, ids, slots, exs))
+    for p0 in range(0, B + b, b):
+        time.sleep(0.05)                                       # > idle_ms: the server has left its loop
+        got = list(range(p0, min(p0 + b, B + b)))
+        srv.submit(s.BURST_EXCHANGE, s.packet_burst(xd, out, P, W, b, recv, got, slots[:len(got)], exs[:len(got)],
+                                                    flags=s.FLAG_PROCESS_PACKET))
+        if p0 == b:
+            srv.stop()                                         # stopped explicitly: restarted by the next submit
+    ref = O.dummy_packet_stream(x, P=P, batch_max=b, num_workers=W)[2]
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    with pytest.raises(s.SwitchMLError):                       # another packet size
+        srv.submit(s.BURST_PRE, s.packet_burst(xd, out, 64, W, b, recv, [0], slots[:1], exs[:1]))
+    with pytest.raises(s.SwitchMLError):                       # another rounding mode
+        srv.submit(s.BURST_PRE, s.packet_burst(xd, out, P, W, b, recv, [0], slots[:1], exs[:1],
+                                               flags=s.FLAG_ROUND_RNE))
+    srv.close()
+    srv.close()

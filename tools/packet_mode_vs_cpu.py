@@ -41,7 +41,11 @@ def gpu_packet_mode(numel, T, W, jobs=7):
     with tempfile.NamedTemporaryFile("w", suffix=".cfg", delete=False) as f:
         f.write("[backend.hip]\npacket_ring = pinned\n")
         pinned_cfg = f.name
+    with tempfile.NamedTemporaryFile("w", suffix=".cfg", delete=False) as f:
+        f.write("[backend.hip]\npacket_ring = pinned\nburst_server = true\n")
+        server_cfg = f.name
     for name, mode, extra in (("packet", "packet", []), ("packet_pinned_ring", "packet", ["--config", pinned_cfg]),
+                              ("packet_pinned_ring_burst_server", "packet", ["--config", server_cfg]),
                               ("bulk", "bulk", []), ("fused", "fused", [])):
         r = subprocess.run([exe, "--tensor-numel", str(numel), "--tensor-type", "float", "--num-workers", str(W),
                             "--num-worker-threads", str(T), "--bandwidth", "0", "--device", "gpu", "--mode", mode,
@@ -51,6 +55,7 @@ def gpu_packet_mode(numel, T, W, jobs=7):
         ns = [int(m) for m in re.findall(r"Duration: #(\d+)# ns", r.stdout)]
         res[name] = {"median_ms": median(ns) / 1e6, "jobs": len(ns)}
     os.unlink(pinned_cfg)
+    os.unlink(server_cfg)
     return res
 
 
@@ -85,6 +90,8 @@ def main():
            "packet_mode_vs_cpu_preprocess_only": round(c["preprocess_only"]["median_ms"] / g["packet"]["median_ms"], 3),
            "pinned_ring_vs_cpu_roundtrip": round(c["roundtrip"]["median_ms"] /
                                                  g["packet_pinned_ring"]["median_ms"], 3),
+           "pinned_ring_burst_server_vs_cpu_roundtrip": round(c["roundtrip"]["median_ms"] /
+                                                              g["packet_pinned_ring_burst_server"]["median_ms"], 3),
            "note": ("GPU packet mode = the whole all-reduce (per-packet ProcessPacket + post + pre through the "
                     "HIP PPP's exchange bursts: PostprocessReuseBurst, one launch per pass over the b-slot ring; "
                     "device ring, and a pinned host ring like a NIC's mbuf pool); CPU = the oracle's restatement "
