@@ -68,10 +68,14 @@ __device__ __forceinline__ void preprocess_one(const sml_packet_burst& a, uint32
             const uint64_t j = (uint64_t)u * 256 + lane * 4;
             const f4 x = act ? load4_guarded(in + j, j, n) : mkf4(0, 0, 0, 0);
             const u4 w = quantize4<RNE>(x, s, j, body);
-            if (act && j + 0 < n) dst[j + 0] = bswap(w.x);
-            if (act && j + 1 < n) dst[j + 1] = bswap(w.y);
-            if (act && j + 2 < n) dst[j + 2] = bswap(w.z);
-            if (act && j + 3 < n) dst[j + 3] = bswap(w.w);
+            if (act && j + 4 <= n) {
+                *reinterpret_cast<u4a*>(dst + j) = u4a{bswap(w.x), bswap(w.y), bswap(w.z), bswap(w.w)};
+            } else {
+                if (act && j + 0 < n) dst[j + 0] = bswap(w.x);
+                if (act && j + 1 < n) dst[j + 1] = bswap(w.y);
+                if (act && j + 2 < n) dst[j + 2] = bswap(w.z);
+                if (act && j + 3 < n) dst[j + 3] = bswap(w.w);
+            }
         }
     }
     if (q < B) {
@@ -115,12 +119,19 @@ __device__ __forceinline__ void postprocess_one(const sml_packet_burst& a, uint3
         const float s = scale_for(a.num_workers, (int)a.recv_exps[k]);
         float* out = a.out + off;
 #pragma unroll
-        for (int u = 0; u < U; u++)
+        for (int u = 0; u < U; u++) {
+            const uint64_t j = (uint64_t)u * 256 + lane * 4;
+            if (act && j + 4 <= n) {   // one 16-B read of the packet per lane
+                const u4a v = *reinterpret_cast<const u4a*>(src + j);
+                const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const uint64_t j = (uint64_t)u * 256 + lane * 4 + t;
-                if (act && j < n) out[j] = dequantize1(bswap(src[j]), s);
+                for (int t = 0; t < 4; t++) out[j + t] = dequantize1(bswap(vv[t]), s);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    if (act && j + t < n) out[j + t] = dequantize1(bswap(src[j + t]), s);
             }
+        }
     }
     if (q < B && lane == 0) a.recv_exps[q] = *static_cast<const int8_t*>(a.extras[i]);
 }
@@ -169,10 +180,16 @@ __device__ __forceinline__ void exchange_one(const sml_packet_burst& a, uint32_t
     f4 xq[U], xe[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
+        {   // one 16-B access per lane where the group is whole (a packet over
+            // PCIe then costs one read per 64 B line, not four)
+            const uint64_t j = (uint64_t)u * 256 + lane * 4;
+            if (act && j + 4 <= n_read) {
+                const u4a v = *reinterpret_cast<const u4a*>(ent + j);
+                w[u][0] = v.x, w[u][1] = v.y, w[u][2] = v.z, w[u][3] = v.w;
+            } else {
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const uint64_t j = (uint64_t)u * 256 + lane * 4 + t;
-            w[u][t] = act && j < n_read ? ent[j] : 0u;
+                for (int t = 0; t < 4; t++) w[u][t] = act && j + t < n_read ? ent[j + t] : 0u;
+            }
         }
         const uint64_t j = (uint64_t)u * 256 + lane * 4;
         if (flt) {
@@ -233,12 +250,16 @@ __device__ __forceinline__ void exchange_one(const sml_packet_burst& a, uint32_t
     // the buffer's words: the new packet's, or (PROC) the processed ones
     const uint64_t n_write = PROC ? P : n_pre;
 #pragma unroll
-    for (int u = 0; u < U; u++)
+    for (int u = 0; u < U; u++) {
+        const uint64_t j = (uint64_t)u * 256 + lane * 4;
+        if (act && j + 4 <= n_write) {
+            *reinterpret_cast<u4a*>(ent + j) = u4a{w[u][0], w[u][1], w[u][2], w[u][3]};
+        } else {
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const uint64_t j = (uint64_t)u * 256 + lane * 4 + t;
-            if (act && j < n_write) ent[j] = w[u][t];
+            for (int t = 0; t < 4; t++)
+                if (act && j + t < n_write) ent[j + t] = w[u][t];
         }
+    }
     if (pre_exp) {
         uint32_t m = 0;
 #pragma unroll
@@ -288,9 +309,9 @@ constexpr int kServerThreads = 1024;
 constexpr int kServerGroups = SML_MAX_BURST / (kServerThreads / kWave);   // 4
 
 struct alignas(64) ServerCtl {
-    uint64_t doorbell;         // host: sequence number of the last submitted burst
-    uint32_t op;               // host: SML_BURST_* of that burst
+    uint64_t doorbell;         // host: (sequence number << 2) | SML_BURST_* of the last submitted burst
     uint32_t stop;             // host: 1 = leave the loop
+    uint32_t pad_stop;
     uint64_t pad0[6];
     uint64_t done;             // device: sequence number of the last completed burst
     uint32_t exited[kServerGroups];   // device: workgroup g has left its loop
@@ -323,12 +344,13 @@ __global__ __launch_bounds__(kServerThreads) void k_burst_server(ServerCtl* ctl,
             uint64_t db = seen;
             for (;;) {
                 if (sys_poll(&ctl->stop)) break;
-                db = sys_poll(&ctl->doorbell);
+                db = sys_poll(&ctl->doorbell) >> 2;
                 if (db != seen) {
                     // acquire once, by the thread that saw the doorbell; the
-                    // barrier below orders every other thread after it
+                    // barrier below orders every other thread after it.  The
+                    // op rides in the doorbell word (no second round trip).
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                    cmd = (int)sys_poll(&ctl->op);
+                    cmd = (int)(sys_poll(&ctl->doorbell) & 3u);
                     break;
                 }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;
@@ -340,9 +362,10 @@ __global__ __launch_bounds__(kServerThreads) void k_burst_server(ServerCtl* ctl,
         __syncthreads();
         const int cmd = s_cmd;
         if (cmd < 0) break;
-        constexpr uint32_t kWords = sizeof(sml_packet_burst) / 4;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&ctl->burst);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&sa);
+        static_assert(sizeof(sml_packet_burst) % 8 == 0, "descriptor copied in 8-byte words");
+        constexpr uint32_t kWords = sizeof(sml_packet_burst) / 8;
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(&ctl->burst);
+        uint64_t* dst = reinterpret_cast<uint64_t*>(&sa);
         for (uint32_t k = tid; k < kWords; k += kServerThreads)
             dst[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __syncthreads();
@@ -593,8 +616,7 @@ sml_status_t sml_burst_server_submit(sml_burst_server* s, uint32_t op, const sml
         if (st != SML_OK) return st;
     }
     memcpy(&s->ctl->burst, burst, sizeof(sml_packet_burst));
-    __atomic_store_n(&s->ctl->op, op, __ATOMIC_RELEASE);
-    __atomic_store_n(&s->ctl->doorbell, ++s->seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&s->ctl->doorbell, (++s->seq << 2) | op, __ATOMIC_RELEASE);
     const auto t_end = std::chrono::steady_clock::now() + std::chrono::seconds(10);
     for (uint32_t spins = 0; host_load(&s->ctl->done) != s->seq; spins++) {
         if ((spins & 255) != 255) continue;
