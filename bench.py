@@ -22,6 +22,8 @@ switch simulation with W = N real workers (each holding its own 1 GiB bucket):
   xgmi_switch the client's Context::AllReduce with backend = xgmi (the
               native in-node switch: shm rendezvous, exponent max over the
               peers' planes, K3, K6 on this rank's shard, gather)
+  xgmi_switch_push  the same in its push form (backend.xgmi.push: K3 writes
+              each shard into its owner's inbox over xGMI, K6 reads local HBM)
 each checked (bit-equal to each other, and within the quantization bound of
 an fp32 all-reduce of the same buckets) and set against its xGMI bound; and
 configs4_plugin: the ResNet-50 buckets through the CollNet plugin table on an
@@ -552,7 +554,7 @@ def main():
             fields.update(exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev))
         except Exception as e:  # noqa: BLE001 - recorded, then the run fails
             fields["switchsim"] = {"error": repr(e)[:400]}
-        for k in ("switchsim", "p2p_switch", "xgmi_switch"):
+        for k in ("switchsim", "p2p_switch", "xgmi_switch", "xgmi_switch_push"):
             f = fields.get(k, {})
             if "error" in f or not f.get("verified", False):
                 diag_failures.append(f"{k}: {f.get('error', 'not verified')}")
@@ -764,7 +766,7 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
       p2p_switch  the payload summed at the reader from the peers' planes
                   mapped over xGMI (K6), fp32 shards all-gathered
       xgmi_switch the same switch natively in the client runtime
-                  (Context::AllReduce, backend = xgmi)
+                  (Context::AllReduce, backend = xgmi), pull and push forms
     Verified: the two outputs are bit-identical, and both are within the
     quantization bound of an fp32 all-reduce of the same buckets.  Timed:
     max over ranks of the mean of `reps` calls.  xGMI bound: each GPU moves
@@ -870,50 +872,57 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
         except Exception as e:  # noqa: BLE001
             res[name] = {"error": repr(e)[:400], "pipeline": pipe}
     # the native in-node switch: the client's Context with backend = xgmi
-    # (C++ runtime, no torch.distributed in the data path)
-    pipe = ("Context::AllReduce, backend xgmi: K2 -> int8 max over the peers' exponent planes -> K3 BE -> K6 on "
-            "this worker's shard over the peers' planes (hipIpc, xGMI) -> gather of the W shards")
-    try:
-        from switchml_amd import client as C
-        session = [f"bench-xgmi-{os.getpid()}-{int(time.time() * 1e3)}" if rank == 0 else None]
-        dist.broadcast_object_list(session, src=0)
-        if C.state() == C.RUNNING:
+    # (C++ runtime, no torch.distributed in the data path), in its pull form
+    # (K6 reads the peers' planes over xGMI) and its push form (K3 writes
+    # each shard into its owner's inbox over xGMI; backend.xgmi.push)
+    for name, push in (("xgmi_switch", False), ("xgmi_switch_push", True)):
+        pipe = ("Context::AllReduce, backend xgmi: K2 -> int8 max over the peers' exponent planes -> " +
+                ("K3 writing each shard into its owner's inbox (hipIpc, xGMI) -> K6 on this worker's shard over "
+                 "the local inbox" if push else
+                 "K3 BE -> K6 on this worker's shard over the peers' planes (hipIpc, xGMI)") +
+                " -> gather of the W shards")
+        try:
+            from switchml_amd import client as C
+            session = [f"bench-xgmi-{os.getpid()}-{int(time.time() * 1e3)}-{int(push)}" if rank == 0 else None]
+            dist.broadcast_object_list(session, src=0)
+            if C.state() == C.RUNNING:
+                C.stop()
+            C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=1, packet_numel=P,
+                                  max_outstanding_packets=256, mode="bulk", bandwidth=0, device=dev.index,
+                                  session=session[0], max_slice_numel=64 << 20, push=push))
+            out = torch.empty_like(x)
+            C.allreduce(x, out)
+            torch.cuda.synchronize()
+            err = (out - ref).abs()
+            within = bool((err <= tol).all().item())
+            touts = [torch.empty_like(x) for _ in range(reps)]
+            dist.barrier()
+            t0 = time.perf_counter()
+            for i in range(reps):
+                C.allreduce(x, touts[i])
+            torch.cuda.synchronize()
+            tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = float(tt[0])
             C.stop()
-        C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=1, packet_numel=P,
-                              max_outstanding_packets=256, mode="bulk", bandwidth=0, device=dev.index,
-                              session=session[0], max_slice_numel=64 << 20))
-        out = torch.empty_like(x)
-        C.allreduce(x, out)
-        torch.cuda.synchronize()
-        err = (out - ref).abs()
-        within = bool((err <= tol).all().item())
-        touts = [torch.empty_like(x) for _ in range(reps)]
-        dist.barrier()
-        t0 = time.perf_counter()
-        for i in range(reps):
-            C.allreduce(x, touts[i])
-        torch.cuda.synchronize()
-        tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt[0])
-        C.stop()
-        same = all(bool(torch.equal(o, out)) for o in touts)
-        del touts
-        ok_t = torch.tensor([int(within), int(same)], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
-        same = bool(ok_t[1].item())
-        outs["xgmi_switch"] = out
-        res["xgmi_switch"] = {"workers": W, "numel_per_worker": n, "packet_numel": P,
-                              "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * n / t / 1e9, 2),
-                              "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
-                              "xgmi_bound_ms": round(bound_s * 1e3, 3), "frac_of_xgmi_bound": round(bound_s / t, 4),
-                              "within_quantization_bound": bool(ok_t[0].item()), "timed_calls_equal_first": same,
-                              "max_abs_err_vs_fp32_allreduce": float(err.max().item()), "pipeline": pipe}
-        del err
-    except Exception as e:  # noqa: BLE001
-        res["xgmi_switch"] = {"error": repr(e)[:400], "pipeline": pipe}
+            same = all(bool(torch.equal(o, out)) for o in touts)
+            del touts
+            ok_t = torch.tensor([int(within), int(same)], dtype=torch.int32, device=dev)
+            dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+            same = bool(ok_t[1].item())
+            outs[name] = out
+            res[name] = {"workers": W, "numel_per_worker": n, "packet_numel": P,
+                         "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * n / t / 1e9, 2),
+                         "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
+                         "xgmi_bound_ms": round(bound_s * 1e3, 3), "frac_of_xgmi_bound": round(bound_s / t, 4),
+                         "within_quantization_bound": bool(ok_t[0].item()), "timed_calls_equal_first": same,
+                         "max_abs_err_vs_fp32_allreduce": float(err.max().item()), "pipeline": pipe}
+            del err
+        except Exception as e:  # noqa: BLE001
+            res[name] = {"error": repr(e)[:400], "pipeline": pipe}
     # the three paths compute the same switch: bit-equal outputs
-    names = [k for k in ("switchsim", "p2p_switch", "xgmi_switch") if k in outs]
+    paths = ("switchsim", "p2p_switch", "xgmi_switch", "xgmi_switch_push")
+    names = [k for k in paths if k in outs]
     eqs = {}
     for k in names:
         if k == "switchsim" or "switchsim" not in outs:
@@ -921,7 +930,7 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
         eq = torch.tensor([int(torch.equal(outs["switchsim"], outs[k]))], dtype=torch.int32, device=dev)
         dist.all_reduce(eq, op=dist.ReduceOp.MIN)
         eqs[k] = bool(eq.item())
-    for name in ("switchsim", "p2p_switch", "xgmi_switch"):
+    for name in paths:
         r = res[name]
         if "error" not in r:
             same = all(eqs.values()) if name == "switchsim" else eqs.get(name)

@@ -73,6 +73,12 @@ struct XgmiBackendConfig {
     std::string session;
     uint64_t max_slice_numel = 16ull << 20;   // exchange chunk (elements) and plane size per worker thread
     uint64_t timeout_ms = 60000;              // a worker missing a barrier this long fails the slice
+    // FLOAT32 exchange direction: false = every worker's K6 READS its shard
+    // of the W payload planes over xGMI (pull); true = every worker's K3
+    // WRITES each shard of its payload straight into the owner's inbox over
+    // xGMI and K6 reads only local HBM (push).  Same bytes; all workers of a
+    // session must agree.  The multicast (gather) pulls in both.
+    bool push = false;
 };
 
 struct BackendConfig {

@@ -55,6 +55,7 @@ struct XgmiShm {
     std::atomic<uint32_t> poisoned;        // a worker failed inside an exchange: every later barrier throws
     std::atomic<uint32_t> attached;
     std::atomic<uint32_t> detached;
+    uint32_t push;                         // backend.xgmi.push of worker 0 (every worker must match)
     ShmBarrier bar[kMaxT + 1];             // [t]: worker thread t; [kMaxT]: setup / teardown
     ShmPlanes planes[kMaxW][kMaxT];
 };
@@ -86,6 +87,7 @@ void XgmiSwitch::OpenSegment() {
                 shm_->T = (uint32_t)T_;
                 shm_->P = P_;
                 shm_->cap = cap_;
+                shm_->push = push_ ? 1u : 0u;
                 shm_->creator_pid.store(getpid());
                 shm_->magic.store(kMagic, std::memory_order_release);
                 return;
@@ -138,6 +140,7 @@ XgmiSwitch::XgmiSwitch(const Config& config, int device) {
     P_ = (uint32_t)g.packet_numel;
     cap_ = (config.backend_.xgmi.max_slice_numel + 1023) / 1024 * 1024;
     timeout_ms_ = config.backend_.xgmi.timeout_ms;
+    push_ = config.backend_.xgmi.push;
     if (W_ < 1 || W_ > kMaxW) throw SwitchMLFatal("xgmi switch: num_workers must be 1..16");
     if (T_ < 1 || T_ > kMaxT) throw SwitchMLFatal("xgmi switch: num_worker_threads must be 1..16");
     if (rank_ < 0 || rank_ >= W_) throw SwitchMLFatal("xgmi switch: general.rank must be < num_workers");
@@ -162,7 +165,9 @@ void XgmiSwitch::Setup(int device) {
     for (int t = 0; t < T_; t++) {
         ThreadPlanes& tp = planes_[t];
         hip_ok(hipMalloc(&tp.exps, cap_b), "hipMalloc");
-        hip_ok(hipMalloc(&tp.payload, cap_ * 4), "hipMalloc");
+        // + W packets of the largest size: the inbox's W rows of ceil(B / W)
+        // blocks may exceed B blocks by up to W - 1 (push form)
+        hip_ok(hipMalloc(&tp.payload, (cap_ + (uint64_t)kMaxW * 1024) * 4), "hipMalloc");
         hip_ok(hipMalloc(&tp.out, cap_ * 4), "hipMalloc");
         hip_ok(hipMalloc(&tp.gexp, cap_b), "hipMalloc");
         hip_ok(hipStreamCreateWithFlags(&tp.xst, hipStreamNonBlocking), "hipStreamCreate");
@@ -177,9 +182,10 @@ void XgmiSwitch::Setup(int device) {
         sp.published.store(1, std::memory_order_release);
     }
     Barrier(kMaxT);   // every worker's handles are published
-    if (shm_->W != (uint32_t)W_ || shm_->T != (uint32_t)T_ || shm_->P != P_ || shm_->cap != cap_)
+    if (shm_->W != (uint32_t)W_ || shm_->T != (uint32_t)T_ || shm_->P != P_ || shm_->cap != cap_ ||
+        shm_->push != (push_ ? 1u : 0u))
         throw SwitchMLFatal("xgmi switch: workers disagree on num_workers / num_worker_threads / packet_numel / "
-                            "max_slice_numel");
+                            "max_slice_numel / push");
     for (int t = 0; t < T_; t++) {
         ThreadPlanes& tp = planes_[t];
         tp.peer_exps.resize(W_);
@@ -299,11 +305,26 @@ constexpr uint32_t kPeer = SML_FLAG_PEER_PLANES;   // the reader's half: acquire
 }  // namespace
 
 // The switch's exponent max over the W planes into gexp, then K3: quantize
-// with the global exponents into the own BE payload plane.
+// with the global exponents into the own BE payload plane (pull), or each
+// shard w straight into row `rank` of worker w's inbox (push: one K3 launch
+// per shard, W − 1 of them writing over xGMI).
 void XgmiSwitch::Quantize(ThreadPlanes& tp, const float* in, uint64_t n, hipStream_t st) {
     const uint64_t B = sml_num_blocks(n, P_);
     sml_ok(sml_switch_exps(tp.peer_exps.data(), (uint16_t)W_, B, tp.gexp, kPeer, st), "sml_switch_exps");
-    sml_ok(sml_quantize_pack(in, n, P_, (uint16_t)W_, tp.gexp, tp.payload, nullptr, 0, st), "sml_quantize_pack");
+    if (!push_) {
+        sml_ok(sml_quantize_pack(in, n, P_, (uint16_t)W_, tp.gexp, tp.payload, nullptr, 0, st), "sml_quantize_pack");
+        return;
+    }
+    const uint64_t S = (B + W_ - 1) / W_;
+    for (int w = 0; w < W_; w++) {
+        const uint64_t b0 = std::min<uint64_t>((uint64_t)w * S, B);
+        const uint64_t nb = std::min<uint64_t>(S, B - b0);
+        if (!nb) continue;
+        const uint64_t n_el = std::min<uint64_t>(nb * P_, n - b0 * P_);
+        int32_t* row = const_cast<int32_t*>(tp.peer_payload[w]) + (uint64_t)rank_ * S * P_;
+        sml_ok(sml_quantize_pack(in + b0 * P_, n_el, P_, (uint16_t)W_, tp.gexp + b0, row, nullptr, 0, st),
+               "sml_quantize_pack");
+    }
 }
 
 // K6: the wrapping sum of this worker's shard over the W planes, dequantized
@@ -318,7 +339,8 @@ void XgmiSwitch::Aggregate(ThreadPlanes& tp, uint64_t n, hipStream_t st) {
     const int32_t* planes[kMaxW];
     const int8_t* exps[kMaxW];
     for (int w = 0; w < W_; w++) {
-        planes[w] = tp.peer_payload[w] + blk0 * P_;
+        // pull: worker w's plane at this shard; push: row w of the own inbox
+        planes[w] = push_ ? tp.payload + (uint64_t)w * S * P_ : tp.peer_payload[w] + blk0 * P_;
         exps[w] = tp.gexp + blk0;
     }
     sml_ok(sml_switch_aggregate(planes, exps, (uint16_t)W_, n_el, P_, nullptr, nullptr, tp.out + blk0 * P_, kPeer,

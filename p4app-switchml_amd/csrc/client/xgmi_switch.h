@@ -28,8 +28,12 @@
 //     HBM work beside the xGMI phases), two barriers per chunk; one set of
 //     planes suffices because every plane's readers finish one phase before
 //     its next writer starts (xgmi_switch.cc, FloatSlice);
+//   * push form (backend.xgmi.push): K3 writes each shard of the quantized
+//     payload straight into its owner's inbox plane (W − 1 shards over xGMI,
+//     posted writes) and K6 reads the W rows of the own inbox from local HBM;
+//     same phases, barriers and bytes;
 //   * INT32 slices: the words themselves are summed (the INT32 PPP only
-//     reorders bytes, ppp.cc:158-190, 262-298).
+//     reorders bytes, ppp.cc:158-190, 262-298), pulled in both forms.
 // Results are bit-identical to the oracle's W-worker software switch
 // (orc_switch_exps / orc_switch_payload + dequantize), slice by slice.
 //
@@ -79,6 +83,9 @@ class XgmiSwitch {
   private:
     struct ThreadPlanes {
         int8_t* exps = nullptr;        // own planes (IPC-exported)
+        // the own BE payload plane (pull), or this worker's inbox (push): W
+        // rows of S blocks, row r = worker r's quantized share of this
+        // worker's shard
         int32_t* payload = nullptr;
         float* out = nullptr;
         int8_t* gexp = nullptr;        // local: the global exponents
@@ -102,6 +109,7 @@ class XgmiSwitch {
     uint32_t P_;
     uint64_t cap_;          // elements per chunk (multiple of 1024)
     uint64_t timeout_ms_;
+    bool push_ = false;     // backend.xgmi.push: K3 writes into the owners' inboxes
     std::string name_;
     XgmiShm* shm_ = nullptr;
     bool created_ = false;    // this worker (rank 0) created the segment

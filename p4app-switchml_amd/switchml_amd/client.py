@@ -64,7 +64,7 @@ def make_config(**kw) -> str:
     dummy = {k: v for k, v in kw.items() if k in ("bandwidth", "process_packets", "fail_worker_thread")}
     hip = {k: v for k, v in kw.items() if k in ("device", "mode", "packet_ring", "burst_server", "batch_jobs",
                                                      "coalesce_us")}
-    xgmi = {k: v for k, v in kw.items() if k in ("session", "max_slice_numel", "timeout_ms")}
+    xgmi = {k: v for k, v in kw.items() if k in ("session", "max_slice_numel", "timeout_ms", "push")}
     unknown = set(kw) - set(general) - set(dummy) - set(hip) - set(xgmi)
     if unknown:
         raise KeyError(f"unknown config keys {sorted(unknown)}")

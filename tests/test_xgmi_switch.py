@@ -49,13 +49,13 @@ def _paths():
             sys.path.insert(0, p)
 
 
-def _client_worker(rank, W, T, P, session, cap, q):
+def _client_worker(rank, W, T, P, session, cap, push, q):
     try:
         _paths()
         from switchml_amd import client as C
         C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=T, packet_numel=P,
                               max_outstanding_packets=64 * T, mode="bulk", bandwidth=0, device=0,
-                              session=session, max_slice_numel=cap))
+                              session=session, max_slice_numel=cap, push=push))
         res = []
         sizes = [100_003, 1, 3 * cap + 517, 0, 4 * P * W + 5]
         for i, n in enumerate(sizes):
@@ -96,29 +96,50 @@ def _client_worker(rank, W, T, P, session, cap, q):
         q.put((rank, None, traceback.format_exc()[-2000:]))
 
 
-def _run(target, W, args):
+def _run(target, W, args, timeout=240):
+    """Run `target` in W spawned worker processes; a worker that dies without
+    reporting (or a run past `timeout`) fails the test at once instead of
+    leaving the parent waiting on the queue."""
+    import queue
+    import time
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=target, args=(r, W) + args + (q,)) for r in range(W)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
+    res, t_end = [], time.time() + timeout
+    while len(res) < W:
+        try:
+            res.append(q.get(timeout=2))
+            continue
+        except queue.Empty:
+            pass
+        reported = {r[0] for r in res}
+        dead = [(i, p.exitcode) for i, p in enumerate(procs) if p.exitcode not in (None, 0) and i not in reported]
+        if dead or time.time() > t_end:
+            for p in procs:
+                if p.is_alive():
+                    p.kill()
+            pytest.fail(f"workers failed without a result (rank, exit code: {dead}) or timed out; "
+                        f"got {len(res)} of {W}")
     for p in procs:
         p.join(timeout=60)
     return res
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,T,P", [(2, 1, 256), (3, 2, 64), (4, 4, 1024)])
-def test_xgmi_backend_allreduce_matches_oracle_switch(cuda, W, T, P):
+@pytest.mark.parametrize("W,T,P,push", [(2, 1, 256, False), (3, 2, 64, False), (4, 4, 1024, False),
+                                        (2, 1, 256, True), (3, 2, 64, True), (5, 2, 1024, True)])
+def test_xgmi_backend_allreduce_matches_oracle_switch(cuda, W, T, P, push):
     """Context::AllReduce with backend = xgmi on W worker processes: FLOAT32
     buckets (device, pageable and pinned host tensors; in place and not;
     ragged sizes, one element, empty, and slices exchanged in several chunks of
     max_slice_numel), INT32 buckets, and four jobs in flight — every result
-    bit-exact against the oracle switch over the same W workers."""
+    bit-exact against the oracle switch over the same W workers, in the pull
+    and the push form (backend.xgmi.push: K3 writes into the owners' inboxes)."""
     session = "test-" + uuid.uuid4().hex
     cap = 8192 * (P // 64)
-    for rank, res, err in _run(_client_worker, W, (T, P, session, cap)):
+    for rank, res, err in _run(_client_worker, W, (T, P, session, cap, push)):
         assert res is not None, (rank, err)
         assert all(res), (rank, res)
 
@@ -234,7 +255,7 @@ def test_xgmi_replaces_stale_segment(cuda):
         import struct
         hdr = struct.pack("<IIIIQiIII", 0x534D4C58, 2, 1, 256, 1 << 20, dead_pid, 0, 2, 0)
         f.write(hdr + b"\0" * (1 << 16))
-    for rank, res, err in _run(_client_worker, 2, (1, 256, session, 8192 * 4)):
+    for rank, res, err in _run(_client_worker, 2, (1, 256, session, 8192 * 4, False)):
         assert res is not None, (rank, err)
         assert all(res), (rank, res)
     assert not os.path.exists(path)
