@@ -353,6 +353,10 @@ void XgmiSwitch::Aggregate(ThreadPlanes& tp, uint64_t n, hipStream_t st) {
 //   prologue   K2(0) | barrier | max + K3(0) | barrier
 //   chunk c    K6(c) on xst  beside  K2(c+1) on st          | barrier
 //              gather(c) on xst  beside  max + K3(c+1) on st | barrier
+// Push form: chunk c's phase 1 also writes the own shard into every peer's
+// out plane, and phase 2's gather becomes one local copy of the own out plane
+// (all W shards are there after the barrier); the out plane is next written
+// in chunk c + 1's phase 1, after the barrier that ends phase 2.
 // Every plane's readers finish before the barrier that precedes its next
 // writer: exps (peers' max of chunk c+1, phase 2) before K2(c+2) (phase 1 of
 // the next chunk); payload (peers' K6(c), phase 1) before K3(c+1) (phase 2);
@@ -375,6 +379,7 @@ void XgmiSwitch::FloatSlice(int tid, const float* in, float* out, uint64_t numel
         const bool next = c + 1 < nchunks;
         const float* in_next = in + (c + 1) * cap_;
         Aggregate(tp, n, tp.xst);
+        if (push_) PushShard(tp, n, B, S, tp.xst);   // the multicast, as writes into the peers' out planes
         release(tp.xst);
         if (next) {
             sml_ok(sml_exponents(in_next, len(c + 1), P_, tp.exps, st), "sml_exponents");
@@ -383,7 +388,13 @@ void XgmiSwitch::FloatSlice(int tid, const float* in, float* out, uint64_t numel
         stream_sync(tp.xst);
         stream_sync(st);
         Barrier(tid);
-        Gather(tp, out + c * cap_, n, B, S, tp.xst);
+        if (push_) {   // every shard is in the own out plane now: one local copy
+            const void* src = tp.out;
+            void* dst = out + c * cap_;
+            sml_ok(sml_copy_segments(&src, &dst, &n, 1, kPeer, tp.xst), "sml_copy_segments");
+        } else {
+            Gather(tp, out + c * cap_, n, B, S, tp.xst);
+        }
         if (next) {
             Quantize(tp, in_next, len(c + 1), st);
             release(st);
@@ -392,6 +403,29 @@ void XgmiSwitch::FloatSlice(int tid, const float* in, float* out, uint64_t numel
         stream_sync(st);
         Barrier(tid);   // peers are done reading our planes before they are written again
     }
+}
+
+// Push form: this worker's dequantized shard (blocks [rank S, ...) of the own
+// out plane) written into the same place of every peer's out plane (W − 1
+// segments in one launch, over xGMI), so that after the next barrier every
+// out plane holds all W shards.
+void XgmiSwitch::PushShard(ThreadPlanes& tp, uint64_t n, uint64_t B, uint64_t S, hipStream_t st) {
+    const uint64_t b0 = std::min<uint64_t>((uint64_t)rank_ * S, B);
+    const uint64_t nb = std::min<uint64_t>(S, B - b0);
+    if (!nb || W_ == 1) return;
+    const uint64_t words = std::min<uint64_t>(nb * P_, n - b0 * P_);
+    const void* srcs[kMaxW];
+    void* dsts[kMaxW];
+    uint64_t cnt[kMaxW];
+    uint32_t k = 0;
+    for (int w = 0; w < W_; w++) {
+        if (w == rank_) continue;
+        srcs[k] = tp.out + b0 * P_;
+        dsts[k] = const_cast<float*>(tp.peer_out[w]) + b0 * P_;
+        cnt[k] = words;
+        k++;
+    }
+    sml_ok(sml_copy_segments(srcs, dsts, cnt, k, 0, st), "sml_copy_segments");
 }
 
 // Worker w's shard of every plane (blocks [w S, min((w+1) S, B))) from its

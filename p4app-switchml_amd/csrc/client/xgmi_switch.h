@@ -31,7 +31,9 @@
 //   * push form (backend.xgmi.push): K3 writes each shard of the quantized
 //     payload straight into its owner's inbox plane (W − 1 shards over xGMI,
 //     posted writes) and K6 reads the W rows of the own inbox from local HBM;
-//     same phases, barriers and bytes;
+//     the multicast likewise writes the own dequantized shard into every
+//     peer's out plane, and the gather becomes one local copy; same phases,
+//     barriers and bytes, every xGMI transfer a write;
 //   * INT32 slices: the words themselves are summed (the INT32 PPP only
 //     reorders bytes, ppp.cc:158-190, 262-298), pulled in both forms.
 // Results are bit-identical to the oracle's W-worker software switch
@@ -104,6 +106,7 @@ class XgmiSwitch {
     void Quantize(ThreadPlanes& tp, const float* in, uint64_t n, hipStream_t st);
     void IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, hipStream_t st);
     void Gather(ThreadPlanes& tp, void* out, uint64_t n, uint64_t B, uint64_t S, hipStream_t st);
+    void PushShard(ThreadPlanes& tp, uint64_t n, uint64_t B, uint64_t S, hipStream_t st);
 
     int rank_, W_, T_;
     uint32_t P_;
