@@ -503,7 +503,7 @@ def main():
         if nb > 1:
             line["roofline"]["note"] = (f"steps cycle {nb} distinct buckets + planes ({nb * (8 * N + B) >> 20} MiB "
                                         "per GPU, past the 256 MiB Infinity Cache): an HBM-proper rate")
-        if "resident" in side:
+        if "frac" in side.get("resident", {}):
             line["roofline"]["frac_resident"] = side["resident"]["frac"]
             line["roofline"]["traffic_resident"] = load_traffic(args.numel, P, "quantize_pack")
         line.update(fields)
@@ -520,28 +520,23 @@ def main():
         print(json.dumps(line), flush=True)
 
     side_cpu = {}
-    if world == 1 and not args.no_side:
-        if nb > 1:
-            side["resident"] = bucket_measure(sw, torch, args.numel, P, stream, nbuf=1)
-        else:
-            side["cold_hbm"] = bucket_measure(sw, torch, args.numel, P, stream, nbuf=4)
-        side["copy_ceiling"] = copy_ceiling(sw, torch, args.numel, stream, nbuf=nb, k1_ms=kern_ms_max)
-        side["configs3_1gpu"] = job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev)
-    if world > 1 and not args.no_side:
-        side["weak_256MiB_per_gpu"] = weak_measure(sw, torch, dist, args.numel, P, stream, dev, world)
-        if rank == 0:
-            # what the peer-to-peer paths rely on: every pair of the node's GPUs can map each other
-            side["topology"] = {
-                "devices": ndev, "name": torch.cuda.get_device_name(dev),
-                "peer_access": [[i == j or torch.cuda.can_device_access_peer(i, j) for j in range(ndev)]
-                                for i in range(ndev)]}
+
+    def guarded(key, fn):
+        """A side measurement: its failure is reported, never the headline's."""
+        try:
+            side[key] = fn()
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            side[key] = {"error": repr(e)[:300]}
+            diag_failures.append(f"side.{key}: {side[key]['error']}")
+
     watchdog = None
     if world > 1:
-        # The multi-GPU exchange phase (switch paths, plugin over the in-node
-        # switch) is where a hang could happen; past the deadline the run
-        # reports what it has, with the failure, and every rank exits 1.
+        # The multi-GPU phase (side fields, switch paths, plugin over the
+        # in-node switch) is where a hang could happen; past the deadline the
+        # run reports what it has, with the timeout, and every rank exits
+        # (1 only if the headline's own check failed).
         def on_timeout():
-            diag_failures.append(f"timeout: the switch / plugin phase exceeded {args.exchange_timeout:g} s")
+            diag_failures.append(f"timeout: the multi-GPU diagnostic phase exceeded {args.exchange_timeout:g} s")
             try:
                 emit()
             finally:
@@ -549,10 +544,25 @@ def main():
         watchdog = threading.Timer(args.exchange_timeout, on_timeout)
         watchdog.daemon = True
         watchdog.start()
+    if world == 1 and not args.no_side:
+        if nb > 1:
+            guarded("resident", lambda: bucket_measure(sw, torch, args.numel, P, stream, nbuf=1))
+        else:
+            guarded("cold_hbm", lambda: bucket_measure(sw, torch, args.numel, P, stream, nbuf=4))
+        guarded("copy_ceiling", lambda: copy_ceiling(sw, torch, args.numel, stream, nbuf=nb, k1_ms=kern_ms_max))
+        guarded("configs3_1gpu", lambda: job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev))
+    if world > 1 and not args.no_side:
+        guarded("weak_256MiB_per_gpu", lambda: weak_measure(sw, torch, dist, args.numel, P, stream, dev, world))
+        if rank == 0:
+            # what the peer-to-peer paths rely on: every pair of the node's GPUs can map each other
+            guarded("topology", lambda: {
+                "devices": ndev, "name": torch.cuda.get_device_name(dev),
+                "peer_access": [[i == j or torch.cuda.can_device_access_peer(i, j) for j in range(ndev)]
+                                for i in range(ndev)]})
     if world > 1 and args.switch_numel:
         try:
             fields.update(exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev))
-        except Exception as e:  # noqa: BLE001 - recorded, then the run fails
+        except Exception as e:  # noqa: BLE001 - recorded as a diagnostic failure below
             fields["switchsim"] = {"error": repr(e)[:400]}
         for k in ("switchsim", "p2p_switch", "xgmi_switch", "xgmi_switch_push"):
             f = fields.get(k, {})
@@ -584,7 +594,10 @@ def main():
         if not fields["rccl_collnet"].get("ok", False):
             diag_failures.append("rccl_collnet: " + fields["rccl_collnet"].get("error", "not ok"))
     if world == 1 and not args.no_cpu_baseline:
-        side_cpu["cpu_baseline"] = cpu_baseline(N, P, args.cpu_seconds)
+        try:
+            side_cpu["cpu_baseline"] = cpu_baseline(N, P, args.cpu_seconds)
+        except Exception as e:  # noqa: BLE001 - reported; the headline stands
+            diag_failures.append(f"cpu_baseline: {repr(e)[:300]}")
     emit()
     if failures:
         sys.exit(1)
