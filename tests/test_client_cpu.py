@@ -86,6 +86,10 @@ def test_config_validation(ctx):
     C.stop()
     C.start(C.make_config(prepostprocessor="bypass", coalesce_us=0, bandwidth=0))
     assert "coalesce_us = 0" in C.config_text()
+    assert "burst_server = false" in C.config_text() and "push = false" in C.config_text()   # defaults
+    C.stop()
+    C.start(C.make_config(prepostprocessor="bypass", burst_server=True, push=True, bandwidth=0))
+    assert "burst_server = true" in C.config_text() and "push = true" in C.config_text()
     C.stop()
     for bad in (dict(prepostprocessor="nope"), dict(backend="dpdk"), dict(mode="turbo"),
                 dict(num_worker_threads=8, max_outstanding_packets=4)):
