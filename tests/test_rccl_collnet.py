@@ -56,3 +56,27 @@ def test_worker_env_drops_launcher_state():
     assert env["NCCL_NET_PLUGIN"].endswith("librccl-net-switchml.so") and env["NCCL_COLLNET_ENABLE"] == "1"
     assert env["NCCL_HOSTID"] == "switchml-worker-s1-1"
     assert "rank = 1" in env["SWITCHML_CONFIG_INI"] and "device = 1" in env["SWITCHML_CONFIG_INI"]
+
+
+def test_installed_rccl_has_no_collnet_allreduce_device_code():
+    """Why the CollNet table declines RCCL: the RCCL builds
+    on this image hold AllReduce device functions for RING and TREE only —
+    no ncclDevFunc_AllReduce_COLLNET_* exists, so no CollNet plugin can be
+    handed an all-reduce by them (tools/rccl_devfuncs.py)."""
+    import importlib.util
+    import json
+    import subprocess
+    libs = ["/opt/rocm/lib/librccl.so"]
+    spec = importlib.util.find_spec("torch")
+    if spec is not None:
+        libs.append(os.path.join(os.path.dirname(spec.origin), "lib", "librccl.so"))
+    libs = [l for l in libs if os.path.exists(l)]
+    if not libs:
+        pytest.skip("no librccl.so on this machine")
+    tool = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "rccl_devfuncs.py")
+    for lib in libs:
+        out = subprocess.run([sys.executable, tool, lib], capture_output=True, text=True, check=True).stdout
+        rep = json.loads(out)
+        assert rep["device_functions"] > 100, lib
+        assert "RING" in rep["allreduce_algorithms_with_device_code"], lib
+        assert rep["collnet_allreduce_device_functions"] == [], lib
