@@ -28,11 +28,14 @@ each checked (bit-equal to each other, and within the quantization bound of
 an fp32 all-reduce of the same buckets) and set against its xGMI bound; and
 configs4_plugin: the ResNet-50 buckets through the CollNet plugin table on an
 N-rank communicator over the xgmi backend (device and pinned host buffers).
-The exit status is 1 only when the headline's own check fails (the timed
-planes differ from the committed digests) or the headline cannot be
-measured; a failed or timed-out diagnostic field (switch paths, plugin,
-rccl_collnet) is reported in the line under "diagnostic_failures" and in its
-own field, so one experimental path cannot void the measured headline.
+The exit status is 1 when the headline's own check fails (the timed planes
+differ from the committed digests), when the headline cannot be measured, or
+when a switch path RAN and gave wrong bits (not within the quantization
+bound, not bit-equal to the other paths, or timed calls that differ from the
+first): a correctness regression is fatal.  A diagnostic field that could
+not run or timed out (switch paths, plugin, rccl_collnet) is reported in the
+line under "diagnostic_failures" and in its own field, so one path that
+cannot start cannot void the measured headline.
 
 Units: value / roofline.achieved = ALGORITHMIC bytes per second: 4N read
 (fp32 in) + 4N written (int32 payload) + B written (int8 exponents),
@@ -314,15 +317,23 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # SML_BENCH_REHEARSE=1: rehearse the N>1 path on a 1-GPU box (all ranks on
-    # device local % device_count, gloo instead of RCCL).  Never used for numbers.
-    rehearse = os.environ.get("SML_BENCH_REHEARSE") == "1"
+    # SML_BENCH_REHEARSE=1: rehearse the N>1 path on a 1-GPU box — all ranks
+    # on device local % device_count, still over RCCL: every rank is an RCCL
+    # host of its own (NCCL_HOSTID), the ranks linked by the SwitchML
+    # library's TCP net (switchml_amd.rccl_collnet.same_gpu_rccl_env), so the
+    # reductions run in the same RCCL kernels as on a node.  SML_BENCH_REHEARSE
+    # =gloo keeps the old host-reduction rehearsal.  Never used for numbers.
+    rehearse_mode = os.environ.get("SML_BENCH_REHEARSE", "")
+    rehearse = rehearse_mode in ("1", "gloo")
     ndev = torch.cuda.device_count()
     local_dev = local % ndev if rehearse else local
     if world > 1:
-        if rehearse:
+        if rehearse_mode == "gloo":
             dist.init_process_group("gloo")
         else:
+            if rehearse:
+                from switchml_amd.rccl_collnet import same_gpu_rccl_env
+                os.environ.update(same_gpu_rccl_env(rank, "bench" + os.environ.get("MASTER_PORT", "0")))
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
@@ -566,8 +577,15 @@ def main():
             fields["switchsim"] = {"error": repr(e)[:400]}
         for k in ("switchsim", "p2p_switch", "xgmi_switch", "xgmi_switch_push"):
             f = fields.get(k, {})
-            if "error" in f or not f.get("verified", False):
-                diag_failures.append(f"{k}: {f.get('error', 'not verified')}")
+            if "error" in f or "verified" not in f:
+                # could not run (an error, a missing path): diagnostic
+                diag_failures.append(f"{k}: {f.get('error', 'not run')}")
+            elif not f["verified"]:
+                # ran and gave wrong bits (or calls that disagree): a
+                # correctness regression of a switch path fails the run
+                failures.append(f"{k}: not verified (within bound {f.get('within_quantization_bound')}, "
+                                f"bit-equal {f.get('bit_equal_to_switchsim', f.get('bit_equal_to_other_paths'))}, "
+                                f"timed calls equal {f.get('timed_calls_equal_first')})")
     if world > 1 and not args.no_plugin:
         # configs[4] on every GPU at once: each rank hands the ResNet-50 buckets
         # to its own plugin instance, on an N-rank communicator whose backend
@@ -696,7 +714,8 @@ def bucket_measure(sw, torch, N, P, stream, nbuf=4, reps=200):
 
 def copy_ceiling(sw, torch, N, stream, nbuf=4, reps=200, k1_ms=None):
     """The practical HBM ceiling for K1's access pattern: sml_stream_copy (the
-    same 1024-element tiles, XCD order and 16-B non-temporal accesses, no
+    same 1024-element tiles, XCD order, non-temporal 16-B loads and K1's store
+    policy for a plane of this size — non-temporal at >= 64 MiB — no
     arithmetic) moving the same 4N read + 4N written bytes, its steps cycling
     the same number of distinct buckets as the headline."""
     g = torch.Generator(device=stream.device)

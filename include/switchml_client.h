@@ -62,6 +62,17 @@ void sml_job_release(sml_job_t job);
  * [3] job slices processed, [4] packets (LTUs) processed incl. extra batch. */
 int sml_context_stats(uint64_t out[5]);
 
+/* Whether the PrePostProcessor a factory key names (config key
+ * general.prepostprocessor; PrePostProcessor::CreateInstance,
+ * client_lib/src/prepostprocessor.cc:32-41) accepts per-LTU calls
+ * (PreprocessSingle / PostprocessSingle once per packet): 1 yes
+ * ("hip_exponent_quantizer", "bypass"), 0 no — "cpu_exponent_quantizer", the
+ * reference's name, maps to the MI355X quantizer driven by its bulk / burst
+ * hooks, and its per-LTU calls throw rather than run one launch and host sync
+ * per 1 KiB packet — or SML_CTX_ERR_CONFIG for a name the factory rejects.
+ * A packet-driven backend (a DPDK / RDMA worker) checks this at setup. */
+int sml_ppp_per_ltu_calls(const char* name);
+
 #ifdef __cplusplus
 }
 #endif

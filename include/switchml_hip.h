@@ -288,6 +288,16 @@ sml_status_t sml_burst_server_submit(sml_burst_server* server, uint32_t op, cons
  * the server's memory and stream are kept for that. */
 sml_status_t sml_burst_server_stop(sml_burst_server* server);
 sml_status_t sml_burst_server_destroy(sml_burst_server* server);
+/* Start the server now (it idles on the doorbell) instead of on the first
+ * submit: takes the launch off the first burst's latency.  A relaunch marks
+ * every doorbell rung before it as handled, so a burst that failed (a
+ * timeout, a workgroup's idle exit mid-burst) is never replayed. */
+sml_status_t sml_burst_server_start(sml_burst_server* server);
+/* Fault injection for tests: stop the server, then write `burst` and ring the
+ * doorbell for it with no server to answer — the state a failed submit
+ * leaves (done < doorbell).  Never used on the data path. */
+sml_status_t sml_burst_server_inject_unanswered(sml_burst_server* server, uint32_t op,
+                                                const sml_packet_burst* burst);
 
 /* Plane sharing for the peer-to-peer switch: export the allocation holding
  * d_ptr as an IPC handle of sml_ipc_handle_bytes() bytes plus d_ptr's byte
@@ -383,8 +393,10 @@ sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t num_blocks, uint32_t ba
 
 /* Measurement probe (not part of the PPP): copy `bytes` (a multiple of 4 KiB,
  * 16-B aligned buffers) with the quantize kernel's tile shape and access
- * policy (non-temporal loads, default-policy stores) — the practical HBM
- * ceiling bench.py reports. */
+ * policy (non-temporal loads; non-temporal stores from the payload
+ * non-temporal threshold on, default-policy stores below it — the store
+ * policy sml_quantize_pack uses for an output plane of `bytes`) — the
+ * practical HBM ceiling bench.py reports. */
 sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void* stream);
 
 /* Launch-geometry knob for experiments: workgroups per launch for the

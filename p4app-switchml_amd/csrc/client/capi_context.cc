@@ -3,6 +3,7 @@
 #include <string>
 
 #include "context.h"
+#include "prepostprocessor.h"
 #include "switchml_client.h"
 
 using namespace switchml;
@@ -110,6 +111,12 @@ int sml_context_stats(uint64_t out[5]) {
     out[3] = s.slices_processed();
     out[4] = s.ltus_processed();
     return SML_CTX_OK;
+}
+
+int sml_ppp_per_ltu_calls(const char* name) {
+    if (!name) return SML_CTX_ERR_ARG;
+    const int r = PrePostProcessor::PerLtuCalls(name);
+    return r < 0 ? fail(SML_CTX_ERR_CONFIG, std::string("'") + name + "' is not a valid prepostprocessor.") : r;
 }
 
 }  // extern "C"

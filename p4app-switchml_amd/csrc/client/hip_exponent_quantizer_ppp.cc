@@ -15,8 +15,8 @@ static void hip_ok(hipError_t e, const char* what) {
 }
 
 HipExponentQuantizerPPP::HipExponentQuantizerPPP(Config& config, WorkerTid worker_tid, Numel ltu_size,
-                                                 Numel batch_num_ltus)
-    : PrePostProcessor(config, worker_tid, ltu_size, batch_num_ltus) {
+                                                 Numel batch_num_ltus, bool per_ltu_calls)
+    : PrePostProcessor(config, worker_tid, ltu_size, batch_num_ltus), per_ltu_calls_(per_ltu_calls) {
     ltu_numel_ = ltu_size / 4;
     if (ltu_size % 4 || !(ltu_numel_ == 64 || ltu_numel_ == 128 || ltu_numel_ == 256 || ltu_numel_ == 512 ||
                           ltu_numel_ == 1024))
@@ -34,6 +34,22 @@ HipExponentQuantizerPPP::~HipExponentQuantizerPPP() {
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
+// The per-LTU trap: a reference worker that keeps
+// `prepostprocessor = cpu_exponent_quantizer` and calls PreprocessSingle once
+// per 1 KiB packet (DpdkWorkerThread via BuildPacket,
+// dpdk_worker_thread_utils.inc:134; RdmaWorkerThread::PostSendWr) would run a
+// launch, pointer queries and a host sync per packet — ~14-24 us against the
+// CPU loop's ~0.1 us — with no warning.  Under that name the per-LTU calls
+// therefore refuse, naming the way out.
+void HipExponentQuantizerPPP::refuse_per_ltu(const char* call) const {
+    throw SwitchMLFatal(std::string(call) +
+                        ": prepostprocessor 'cpu_exponent_quantizer' runs on the MI355X and is driven by its bulk "
+                        "hooks (PreprocessBulk / PostprocessBulk) or burst hooks (PreprocessBurst / PostprocessBurst "
+                        "/ PostprocessReuseBurst: one launch per rx/tx burst); one call per packet would cost a "
+                        "kernel launch and a host sync per 1 KiB packet. Call the burst hooks, or set "
+                        "prepostprocessor = hip_exponent_quantizer to accept per-packet launches.");
+}
+
 void HipExponentQuantizerPPP::check(int status, const char* what) const {
     if (status != SML_OK)
         throw SwitchMLFatal(std::string(what) + " failed: " + sml_status_string((sml_status_t)status) + " " +
@@ -44,6 +60,7 @@ uint64_t HipExponentQuantizerPPP::SetupJobSlice(JobSlice* job_slice) {
     // ppp.cc:54-62
     job_slice_ = job_slice;
     pool_probe_ = nullptr;
+    xpool_probe_ = nullptr;
     const uint64_t bytes = job_slice->slice.numel * DataTypeSize(job_slice->slice.data_type);
     total_main_num_ltus_ = (bytes + ltu_size_ - 1) / ltu_size_;
     batch_num_ltus_ = std::min<uint64_t>(total_main_num_ltus_, batch_max_num_ltus_);
@@ -103,6 +120,16 @@ PacketMem packet_mem(void* p) {
 // that opted into stream order (SetStreamOrdered) with a device-memory packet
 // skips the host sync.
 void HipExponentQuantizerPPP::PreprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
+    if (!per_ltu_calls_) refuse_per_ltu("PreprocessSingle");
+    preprocess_single(ltu_id, entries_ptr, extra_info);
+}
+
+void HipExponentQuantizerPPP::PostprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
+    if (!per_ltu_calls_) refuse_per_ltu("PostprocessSingle");
+    postprocess_single(ltu_id, entries_ptr, extra_info);
+}
+
+void HipExponentQuantizerPPP::preprocess_single(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
     const Tensor& s = job_slice_->slice;
     const uint32_t P = (uint32_t)ltu_numel_;
     ensure_single_buffers();
@@ -151,7 +178,7 @@ void HipExponentQuantizerPPP::PreprocessSingle(uint64_t ltu_id, void* entries_pt
 // buffer in place when the device can address it (packet buffers hold P
 // words, ltu_size bytes); the caller may reuse a host-memory packet buffer
 // as soon as this returns, so those calls synchronise.
-void HipExponentQuantizerPPP::PostprocessSingle(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
+void HipExponentQuantizerPPP::postprocess_single(uint64_t ltu_id, void* entries_ptr, void* extra_info) {
     const Tensor& s = job_slice_->slice;
     const uint32_t P = (uint32_t)ltu_numel_;
     ensure_single_buffers();
@@ -216,19 +243,44 @@ void HipExponentQuantizerPPP::burst(BurstKind kind, uint32_t n, const uint64_t* 
         pool_host_ = pm.host;
     }
     const PacketMem m{pool_dev_, pool_host_};
-    if (!m.dev) {
+    // the extra-info slots may be another allocation (a separate ring, a
+    // second registration): queried on their own
+    PacketMem xm{};
+    if (extras && extras[0]) {
+        if (extras[0] != xpool_probe_) {
+            xpool_probe_ = extras[0];
+            const PacketMem pm = packet_mem(extras[0]);
+            xpool_dev_ = pm.dev;
+            xpool_host_ = pm.host;
+        }
+        xm = {xpool_dev_, xpool_host_};
+    }
+    if (!m.dev || (extras && extras[0] && !xm.dev)) {
         if (kind == BurstKind::kProcessExchange)
             throw SwitchMLFatal("ProcessPostprocessReuseBurst: packet buffers must be device-addressable");
         for (uint32_t i = 0; i < n; i++) {
             void* x = extras ? extras[i] : nullptr;
-            if (kind != BurstKind::kPre) PostprocessSingle(ltu_ids[i], entries[i], x);
-            if (kind == BurstKind::kPre) PreprocessSingle(ltu_ids[i], entries[i], x);
+            if (kind != BurstKind::kPre) postprocess_single(ltu_ids[i], entries[i], x);
+            if (kind == BurstKind::kPre) preprocess_single(ltu_ids[i], entries[i], x);
             else if (kind == BurstKind::kExchange && ltu_ids[i] + batch_num_ltus_ < total)
-                PreprocessSingle(ltu_ids[i] + batch_num_ltus_, entries[i], x);
+                preprocess_single(ltu_ids[i] + batch_num_ltus_, entries[i], x);
         }
         return;
     }
+    // Host address -> device address: the probe's offset applies to the
+    // buffers of its own registration only.  When host and device addresses
+    // coincide (HBM, hipHostMalloc) every buffer maps to itself; otherwise (a
+    // hipHostRegister'd NIC pool) each buffer is translated by its own query,
+    // so buffers of other registrations are never shifted by a wrong offset.
     const intptr_t delta = static_cast<char*>(m.dev) - static_cast<char*>(entries[0]);
+    const intptr_t xdelta = xm.dev ? static_cast<char*>(xm.dev) - static_cast<char*>(extras[0]) : 0;
+    const bool per_buffer = delta != 0 || xdelta != 0;
+    auto dev_addr = [&](void* p) -> void* {
+        if (!p || !per_buffer) return p;
+        void* a = packet_mem(p).dev;
+        if (!a) throw SwitchMLFatal("burst: a packet buffer of the burst is not device-addressable");
+        return a;
+    };
     const bool exchange = kind == BurstKind::kExchange || kind == BurstKind::kProcessExchange;
     sml_packet_burst b{};
     b.in = static_cast<const float*>(s.in_ptr);
@@ -257,8 +309,8 @@ void HipExponentQuantizerPPP::burst(BurstKind kind, uint32_t n, const uint64_t* 
         b.count = std::min<uint32_t>(SML_MAX_BURST, n - i0);
         for (uint32_t i = 0; i < b.count; i++) {
             b.pkt_ids[i] = ltu_ids[i0 + i];
-            b.entries[i] = static_cast<char*>(entries[i0 + i]) + delta;
-            b.extras[i] = extras && extras[i0 + i] ? static_cast<char*>(extras[i0 + i]) + delta : nullptr;
+            b.entries[i] = dev_addr(entries[i0 + i]);
+            b.extras[i] = extras ? dev_addr(extras[i0 + i]) : nullptr;
         }
         if (serve) {   // returns with the burst complete
             check(sml_burst_server_submit(server_, op, &b), "sml_burst_server_submit");
@@ -342,13 +394,19 @@ void HipExponentQuantizerPPP::PostprocessBulk(const void* payload_plane, const v
     }
 }
 
+int PrePostProcessor::PerLtuCalls(const std::string& name) {
+    if (name == "hip_exponent_quantizer" || name == "bypass") return 1;
+    if (name == "cpu_exponent_quantizer") return 0;   // bulk / burst hooks only (refuse_per_ltu)
+    return -1;
+}
+
 std::shared_ptr<PrePostProcessor> PrePostProcessor::CreateInstance(Config& config, WorkerTid worker_tid,
                                                                    Numel ltu_size, Numel batch_num_ltus) {
     const std::string& name = config.general_.prepostprocessor;
-    if (name == "hip_exponent_quantizer" || name == "cpu_exponent_quantizer")
-        return std::make_shared<HipExponentQuantizerPPP>(config, worker_tid, ltu_size, batch_num_ltus);
+    const int per_ltu = PerLtuCalls(name);
+    if (per_ltu < 0) throw SwitchMLFatal("'" + name + "' is not a valid prepostprocessor.");
     if (name == "bypass") return std::make_shared<BypassPPP>(config, worker_tid, ltu_size, batch_num_ltus);
-    throw SwitchMLFatal("'" + name + "' is not a valid prepostprocessor.");
+    return std::make_shared<HipExponentQuantizerPPP>(config, worker_tid, ltu_size, batch_num_ltus, per_ltu == 1);
 }
 
 }  // namespace switchml

@@ -24,7 +24,11 @@ namespace switchml {
 
 class HipExponentQuantizerPPP : public PrePostProcessor {
   public:
-    HipExponentQuantizerPPP(Config& config, WorkerTid worker_tid, Numel ltu_size, Numel batch_num_ltus);
+    // per_ltu_calls = false: PreprocessSingle / PostprocessSingle called from
+    // outside (a reference worker's per-packet loop) throw instead of running
+    // one launch + host sync per packet; bulk and burst hooks are unaffected.
+    HipExponentQuantizerPPP(Config& config, WorkerTid worker_tid, Numel ltu_size, Numel batch_num_ltus,
+                            bool per_ltu_calls = true);
     ~HipExponentQuantizerPPP() override;
 
     uint64_t SetupJobSlice(JobSlice* job_slice) override;
@@ -65,6 +69,9 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
 
   private:
     void check(int status, const char* what) const;
+    void refuse_per_ltu(const char* call) const;
+    void preprocess_single(uint64_t ltu_id, void* entries_ptr, void* extra_info);
+    void postprocess_single(uint64_t ltu_id, void* entries_ptr, void* extra_info);
     void ensure_single_buffers();
     enum class BurstKind { kPre, kPost, kExchange, kProcessExchange };
     void burst(BurstKind kind, uint32_t n, const uint64_t* ltu_ids, void* const* entries, void* const* extras);
@@ -81,11 +88,16 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     int32_t* d_stage_ = nullptr;
     int8_t* d_stage_exp_ = nullptr;
     bool stream_ordered_ = false;
+    bool per_ltu_calls_ = true;
     // where the slice's packet pool lives (burst calls): the first buffer
-    // pointer seen, and its packet_mem() answer
+    // pointer seen, and its packet_mem() answer — for the entries and, as a
+    // separate query, the extra-info slots (they may be another allocation)
     void* pool_probe_ = nullptr;
     void* pool_dev_ = nullptr;
     bool pool_host_ = true;
+    void* xpool_probe_ = nullptr;
+    void* xpool_dev_ = nullptr;
+    bool xpool_host_ = true;
     // persistent burst server for host-memory packets (backend.hip.burst_server)
     sml_burst_server* server_ = nullptr;
     bool server_synced_ = false;   // stream_ drained before the slice's first server burst

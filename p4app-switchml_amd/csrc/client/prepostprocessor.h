@@ -10,6 +10,7 @@
 #define SWITCHML_AMD_PREPOSTPROCESSOR_H_
 
 #include <memory>
+#include <string>
 
 #include "common.h"
 #include "config.h"
@@ -22,11 +23,18 @@ class PrePostProcessor {
     // Factory keyed by config.general_.prepostprocessor (prepostprocessor.cc:32-41):
     //   "hip_exponent_quantizer"  -> HipExponentQuantizerPPP (MI355X kernels)
     //   "cpu_exponent_quantizer"  -> HipExponentQuantizerPPP as well: the drop-in
-    //                                name of the reference's quantizer, same bytes
+    //                                name of the reference's quantizer, same bytes,
+    //                                driven by bulk / burst hooks only — its
+    //                                PreprocessSingle / PostprocessSingle throw
+    //                                (a per-packet caller would pay a launch and
+    //                                a host sync per packet)
     //   "bypass"                  -> BypassPPP
     // Anything else throws SwitchMLFatal (the reference: LOG(FATAL)).
     static std::shared_ptr<PrePostProcessor> CreateInstance(Config& config, WorkerTid worker_tid,
                                                             Numel ltu_size, Numel batch_num_ltus);
+    // Whether the PPP a factory key names takes per-LTU calls: 1 yes, 0 no
+    // (bulk / burst hooks only), -1 not a valid prepostprocessor.
+    static int PerLtuCalls(const std::string& name);
     virtual ~PrePostProcessor() = default;
     PrePostProcessor(const PrePostProcessor&) = delete;
     PrePostProcessor& operator=(const PrePostProcessor&) = delete;

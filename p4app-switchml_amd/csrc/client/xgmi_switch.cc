@@ -5,6 +5,7 @@
 #include <fcntl.h>
 #include <signal.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -64,6 +65,19 @@ static_assert(std::atomic<uint32_t>::is_always_lock_free, "shared-memory atomics
 
 namespace {
 bool pid_alive(int32_t pid) { return pid > 0 && (kill(pid, 0) == 0 || errno == EPERM); }
+
+// mmap of a segment another process creates: worker 0 sizes it (ftruncate)
+// only after its O_EXCL create, so a file opened in between is still 0 bytes
+// and touching its mapping would raise SIGBUS.  A segment shorter than
+// XgmiShm is "not ready" (or stale): closed, nullptr returned.  Closes fd.
+XgmiShm* map_sized(int fd, int prot) {
+    struct stat st;
+    void* m = MAP_FAILED;
+    if (fstat(fd, &st) == 0 && (uint64_t)st.st_size >= sizeof(XgmiShm))
+        m = mmap(nullptr, sizeof(XgmiShm), prot, MAP_SHARED, fd, 0);
+    close(fd);
+    return m == MAP_FAILED ? nullptr : static_cast<XgmiShm*>(m);
+}
 }  // namespace
 
 // Worker 0 creates the segment (O_EXCL), replacing one left behind by a run
@@ -95,10 +109,10 @@ void XgmiSwitch::OpenSegment() {
             if (errno != EEXIST || attempt > 3) fail("shm_open " + name_ + ": " + strerror(errno));
             const int fe = shm_open(name_.c_str(), O_RDONLY, 0600);
             if (fe >= 0) {
-                void* o = mmap(nullptr, sizeof(XgmiShm), PROT_READ, MAP_SHARED, fe, 0);
-                close(fe);
-                if (o != MAP_FAILED) {
-                    const int32_t pid = static_cast<XgmiShm*>(o)->creator_pid.load();
+                // a segment too short to hold the header is stale (its creator
+                // died between create and size): replaced below
+                if (XgmiShm* o = map_sized(fe, PROT_READ)) {
+                    const int32_t pid = o->creator_pid.load();
                     munmap(o, sizeof(XgmiShm));
                     if (pid_alive(pid) && pid != getpid())
                         fail("session " + name_ + " is in use by process " + std::to_string(pid) +
@@ -112,10 +126,9 @@ void XgmiSwitch::OpenSegment() {
     for (;;) {
         const int fd = shm_open(name_.c_str(), O_RDWR, 0600);
         if (fd >= 0) {
-            void* m = mmap(nullptr, sizeof(XgmiShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-            close(fd);
-            if (m != MAP_FAILED) {
-                auto* s = static_cast<XgmiShm*>(m);
+            // not yet sized by worker 0: not ready, retry (map_sized)
+            if (XgmiShm* s = map_sized(fd, PROT_READ | PROT_WRITE)) {
+                void* m = s;
                 while (s->magic.load(std::memory_order_acquire) != kMagic &&
                        std::chrono::steady_clock::now() < deadline)
                     std::this_thread::sleep_for(std::chrono::microseconds(200));

@@ -540,6 +540,13 @@ sml_status_t server_launch(sml_burst_server* s) {
     if (st != SML_OK) return st;
     for (int g = 0; g < sml::kServerGroups; g++) __atomic_store_n(&s->ctl->exited[g], 0u, __ATOMIC_RELEASE);
     __atomic_store_n(&s->ctl->stop, 0u, __ATOMIC_RELEASE);
+    // The new kernel starts from seen = done.  After a failed burst (timeout,
+    // a workgroup's idle exit mid-burst) done lags the last doorbell; the
+    // relaunched server would take that stale doorbell for a new burst and
+    // replay its descriptor (an exchange burst applied twice, or buffers of a
+    // finished slice).  No kernel runs here (joined above): mark every rung
+    // doorbell as handled.
+    __atomic_store_n(&s->ctl->done, s->seq, __ATOMIC_RELEASE);
     st = sml::hip_check(hipMemsetAsync(s->arrive, 0, sizeof(uint32_t), s->stream));
     if (st != SML_OK) return st;
     const dim3 grid(sml::kServerGroups), block(sml::kServerThreads);
@@ -639,6 +646,21 @@ sml_status_t sml_burst_server_submit(sml_burst_server* s, uint32_t op, const sml
 sml_status_t sml_burst_server_stop(sml_burst_server* s) {
     if (!s) return SML_ERR_INVALID_ARG;
     return server_join(s);
+}
+
+sml_status_t sml_burst_server_start(sml_burst_server* s) {
+    if (!s) return SML_ERR_INVALID_ARG;
+    if (s->launched && !any_exited(s)) return SML_OK;
+    return server_launch(s);
+}
+
+sml_status_t sml_burst_server_inject_unanswered(sml_burst_server* s, uint32_t op, const sml_packet_burst* burst) {
+    if (!s || !burst || op > SML_BURST_EXCHANGE) return SML_ERR_INVALID_ARG;
+    const sml_status_t st = server_join(s);
+    if (st != SML_OK) return st;
+    memcpy(&s->ctl->burst, burst, sizeof(sml_packet_burst));
+    __atomic_store_n(&s->ctl->doorbell, (++s->seq << 2) | op, __ATOMIC_RELEASE);
+    return SML_OK;
 }
 
 sml_status_t sml_burst_server_destroy(sml_burst_server* s) {

@@ -332,9 +332,12 @@ struct BswapOp {
 };
 
 // Measurement probe (not on the hot path): the same 1024-element tiles and
-// the same access policy as the quantize kernel (non-temporal 16-B loads,
-// default-policy 16-B stores), no arithmetic — the practical HBM ceiling the
-// quantize kernel is compared against.
+// the same access policy as the quantize kernel — non-temporal 16-B loads,
+// and 16-B stores under K1's store policy for a plane of that size
+// (non-temporal from g_nt_threshold bytes on, default policy below) — no
+// arithmetic: the practical HBM ceiling the quantize kernel is compared
+// against.
+template <bool NTS>
 __global__ __launch_bounds__(kBlockThreads) void k_stream_copy(const u4* in, u4* out, uint64_t ntiles, uint32_t xcd) {
     struct { uint32_t xcd; } a{xcd};
     const int lane = threadIdx.x & (kWave - 1);
@@ -344,7 +347,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_stream_copy(const u4* in, u4*
 #pragma unroll
         for (int u = 0; u < kU; u++) v[u] = __builtin_nontemporal_load(in + t * (kTileElems / 4) + u * kWave + lane);
 #pragma unroll
-        for (int u = 0; u < kU; u++) out[t * (kTileElems / 4) + u * kWave + lane] = v[u];
+        for (int u = 0; u < kU; u++) store_payload_as<NTS>(out + t * (kTileElems / 4) + u * kWave + lane, v[u]);
     }
 }
 
@@ -706,9 +709,14 @@ sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void
     if (bytes == 0) return SML_OK;
     if (!d_in || !d_out || !aligned16(d_in) || !aligned16(d_out) || bytes % (kTileElems * 4)) return SML_ERR_ALIGNMENT;
     const uint64_t ntiles = bytes / (kTileElems * 4);
-    k_stream_copy<<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(
-        reinterpret_cast<const u4*>(d_in), reinterpret_cast<u4*>(d_out), ntiles,
-        g_xcd_chunk.load(std::memory_order_relaxed));
+    const uint32_t xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    auto in = reinterpret_cast<const u4*>(d_in);
+    auto out = reinterpret_cast<u4*>(d_out);
+    // K1's store policy for an output plane of `bytes` (sml_quantize_pack)
+    if (bytes >= g_nt_threshold.load(std::memory_order_relaxed))
+        k_stream_copy<true><<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(in, out, ntiles, xcd);
+    else
+        k_stream_copy<false><<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(in, out, ntiles, xcd);
     return launch_check();
 }
 

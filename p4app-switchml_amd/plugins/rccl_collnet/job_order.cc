@@ -5,6 +5,7 @@
 #include <fcntl.h>
 #include <signal.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -23,6 +24,12 @@ constexpr int kMaxWorkers = 16;
 bool pid_alive(int32_t pid) { return pid > 0 && (kill(pid, 0) == 0 || errno == EPERM); }
 }  // namespace
 
+// mmap of a segment worker 0 creates: it is sized (ftruncate) only after the
+// O_EXCL create, so a file opened in between is 0 bytes and touching the
+// mapping would raise SIGBUS.  Shorter than OrderShm: not ready (or stale) —
+// nullptr.  Closes fd.
+OrderShm* map_sized(int fd, int prot);
+
 struct alignas(64) Counter {
     std::atomic<uint64_t> v;
     char pad[56];
@@ -35,12 +42,22 @@ struct OrderShm {
     std::atomic<uint32_t> poisoned;
     std::atomic<uint32_t> attached;
     std::atomic<uint32_t> detached;
+    uint64_t generation;           // set by the creator: which segment of this name it is
     Counter head;                  // entries worker 0 appended
     Counter done[kMaxWorkers];     // entries each worker > 0 consumed
     CallKey log[kLog];
 };
 
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
+
+OrderShm* map_sized(int fd, int prot) {
+    struct stat st;
+    void* m = MAP_FAILED;
+    if (fstat(fd, &st) == 0 && (uint64_t)st.st_size >= sizeof(OrderShm))
+        m = mmap(nullptr, sizeof(OrderShm), prot, MAP_SHARED, fd, 0);
+    close(fd);
+    return m == MAP_FAILED ? nullptr : static_cast<OrderShm*>(m);
+}
 
 JobOrder::JobOrder(const std::string& session, int rank, int nworkers, uint64_t timeout_ms)
     : name_("/switchml-collnet-" + session), rank_(rank), nworkers_(nworkers) {
@@ -70,14 +87,15 @@ JobOrder::JobOrder(const std::string& session, int rank, int nworkers, uint64_t 
                 throw std::runtime_error("job order: shm_open " + name_ + ": " + strerror(errno));
             // a segment of that name exists: live (another job uses the session
             // name) or left by a crashed run (its creator is gone): replace it
+            // (a segment too short for the header is stale: its creator died
+            // between create and size; one created by this process is an
+            // earlier communicator's that was never closed)
             const int fe = shm_open(name_.c_str(), O_RDWR, 0600);
             if (fe >= 0) {
-                void* o = mmap(nullptr, sizeof(OrderShm), PROT_READ, MAP_SHARED, fe, 0);
-                close(fe);
-                if (o != MAP_FAILED) {
-                    const int32_t pid = static_cast<OrderShm*>(o)->creator_pid.load();
+                if (OrderShm* o = map_sized(fe, PROT_READ)) {
+                    const int32_t pid = o->creator_pid.load();
                     munmap(o, sizeof(OrderShm));
-                    if (pid_alive(pid))
+                    if (pid_alive(pid) && pid != getpid())
                         throw std::runtime_error("job order: session " + name_ + " is in use by process " +
                                                  std::to_string(pid));
                 }
@@ -85,6 +103,8 @@ JobOrder::JobOrder(const std::string& session, int rank, int nworkers, uint64_t 
             shm_unlink(name_.c_str());
         }
         shm_ = static_cast<OrderShm*>(m);
+        shm_->generation = gen_ = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() ^
+                                  ((uint64_t)getpid() << 40);
         shm_->nworkers = (uint32_t)nworkers;
         shm_->creator_pid.store(getpid());
         shm_->attached.store(1);
@@ -95,10 +115,8 @@ JobOrder::JobOrder(const std::string& session, int rank, int nworkers, uint64_t 
     for (;;) {
         const int fd = shm_open(name_.c_str(), O_RDWR, 0600);
         if (fd >= 0) {
-            m = mmap(nullptr, sizeof(OrderShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-            close(fd);
-            if (m != MAP_FAILED) {
-                auto* s = static_cast<OrderShm*>(m);
+            if (OrderShm* s = map_sized(fd, PROT_READ | PROT_WRITE)) {
+                m = s;
                 while (s->magic.load(std::memory_order_acquire) != kMagic && !expired())
                     std::this_thread::sleep_for(std::chrono::microseconds(200));
                 if (s->magic.load(std::memory_order_acquire) == kMagic && pid_alive(s->creator_pid.load())) {
@@ -106,11 +124,21 @@ JobOrder::JobOrder(const std::string& session, int rank, int nworkers, uint64_t 
                         munmap(m, sizeof(OrderShm));
                         throw std::runtime_error("job order: workers disagree on the worker count");
                     }
-                    shm_ = s;
-                    shm_->attached.fetch_add(1);
-                    return;
+                    // One segment serves one communicator: nworkers
+                    // attachments (worker 0's included).  A full one is an
+                    // earlier communicator's, still open on worker 0 (this
+                    // worker closed and reconnected first): its log is not
+                    // ours — wait for worker 0's new segment.
+                    uint32_t a = s->attached.load();
+                    while (a < (uint32_t)nworkers && !s->attached.compare_exchange_weak(a, a + 1)) {
+                    }
+                    if (a < (uint32_t)nworkers) {
+                        shm_ = s;
+                        gen_ = s->generation;
+                        return;
+                    }
                 }
-                munmap(m, sizeof(OrderShm));   // stale (creator gone): worker 0 replaces it
+                munmap(m, sizeof(OrderShm));   // stale (creator gone) or full: wait for worker 0's
             }
         }
         if (expired()) throw std::runtime_error("job order: worker 0 did not create " + name_ + " in time");
@@ -118,11 +146,21 @@ JobOrder::JobOrder(const std::string& session, int rank, int nworkers, uint64_t 
     }
 }
 
+// The last worker to close removes the name — if the name still is ITS
+// segment: worker 0 may already have replaced it with a reconnected
+// communicator's (a new generation), which stays.
 JobOrder::~JobOrder() {
     if (!shm_) return;
     const bool last = shm_->detached.fetch_add(1) + 1 == (uint32_t)nworkers_;
     munmap(shm_, sizeof(OrderShm));
-    if (last) shm_unlink(name_.c_str());
+    if (!last) return;
+    const int fd = shm_open(name_.c_str(), O_RDONLY, 0600);
+    if (fd < 0) return;
+    if (OrderShm* s = map_sized(fd, PROT_READ)) {
+        const bool mine = s->generation == gen_;
+        munmap(s, sizeof(OrderShm));
+        if (mine) shm_unlink(name_.c_str());
+    }
 }
 
 bool JobOrder::Append(const CallKey& k) {

@@ -63,6 +63,7 @@ class JobOrder {
     int rank_, nworkers_;
     OrderShm* shm_ = nullptr;
     uint64_t pos_ = 0;   // worker > 0: next log entry to submit
+    uint64_t gen_ = 0;   // the segment's generation (its creator's nonce)
 };
 
 }  // namespace sml_collnet

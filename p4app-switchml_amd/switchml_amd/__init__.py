@@ -159,6 +159,10 @@ def lib():
     L.sml_burst_server_destroy.argtypes = [vp]
     L.sml_burst_server_stop.restype = i32
     L.sml_burst_server_stop.argtypes = [vp]
+    L.sml_burst_server_start.restype = i32
+    L.sml_burst_server_start.argtypes = [vp]
+    L.sml_burst_server_inject_unanswered.restype = i32
+    L.sml_burst_server_inject_unanswered.argtypes = [vp, u32, ctypes.POINTER(PacketBurst)]
     L.sml_ipc_handle_bytes.restype = u32
     L.sml_ipc_get_handle.restype = i32
     L.sml_ipc_get_handle.argtypes = [vp, vp, ctypes.POINTER(u64)]
@@ -521,6 +525,16 @@ class BurstServer:
     def stop(self):
         """Leave the loop now (the next submit restarts it)."""
         _check("sml_burst_server_stop", lib().sml_burst_server_stop(self._h))
+
+    def start(self):
+        """Start the loop now instead of on the next submit."""
+        _check("sml_burst_server_start", lib().sml_burst_server_start(self._h))
+
+    def inject_unanswered(self, op: int, burst: PacketBurst):
+        """Test fault injection: ring the doorbell for `burst` with the server
+        stopped (what a failed submit leaves behind)."""
+        _check("sml_burst_server_inject_unanswered",
+               lib().sml_burst_server_inject_unanswered(self._h, op, ctypes.byref(burst)))
 
     def close(self):
         if self._h:

@@ -43,6 +43,8 @@ def _lib():
         L.sml_job_release.argtypes = [vp]
         L.sml_context_stats.restype = i32
         L.sml_context_stats.argtypes = [vp]
+        L.sml_ppp_per_ltu_calls.restype = i32
+        L.sml_ppp_per_ltu_calls.argtypes = [ctypes.c_char_p]
         _bound = True
     return L
 
@@ -174,3 +176,12 @@ def stats() -> dict:
     arr = (ctypes.c_uint64 * 5)()
     _ok(_lib().sml_context_stats(ctypes.cast(arr, ctypes.c_void_p)), "sml_context_stats")
     return dict(zip(("jobs_submitted", "jobs_finished", "numel_submitted", "slices", "packets"), list(arr)))
+
+
+def ppp_per_ltu_calls(name: str) -> bool:
+    """Whether the prepostprocessor `name` takes per-packet PreprocessSingle /
+    PostprocessSingle calls (sml_ppp_per_ltu_calls); ContextError for a name
+    the factory rejects."""
+    rc = _lib().sml_ppp_per_ltu_calls(name.encode())
+    _ok(min(rc, 0), "sml_ppp_per_ltu_calls")
+    return rc == 1

@@ -62,6 +62,31 @@ def collnet_stats(path: str = PLUGIN_PATH) -> dict:
     return {k: int(buf[i]) for i, k in enumerate(STATS[:n])}
 
 
+SAME_GPU_NETS = ("switchml", "socket")
+
+
+def same_gpu_rccl_env(rank: int, session: str, net: str = "switchml") -> dict:
+    """RCCL environment for W ranks that share ONE GPU (a one-GPU box standing
+    in for a node): RCCL refuses two ranks of one host on one device, so each
+    rank is a host of its own (NCCL_HOSTID), and the ranks reach each other
+    through a net — `net` = "switchml": this library's TCP net
+    (NCCL_NET_PLUGIN = librccl-net-switchml.so; its CollNet table declines
+    RCCL, so only the net is used), "socket": RCCL's built-in socket net over
+    the loopback interface.  The reductions (ncclInt8 MAX, ncclInt32 SUM) run
+    in RCCL's own ring kernels either way — the code the N-GPU node runs —
+    only the transport between the ranks differs.  Set these before
+    init_process_group("nccl")."""
+    if net not in SAME_GPU_NETS:
+        raise ValueError(f"net must be one of {SAME_GPU_NETS}")
+    env = {"NCCL_HOSTID": f"switchml-worker-{session}-{rank}", "RCCL_MSCCL_ENABLE": "0",
+           "RCCL_MSCCLPP_ENABLE": "0", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    if net == "switchml":
+        env["NCCL_NET_PLUGIN"] = PLUGIN_PATH
+    else:
+        env.update(NCCL_NET_PLUGIN="none", NCCL_NET="Socket", NCCL_SOCKET_IFNAME="lo")
+    return env
+
+
 def rank_env(rank: int, world: int, device: int, session: str, channels: int, algo: str | None,
              log_dir: str | None, threads: int = 1, packet_numel: int = 256) -> dict:
     ini = (f"[general]\nrank = {rank}\nnum_workers = {world}\nnum_worker_threads = {threads}\n"

@@ -105,6 +105,40 @@ int main(int argc, char** argv) {
         int st; waitpid(p, &st, 0);
         return WIFEXITED(st) ? WEXITSTATUS(st) : 1;
     }
+    if (mode == "reconnect") {
+        // worker 1 closes its communicator and reconnects at once, while
+        // worker 0 still holds the first one open; then worker 0 closes and
+        // reconnects in the same process.  Worker 1 must follow the SECOND
+        // order (keys of communicator 1), not the first one's log.
+        pid_t p = fork();
+        if (p == 0) {
+            {
+                JobOrder a(session, 1, 2, 20000);
+                CallKey k;
+                while (!a.Peek(&k)) usleep(100);
+                a.Consume();
+            }
+            CallKey k;
+            {
+                JobOrder b(session, 1, 2, 20000);
+                while (!b.Peek(&k)) usleep(100);
+                b.Consume();
+            }
+            printf("follower second order starts with comm %u\n", k.comm);
+            fflush(stdout);
+            _exit(k.comm == 1 ? 0 : 5);
+        }
+        {
+            JobOrder a(session, 0, 2, 20000);
+            a.Append(CallKey{0, 0, 0, 1, 7, 0});
+            usleep(300000);                          // still open while worker 1 reconnects
+        }
+        JobOrder b(session, 0, 2, 20000);            // same process, same session
+        b.Append(CallKey{1, 0, 0, 1, 7, 0});
+        int st;
+        waitpid(p, &st, 0);
+        return WIFEXITED(st) ? WEXITSTATUS(st) : 1;
+    }
     try {                                            // "join": a second leader for the session
         JobOrder o(session, 0, 2, 2000);
         printf("joined\n");
@@ -166,3 +200,32 @@ def test_stale_segment_replaced_live_one_refused(driver):
 def test_poison_reaches_every_worker(driver):
     r = subprocess.run([driver, "poison", f"poison-{os.getpid()}"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "follower saw poison" in r.stdout
+
+
+def test_reconnect_same_session(driver):
+    """a communicator closed and reconnected under the same
+    session — worker 1 first, while worker 0 still holds the old order — gets
+    the new order: worker 0 removes the name on close, a full segment (all
+    its workers attached) is an old communicator's and is not joined, and
+    worker 0's own old segment never blocks it."""
+    session = f"reconnect-{os.getpid()}"
+    r = subprocess.run([driver, "reconnect", session], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "starts with comm 1" in r.stdout
+    assert not os.path.exists(f"/dev/shm/switchml-collnet-{session}")
+
+
+def test_unsized_segment_is_not_mapped(driver):
+    """a follower that opens worker 0's segment between its O_EXCL
+    create and its ftruncate sees 0 bytes; mapping and reading it would raise
+    SIGBUS.  An empty segment of the session's name (what that window looks
+    like) is waited out by a follower and replaced by worker 0."""
+    session = f"unsized-{os.getpid()}"
+    path = f"/dev/shm/switchml-collnet-{session}"
+    open(path, "wb").close()                         # 0 bytes, like a segment not yet sized
+    try:
+        r = subprocess.run([driver, "join", session], capture_output=True, text=True, timeout=60)
+        assert "joined" in r.stdout, r.stdout + r.stderr
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)

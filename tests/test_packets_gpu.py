@@ -445,3 +445,42 @@ def test_burst_server_idle_restart_and_refusals(cuda):
                                                flags=s.FLAG_ROUND_RNE))
     srv.close()
     srv.close()
+
+
+@pytest.mark.gpu
+def test_burst_server_never_replays_an_unanswered_doorbell(cuda):
+    """after a failed submit the doorbell is ahead of `done`; a
+    relaunched server must not take that stale doorbell for a new burst.  The
+    injected one is an exchange burst on the ring's first window — replayed,
+    it would post-process those packets and overwrite their slots with the
+    next window's packets, so the real exchange of the same window (and the
+    output) would go wrong.  Start the server, give it time to (wrongly)
+    replay, then run the slice: bit-exact vs the oracle's packet loop."""
+    import time
+    import torch
+    s = sw()
+    P, W, n = 256, 2, 20_000
+    x = O.splitmix_normal(19, n)
+    xd = torch.from_numpy(x).to(cuda)
+    out = torch.zeros(n, device=cuda)
+    B = O.num_blocks(n, P)
+    b = 16
+    recv = torch.zeros(B, dtype=torch.int8, device=cuda)
+    ring = torch.zeros(b * P, dtype=torch.int32).pin_memory()
+    extra = torch.zeros(b * 2, dtype=torch.uint8).pin_memory()
+    srv = s.BurstServer(P, idle_ms=2000)
+    ids = list(range(b))
+    slots = [ring.data_ptr() + q * P * 4 for q in ids]
+    exs = [extra.data_ptr() + q * 2 for q in ids]
+    srv.submit(s.BURST_PRE, s.packet_burst(xd, out, P, W, b, recv, ids, slots, exs))
+    srv.inject_unanswered(s.BURST_EXCHANGE, s.packet_burst(xd, out, P, W, b, recv, ids, slots, exs,
+                                                           flags=s.FLAG_PROCESS_PACKET))
+    srv.start()
+    time.sleep(0.05)                       # a replaying server would have run the stale burst by now
+    for p0 in range(0, B + b, b):
+        got = list(range(p0, min(p0 + b, B + b)))
+        srv.submit(s.BURST_EXCHANGE, s.packet_burst(xd, out, P, W, b, recv, got, slots[:len(got)], exs[:len(got)],
+                                                    flags=s.FLAG_PROCESS_PACKET))
+    srv.close()
+    ref = O.dummy_packet_stream(x, P=P, batch_max=b, num_workers=W)[2]
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
