@@ -335,6 +335,10 @@ def main():
                 from switchml_amd.rccl_collnet import same_gpu_rccl_env
                 os.environ.update(same_gpu_rccl_env(rank, "bench" + os.environ.get("MASTER_PORT", "0")))
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+    pg = {"backend": dist.get_backend() if world > 1 else None,
+          "rehearsal": ("ranks share one GPU: " + ("gloo" if rehearse_mode == "gloo" else
+                                                   "RCCL, one RCCL host per rank (NCCL_HOSTID), SwitchML TCP net"))
+          if rehearse else None}
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     sw.lib()
@@ -496,6 +500,7 @@ def main():
                 "buckets_cycled": nb,
                 "xcd_chunk": args.xcd_chunk,
                 "launch": "eager" if args.graph_steps <= 1 else f"hipGraph replay, {args.graph_steps} steps per graph",
+                "process_group": pg,
             },
             "input_GBps": round(4 * (job_numel or world * N) / (elapsed / args.steps) / 1e9, 2),
             "kernel_ms": round(kern_ms_max, 5),
@@ -647,6 +652,7 @@ def rccl_collnet_field(world, same_gpu=False, timeout=120.0):
                "iallreduce_calls": rep["iallreduce_calls"], "returncodes": rep["returncodes"]}
         if ranks:
             out["rccl_int_allreduce_equals_exact_sum"] = all(r["int_exact"] for r in ranks)
+            out["plugin_by_hand_equals_exact_sum"] = all(r.get("hand_int_exact", False) for r in ranks)
             out["plugin_by_hand_equals_rccl_on_ints"] = all(r["int_equal_direct"] for r in ranks)
             out["normal_within_quantization_bound"] = all(r["normal_within_bound"] for r in ranks)
             if all("configs4_ms_per_iter" in r for r in ranks):

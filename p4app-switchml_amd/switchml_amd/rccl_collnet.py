@@ -222,16 +222,22 @@ def rank_main(a):
     r_int = t.cpu().numpy()
     out["int_exact"] = bool(np.array_equal(r_int.view(np.uint32), exact.view(np.uint32)))
 
-    # the same buffer through the plugin's iallreduce by hand (RCCL is done
-    # with it): the xgmi switch, one job
+    # the same data through the plugin's iallreduce by hand, on a FRESH copy
+    # of this rank's input (not RCCL's output buffer): the xgmi switch, one
+    # job.  hand_int_exact checks it against the exact sum on its own;
+    # int_equal_direct compares it with RCCL's result — so when RCCL's
+    # all-reduce is wrong (CollNetChain's no-op) that one is
+    # False while hand_int_exact stays True.
     from .collnet import CollNetComm
     comm = CollNetComm(nranks=W, rank=a.rank, path=PLUGIN_PATH)
-    h = torch.from_numpy(xs[a.rank]).to(dev)
+    h = torch.from_numpy(xs[a.rank].copy()).to(dev)
     torch.cuda.synchronize()
     comm.wait(comm.iallreduce(h.data_ptr(), h.data_ptr(), n))
     r_hand = h.cpu().numpy()
+    out["hand_int_exact"] = bool(np.array_equal(r_hand.view(np.uint32), exact.view(np.uint32)))
     out["int_equal_direct"] = bool(np.array_equal(r_hand.view(np.uint32), r_int.view(np.uint32)))
-    say(f"by-hand iallreduce done: int_exact {out['int_exact']} equal_direct {out['int_equal_direct']}")
+    say(f"by-hand iallreduce done: RCCL int_exact {out['int_exact']}, by-hand int_exact {out['hand_int_exact']}, "
+        f"by-hand equal to RCCL {out['int_equal_direct']}")
 
     # 2) N(0,1) data: RCCL vs by hand (equal when RCCL's CollNet chunks start
     # on packet boundaries) and vs the fp32 sum within the quantization bound
@@ -352,7 +358,9 @@ def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, cha
     rep["collnet_dispatched_by_rccl"] = bool(ok and all(
         r["stats_after_first"]["iallreduce"] > r["stats_before"]["iallreduce"] for r in ranks))
     rep["collnet_declined"] = bool(ok and all(r["stats_end"].get("declined", 0) >= 1 for r in ranks))
-    rep["ok"] = bool(ok and all(r["int_exact"] and r["int_equal_direct"] and r["normal_within_bound"] for r in ranks)
+    rep["hand_int_exact"] = bool(ok and all(r.get("hand_int_exact", False) for r in ranks))
+    rep["ok"] = bool(ok and all(r["int_exact"] and r["hand_int_exact"] and r["int_equal_direct"] and r["normal_within_bound"]
+                                for r in ranks)
                      and (rep["collnet_dispatched_by_rccl"] if allow_collnet else rep["collnet_declined"]))
     return rep
 

@@ -28,7 +28,7 @@ def test_rccl_runs_over_switchml_net_and_collnet_declines(cuda, tmp_path):
     assert rep["returncodes"] == [0, 0], rep.get("tails")
     assert rep["collnet_declined"] and not rep["collnet_dispatched_by_rccl"]
     for r in rep["ranks"]:
-        assert r["int_exact"] and r["int_equal_direct"] and r["normal_within_bound"], r
+        assert r["int_exact"] and r["hand_int_exact"] and r["int_equal_direct"] and r["normal_within_bound"], r
         assert r["stats_after_first"]["iallreduce"] == r["stats_before"]["iallreduce"]
     assert rep["ok"]
     logs = "".join(open(os.path.join(tmp_path, f), errors="replace").read()
