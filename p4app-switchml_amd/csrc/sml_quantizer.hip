@@ -372,10 +372,18 @@ __global__ void k_scale_lut(float* lut, uint32_t W) {
 template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE>
 static void launch_quant_u(uint32_t U, bool nts, dim3 grid, hipStream_t st, const QuantArgs& a) {
     if constexpr (P <= 256) {
-        if (U == 1) { k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 1><<<grid, kBlockThreads, 0, st>>>(a); return; }
+        if (U == 1) {
+            if (nts) k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 1, true><<<grid, kBlockThreads, 0, st>>>(a);
+            else k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 1><<<grid, kBlockThreads, 0, st>>>(a);
+            return;
+        }
     }
     if constexpr (P <= 512) {
-        if (U == 2) { k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 2><<<grid, kBlockThreads, 0, st>>>(a); return; }
+        if (U == 2) {
+            if (nts) k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 2, true><<<grid, kBlockThreads, 0, st>>>(a);
+            else k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 2><<<grid, kBlockThreads, 0, st>>>(a);
+            return;
+        }
     }
     if (nts) { k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 4, true><<<grid, kBlockThreads, 0, st>>>(a); return; }
     k_quantize_pack<P, ALIGNED, GLOBAL, BE, RNE, 4><<<grid, kBlockThreads, 0, st>>>(a);
@@ -576,8 +584,8 @@ static sml_status_t quantize_common(const float* d_in, uint64_t numel, uint32_t 
     dim3 grid(grid_for_tiles(a.ntiles));
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_in), be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
-    // payload store policy by plane size (4-slice tiles only)
-    const bool nts = d_payload && U == 4 && 4 * numel >= g_nt_threshold.load(std::memory_order_relaxed);
+    // payload store policy by plane size
+    const bool nts = d_payload && 4 * numel >= g_nt_threshold.load(std::memory_order_relaxed);
     if (d_gexp) {
         if (al) launch_quant_b<true, true>(be, rne, P, U, nts, grid, st, a);
         else launch_quant_b<false, true>(be, rne, P, U, nts, grid, st, a);
