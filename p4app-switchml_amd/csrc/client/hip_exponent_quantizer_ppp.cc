@@ -61,6 +61,7 @@ uint64_t HipExponentQuantizerPPP::SetupJobSlice(JobSlice* job_slice) {
     job_slice_ = job_slice;
     pool_probe_ = nullptr;
     xpool_probe_ = nullptr;
+    dev_of_.clear();
     const uint64_t bytes = job_slice->slice.numel * DataTypeSize(job_slice->slice.data_type);
     total_main_num_ltus_ = (bytes + ltu_size_ - 1) / ltu_size_;
     batch_num_ltus_ = std::min<uint64_t>(total_main_num_ltus_, batch_max_num_ltus_);
@@ -277,8 +278,11 @@ void HipExponentQuantizerPPP::burst(BurstKind kind, uint32_t n, const uint64_t* 
     const bool per_buffer = delta != 0 || xdelta != 0;
     auto dev_addr = [&](void* p) -> void* {
         if (!p || !per_buffer) return p;
+        auto it = dev_of_.find(p);   // a NIC pool's buffers recur burst after burst: one query per slice
+        if (it != dev_of_.end()) return it->second;
         void* a = packet_mem(p).dev;
         if (!a) throw SwitchMLFatal("burst: a packet buffer of the burst is not device-addressable");
+        dev_of_.emplace(p, a);
         return a;
     };
     const bool exchange = kind == BurstKind::kExchange || kind == BurstKind::kProcessExchange;

@@ -17,6 +17,8 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <unordered_map>
+
 #include "prepostprocessor.h"
 #include "switchml_hip.h"
 
@@ -98,6 +100,9 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     void* xpool_probe_ = nullptr;
     void* xpool_dev_ = nullptr;
     bool xpool_host_ = true;
+    // host -> device address of each packet buffer of the slice, when the
+    // pool's addresses differ (a hipHostRegister'd pool): queried per buffer
+    std::unordered_map<void*, void*> dev_of_;
     // persistent burst server for host-memory packets (backend.hip.burst_server)
     sml_burst_server* server_ = nullptr;
     bool server_synced_ = false;   // stream_ drained before the slice's first server burst

@@ -57,3 +57,21 @@ def test_per_packet_caller_under_hip_name_is_exact(cuda, tmp_path, numel):
     ref = O.dummy_allreduce(x, P=256, max_outstanding_packets=64, num_worker_threads=1, num_workers=1)
     got = np.fromfile(out, dtype=np.float32)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cpu_exponent_quantizer", "hip_exponent_quantizer"])
+def test_burst_hooks_over_registered_pools_are_exact(cuda, tmp_path, name):
+    """the burst hooks over a NIC-like pool — ring and extra-info
+    slots in two separate hipHostRegister'd allocations, whose device
+    addresses may differ from their host addresses and from each other's
+    offset — translate every buffer by its own registration.  The reference
+    name takes the burst hooks (only its per-packet calls are refused)."""
+    out = tmp_path / "o.f32"
+    numel = 70_001
+    r = subprocess.run([BIN, name, str(numel), str(out), "burst-registered"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    x = np.arange(numel, dtype=np.float32) * np.where(np.arange(numel) % 2, -1, 1).astype(np.float32)
+    ref = O.dummy_allreduce(x, P=256, max_outstanding_packets=64, num_worker_threads=1, num_workers=1)
+    assert np.array_equal(np.fromfile(out, dtype=np.float32).view(np.uint32), ref.view(np.uint32))
