@@ -419,9 +419,9 @@ uint32_t sml_set_quantize_tile_slices(uint32_t slices);
 /* Tuning knob: output planes of at least `bytes` bytes are written with
  * non-temporal stores — the payload plane of sml_quantize_pack (K1/K3), the
  * fp32 output of sml_dequantize (K4), sml_roundtrip_loopback and
- * sml_roundtrip_loopback_batch (by the batch's total output; default:
- * larger than the 256 MiB Infinity Cache — DESIGN.md §4); UINT64_MAX =
- * never, 0 = always.
+ * sml_roundtrip_loopback_batch (by the batch's total output) and the
+ * sml_stream_copy probe; default 64 MiB, a quarter of the 256 MiB Infinity
+ * Cache — DESIGN.md §4); UINT64_MAX = never, 0 = always.
  * Results are identical either way.  Returns the previous value. */
 uint64_t sml_set_payload_nt_threshold(uint64_t bytes);
 
