@@ -517,7 +517,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": load_traffic(N, P, "quantize_pack" if nb == 1 else "quantize_pack_cold"),
-                "kernel": f"sml::k_quantize_pack<{P},aligned,fused,BE,half-away>",
+                "kernel": f"sml::k_quantize_pack<{P},aligned,fused,BE,half-away> (K1: 2-slice wave tiles, non-temporal payload stores at >= 64 MiB)",
             },
             "self_check": ok,
             "self_check_detail": {"what": check_note, "buckets_checked_min_over_ranks": checked},

@@ -410,9 +410,10 @@ uint32_t sml_set_grid_limit(uint32_t max_workgroups);
 uint32_t sml_set_xcd_chunk(uint32_t chunk);
 
 /* Tuning knob: slices of 256 elements per wave tile in sml_exponents /
- * sml_quantize_pack (K1/K2/K3): 4 (the default; 0 or any other value
- * restores it), 2 or 1 — never below P / 256.  Results are identical for
- * every size; smaller tiles measured slower.  Returns the
+ * sml_quantize_pack (K1/K2/K3): 4, 2 or 1 for every kernel — never below
+ * P / 256 — or 0 (the default; any other value restores it): by kernel, as
+ * measured fastest — K1 (fused, exponents computed) 2, K2 and K3 4.
+ * Results are identical for every size.  Returns the
  * previous value. */
 uint32_t sml_set_quantize_tile_slices(uint32_t slices);
 

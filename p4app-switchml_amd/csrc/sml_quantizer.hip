@@ -400,12 +400,16 @@ static void launch_quant_p(uint32_t P, uint32_t U, bool nts, dim3 grid, hipStrea
     }
 }
 
-// Slices per K1/K2/K3 tile: 4 (1024-element tiles, the default), 2 or 1
-// (never below P / 256).  sml_set_quantize_tile_slices.  Measured
-// (profiles/r02/sweep_tile_slices_p*.json): 1-slice tiles lose 15 % resident
-// and 4 % cold (one 1 KiB load in flight per wave is latency-bound; K2 -35 %),
-// 2-slice tiles are level on cold HBM and lose up to 11 % resident.
-static std::atomic<uint32_t> g_quant_slices{4};
+// Slices per K1/K2/K3 tile: 4 (1024-element tiles), 2 or 1 (never below
+// P / 256), or 0 = by kernel (the default): K1 2, K2 / K3 4.
+// sml_set_quantize_tile_slices.  Measured with non-temporal payload stores
+// on the bench workload, steps cycling 4 buckets (round 4,
+// profiles/r04/ab_slices_nt.json, interleaved medians): K1 with 2-slice tiles
+// +1.3 / +0.6 / +3.8 / +0.9 % at 128 / 256 / 512 / 1024 MiB, K3 -2.8 % and
+// K2 -2.6 % at 256 MiB; 1-slice tiles lose everywhere (K1 -3 %, K2 -35 %:
+// one 1 KiB load in flight per wave is latency-bound).  Round 2's sweep ran
+// before the non-temporal stores and had 2-slice K1 level cold.
+static std::atomic<uint32_t> g_quant_slices{0};
 
 // Payload planes (and K4 / round-trip fp32 outputs) of at least this many
 // bytes take non-temporal stores (sml_set_payload_nt_threshold; UINT64_MAX =
@@ -422,9 +426,10 @@ static std::atomic<uint32_t> g_quant_slices{4};
 // next reader can find them in the cache.  Bytes are identical either way.
 static std::atomic<uint64_t> g_nt_threshold{64ull << 20};
 
-static uint32_t quant_slices(uint32_t P) {
+static uint32_t quant_slices(uint32_t P, bool fused_k1) {
     const uint32_t need = P > 256 ? P / 256 : 1;
-    const uint32_t want = g_quant_slices.load(std::memory_order_relaxed);
+    uint32_t want = g_quant_slices.load(std::memory_order_relaxed);
+    if (want == 0) want = fused_k1 ? 2u : 4u;
     return want > need ? want : need;
 }
 
@@ -536,7 +541,7 @@ uint32_t sml_set_xcd_chunk(uint32_t chunk) {
 uint64_t sml_set_payload_nt_threshold(uint64_t bytes) { return g_nt_threshold.exchange(bytes); }
 
 uint32_t sml_set_quantize_tile_slices(uint32_t slices) {
-    return g_quant_slices.exchange(slices == 1 || slices == 2 ? slices : 4u);
+    return g_quant_slices.exchange(slices == 1 || slices == 2 || slices == 4 ? slices : 0u);
 }
 
 uint64_t sml_num_blocks(uint64_t numel, uint32_t packet_numel) {
@@ -569,7 +574,7 @@ static sml_status_t quantize_common(const float* d_in, uint64_t numel, uint32_t 
     if (!d_in || !aligned4(d_in)) return SML_ERR_INVALID_ARG;
     if (d_payload && !aligned16(d_payload)) return SML_ERR_ALIGNMENT;
     QuantArgs a;
-    const uint32_t U = quant_slices(P);
+    const uint32_t U = quant_slices(P, d_payload && !d_gexp);
     // XCD runs keep their byte length (C workgroups of 4 U-slice tiles)
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);
     a.in = d_in;

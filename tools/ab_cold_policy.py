@@ -123,7 +123,7 @@ def main(out_path=None, rounds=7):
         del xs, pls, exs
         torch.cuda.empty_cache()
     sw.set_payload_nt_threshold(default_thr)
-    sw.set_quantize_tile_slices(4)
+    sw.set_quantize_tile_slices(0)
     s = json.dumps({"default_nt_threshold_bytes": default_thr, "results": res,
                     "k4_and_roundtrip": main_k4(rounds)}, indent=1)
     print(s)

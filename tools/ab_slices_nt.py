@@ -81,7 +81,7 @@ def main(rounds=9, nbuf=4):
                                                              "GBps": round(alg[kind] / m / 1e3, 1)}
         del xs, pls, exs
         torch.cuda.empty_cache()
-    sw.set_quantize_tile_slices(4)
+    sw.set_quantize_tile_slices(0)
     sw.set_xcd_chunk(64)
     print(json.dumps({"what": "K1 (K3, K2 at 256 MiB) tile slices x XCD run, nt payload stores, bench_bucket data, "
                       f"{nbuf} buckets cycled, {rounds} interleaved rounds, medians", "res": res}, indent=1))

@@ -89,7 +89,7 @@ def main(N=64 << 20, nbuf=4, rounds=7, reps=30):
                 torch.cuda.synchronize()
                 times[(name, kind)].append(a.elapsed_time(b) / r * 1e3)
     sw.set_xcd_chunk(64)
-    sw.set_quantize_tile_slices(4)
+    sw.set_quantize_tile_slices(0)
     alg = {"K1 resident": 8 * N + B, "K1 cold": 8 * N + B, "K1 1GiB": 8 * NB + BB, "K3 cold": 8 * N + B,
            "K2 cold": 4 * N + B}
     out = {}

@@ -52,7 +52,7 @@ def main():
             sw.set_quantize_tile_slices(tpw)
             res[(g, tpw)].append(t_of(lambda: sw.quantize_pack(x, P, W, payload=payload, exps_out=exps, stream=st)))
         sw.set_grid_limit(0)
-        sw.set_quantize_tile_slices(4)
+        sw.set_quantize_tile_slices(0)
         copy.append(t_of(lambda: out.copy_(x)))
         ntcopy.append(t_of(lambda: sw.stream_copy(x, out, stream=st)))
     rows = []

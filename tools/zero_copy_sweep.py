@@ -33,7 +33,7 @@ def main(N=64 * 1024 * 1024, P=256, reps=3, rounds=3):
             torch.cuda.synchronize()
             res.setdefault(f"grid{g}_slices{tpw}", []).append(4 * N * reps / (time.perf_counter() - t0) / 1e9)
     sw.set_grid_limit(0)
-    sw.set_quantize_tile_slices(4)
+    sw.set_quantize_tile_slices(0)
     print(json.dumps({k: round(statistics.median(v), 2) for k, v in res.items()}, indent=1))
 
 
