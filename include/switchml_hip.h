@@ -417,6 +417,12 @@ uint32_t sml_set_xcd_chunk(uint32_t chunk);
  * previous value. */
 uint32_t sml_set_quantize_tile_slices(uint32_t slices);
 
+/* Tuning knob: slices of 256 elements per wave tile in sml_dequantize (K4)
+ * and sml_roundtrip_loopback (the fused round trip; P = 1024 keeps 4): 4 or
+ * 2, or 0 = the default.  Results are identical for every
+ * size.  Returns the previous value. */
+uint32_t sml_set_stream_tile_slices(uint32_t slices);
+
 /* Tuning knob: output planes of at least `bytes` bytes are written with
  * non-temporal stores — the payload plane of sml_quantize_pack (K1/K3), the
  * fp32 output of sml_dequantize (K4), sml_roundtrip_loopback and

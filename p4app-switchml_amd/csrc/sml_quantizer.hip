@@ -134,18 +134,19 @@ struct DequantArgs {
 // K4: dequantize the aggregated payload (PostprocessSingle, ppp.cc:197-251).
 // RCP (power-of-two W): multiply by the exact reciprocal instead of the IEEE
 // division — same bits (rcp_scale_pow2).
-template <int P, bool ALIGNED, bool BE, bool RCP, bool NT = false>
+template <int P, bool ALIGNED, bool BE, bool RCP, bool NT = false, int U = kU>
 __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
     __shared__ float lut[256];
     if constexpr (RCP) build_rcp_lut(lut, a.W);
     else build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    constexpr int kElems = tile_elems<U>();
     for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
-        const uint64_t base = t * kTileElems;
-        const bool full = base + kTileElems <= a.numel;
-        u4 w[kU];
-        float s[kU];
+        const uint64_t base = t * kElems;
+        const bool full = base + kElems <= a.numel;
+        u4 w[U];
+        float s[U];
         if (full && slice_exps_scalar_ok<P>(a.exps)) {
             // Full tile: each slice's exponent bytes with one scalar load
             // (measured: a per-lane byte load per slice costs ~8 % at
@@ -153,19 +154,19 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
             // blocks with the partial-tile path made hipcc wait vmcnt(0), on
             // the previous slice's store too, before every slice.
 #pragma unroll
-            for (int u = 0; u < kU; u++) {
+            for (int u = 0; u < U; u++) {
                 w[u] = __builtin_nontemporal_load(a.payload + (base + (uint64_t)(u * kWave + lane) * 4) / 4);
                 s[u] = lut[slice_exponent_byte<P>(a.exps, base, u, lane)];
             }
 #pragma unroll
-            for (int u = 0; u < kU; u++) {
+            for (int u = 0; u < U; u++) {
                 const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
                 store4<ALIGNED, NT>(a.out + idx, dequant_words<BE, RCP>(w[u], s[u]));
             }
             continue;
         } else {
 #pragma unroll
-            for (int u = 0; u < kU; u++) {
+            for (int u = 0; u < U; u++) {
                 const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
                 if (full || idx < a.numel) {
                     w[u] = __builtin_nontemporal_load(a.payload + idx / 4);
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
             }
         }
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
+        for (int u = 0; u < U; u++) {
             const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
             if (!full && idx >= a.numel) continue;
             const f4 o = dequant_words<BE, RCP>(w[u], s[u]);
@@ -199,35 +200,37 @@ struct RoundTripArgs {
 // Fused dummy-backend round trip: PreprocessSingle -> ProcessPacket (x W) ->
 // PostprocessSingle for every packet of the slice in one HBM pass.  One tile
 // of one slice (blocks restart at the slice start, as in the reference).
-template <int P, bool ALIGNED, bool BE, bool RNE, bool NT = false>
+template <int P, bool ALIGNED, bool BE, bool RNE, bool NT = false, int U = kU>
 __device__ __forceinline__ void roundtrip_tile(const RoundTripArgs& a, uint64_t t, const float* lut, int lane) {
+    static_assert(U * 256 >= P, "a tile holds whole packets");
+    constexpr int kElems = tile_elems<U>();
     const bool pow2 = (a.W & (a.W - 1)) == 0;
     const uint32_t log2W = 31 - __builtin_clz(a.W);
     const uint64_t padded = a.nblocks * P;
-    const uint64_t base = t * kTileElems;
-    const bool full = base + kTileElems <= a.numel;
-    f4 v[kU];
+    const uint64_t base = t * kElems;
+    const bool full = base + kElems <= a.numel;
+    f4 v[U];
     if (full) {
 #pragma unroll
-        for (int u = 0; u < kU; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
+        for (int u = 0; u < U; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
     } else {
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
+        for (int u = 0; u < U; u++) {
             uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
             v[u] = load4_guarded(a.in + idx, idx, a.numel);
         }
     }
-    int e[kU];
+    int e[U];
     tile_exponents<P>(v, e);
     if (a.exps_out) {
-        constexpr int kPk = kTileElems / P;
-        if (((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kTileElems <= padded)
+        constexpr int kPk = kElems / P;
+        if (((uintptr_t)a.exps_out & (kPk - 1)) == 0 && base + kElems <= padded)
             store_tile_exponents<P>(a.exps_out + base / P, lane, e);
         else
             store_exponents<P>(a.exps_out, base, lane, e, a.nblocks);
     }
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
+    for (int u = 0; u < U; u++) {
         const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
         if (idx >= padded) continue;
         const float s = lut[(uint8_t)e[u]];
@@ -260,14 +263,14 @@ __device__ __forceinline__ void roundtrip_tile(const RoundTripArgs& a, uint64_t 
     }
 }
 
-template <int P, bool ALIGNED, bool BE, bool RNE, bool NT = false>
+template <int P, bool ALIGNED, bool BE, bool RNE, bool NT = false, int U = kU>
 __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
     __shared__ float lut[256];
     build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves)
-        roundtrip_tile<P, ALIGNED, BE, RNE, NT>(a, t, lut, lane);
+        roundtrip_tile<P, ALIGNED, BE, RNE, NT, U>(a, t, lut, lane);
 }
 
 // The fused round trip over a batch of slices (of one or several jobs) in ONE
@@ -426,6 +429,15 @@ static std::atomic<uint32_t> g_quant_slices{0};
 // next reader can find them in the cache.  Bytes are identical either way.
 static std::atomic<uint64_t> g_nt_threshold{64ull << 20};
 
+// Slices per K4 / fused round-trip tile: 4 or 2 (sml_set_stream_tile_slices;
+// 0 = the measured default below).
+static std::atomic<uint32_t> g_stream_slices{0};
+
+static uint32_t stream_slices(uint32_t dflt) {
+    const uint32_t want = g_stream_slices.load(std::memory_order_relaxed);
+    return want ? want : dflt;
+}
+
 static uint32_t quant_slices(uint32_t P, bool fused_k1) {
     const uint32_t need = P > 256 ? P / 256 : 1;
     uint32_t want = g_quant_slices.load(std::memory_order_relaxed);
@@ -446,44 +458,54 @@ static void launch_quant_b(bool be, bool rne, uint32_t P, uint32_t U, bool nts, 
     else launch_quant_r<ALIGNED, GLOBAL, false>(rne, P, U, nts, g, st, a);
 }
 
-template <bool ALIGNED, bool BE, bool RCP, bool NT>
+template <bool ALIGNED, bool BE, bool RCP, bool NT, int U>
 static void launch_deq_pn(uint32_t P, dim3 grid, hipStream_t st, const DequantArgs& a) {
     switch (P) {
-        case 64:   k_dequantize<64, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_dequantize<128, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_dequantize<256, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_dequantize<512, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_dequantize<1024, ALIGNED, BE, RCP, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   k_dequantize<64, ALIGNED, BE, RCP, NT, U><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_dequantize<128, ALIGNED, BE, RCP, NT, U><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_dequantize<256, ALIGNED, BE, RCP, NT, U><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_dequantize<512, ALIGNED, BE, RCP, NT, U><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_dequantize<1024, ALIGNED, BE, RCP, NT, U><<<grid, kBlockThreads, 0, st>>>(a); break;
     }
 }
 
 template <bool ALIGNED, bool BE, bool RCP>
-static void launch_deq_p(uint32_t P, bool nt, dim3 grid, hipStream_t st, const DequantArgs& a) {
-    if (nt) launch_deq_pn<ALIGNED, BE, RCP, true>(P, grid, st, a);
-    else launch_deq_pn<ALIGNED, BE, RCP, false>(P, grid, st, a);
+static void launch_deq_p(uint32_t P, uint32_t U, bool nt, dim3 grid, hipStream_t st, const DequantArgs& a) {
+    if (U == 2) {
+        if (nt) launch_deq_pn<ALIGNED, BE, RCP, true, 2>(P, grid, st, a);
+        else launch_deq_pn<ALIGNED, BE, RCP, false, 2>(P, grid, st, a);
+        return;
+    }
+    if (nt) launch_deq_pn<ALIGNED, BE, RCP, true, 4>(P, grid, st, a);
+    else launch_deq_pn<ALIGNED, BE, RCP, false, 4>(P, grid, st, a);
 }
 
 template <bool ALIGNED, bool BE>
-static void launch_deq_w(uint32_t P, bool nt, dim3 grid, hipStream_t st, const DequantArgs& a) {
-    if ((a.W & (a.W - 1)) == 0) launch_deq_p<ALIGNED, BE, true>(P, nt, grid, st, a);
-    else launch_deq_p<ALIGNED, BE, false>(P, nt, grid, st, a);
+static void launch_deq_w(uint32_t P, uint32_t U, bool nt, dim3 grid, hipStream_t st, const DequantArgs& a) {
+    if ((a.W & (a.W - 1)) == 0) launch_deq_p<ALIGNED, BE, true>(P, U, nt, grid, st, a);
+    else launch_deq_p<ALIGNED, BE, false>(P, U, nt, grid, st, a);
 }
 
-template <bool ALIGNED, bool BE, bool RNE, bool NT>
+template <bool ALIGNED, bool BE, bool RNE, bool NT, int U>
 static void launch_rt_pn(uint32_t P, dim3 grid, hipStream_t st, const RoundTripArgs& a) {
     switch (P) {
-        case 64:   k_roundtrip<64, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_roundtrip<128, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_roundtrip<256, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_roundtrip<512, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_roundtrip<1024, ALIGNED, BE, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   k_roundtrip<64, ALIGNED, BE, RNE, NT, U><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_roundtrip<128, ALIGNED, BE, RNE, NT, U><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_roundtrip<256, ALIGNED, BE, RNE, NT, U><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_roundtrip<512, ALIGNED, BE, RNE, NT, U><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_roundtrip<1024, ALIGNED, BE, RNE, NT, 4><<<grid, kBlockThreads, 0, st>>>(a); break;   // a tile holds the packet
     }
 }
 
 template <bool ALIGNED, bool BE, bool RNE>
-static void launch_rt_p(uint32_t P, bool nt, dim3 grid, hipStream_t st, const RoundTripArgs& a) {
-    if (nt) launch_rt_pn<ALIGNED, BE, RNE, true>(P, grid, st, a);
-    else launch_rt_pn<ALIGNED, BE, RNE, false>(P, grid, st, a);
+static void launch_rt_p(uint32_t P, uint32_t U, bool nt, dim3 grid, hipStream_t st, const RoundTripArgs& a) {
+    if (U == 2) {
+        if (nt) launch_rt_pn<ALIGNED, BE, RNE, true, 2>(P, grid, st, a);
+        else launch_rt_pn<ALIGNED, BE, RNE, false, 2>(P, grid, st, a);
+        return;
+    }
+    if (nt) launch_rt_pn<ALIGNED, BE, RNE, true, 4>(P, grid, st, a);
+    else launch_rt_pn<ALIGNED, BE, RNE, false, 4>(P, grid, st, a);
 }
 
 template <bool RNE, bool NT>
@@ -504,9 +526,10 @@ static void launch_rtb_p(uint32_t P, bool nt, dim3 grid, hipStream_t st, const R
 }
 
 template <bool ALIGNED>
-static void launch_rt_a(bool be, bool rne, bool nt, uint32_t P, dim3 g, hipStream_t st, const RoundTripArgs& a) {
-    if (be) { if (rne) launch_rt_p<ALIGNED, true, true>(P, nt, g, st, a); else launch_rt_p<ALIGNED, true, false>(P, nt, g, st, a); }
-    else    { if (rne) launch_rt_p<ALIGNED, false, true>(P, nt, g, st, a); else launch_rt_p<ALIGNED, false, false>(P, nt, g, st, a); }
+static void launch_rt_a(bool be, bool rne, bool nt, uint32_t P, uint32_t U, dim3 g, hipStream_t st,
+                        const RoundTripArgs& a) {
+    if (be) { if (rne) launch_rt_p<ALIGNED, true, true>(P, U, nt, g, st, a); else launch_rt_p<ALIGNED, true, false>(P, U, nt, g, st, a); }
+    else    { if (rne) launch_rt_p<ALIGNED, false, true>(P, U, nt, g, st, a); else launch_rt_p<ALIGNED, false, false>(P, U, nt, g, st, a); }
 }
 
 }  // namespace sml
@@ -539,6 +562,10 @@ uint32_t sml_set_xcd_chunk(uint32_t chunk) {
 }
 
 uint64_t sml_set_payload_nt_threshold(uint64_t bytes) { return g_nt_threshold.exchange(bytes); }
+
+uint32_t sml_set_stream_tile_slices(uint32_t slices) {
+    return g_stream_slices.exchange(slices == 2 || slices == 4 ? slices : 0u);
+}
 
 uint32_t sml_set_quantize_tile_slices(uint32_t slices) {
     return g_quant_slices.exchange(slices == 1 || slices == 2 || slices == 4 ? slices : 0u);
@@ -627,19 +654,20 @@ sml_status_t sml_dequantize(const int32_t* d_payload, const int8_t* d_exps, uint
     if (!d_payload || !d_exps || !d_out || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
     if (!aligned16(d_payload)) return SML_ERR_ALIGNMENT;
     DequantArgs a;
-    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    const uint32_t U = stream_slices(4);
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);   // XCD runs keep their byte length
     a.payload = reinterpret_cast<const u4*>(d_payload);
     a.exps = d_exps;
     a.out = d_out;
     a.numel = numel;
-    a.ntiles = (numel + kTileElems - 1) / kTileElems;
+    a.ntiles = (numel + 256 * U - 1) / (256 * U);
     a.W = num_workers;
     dim3 grid(grid_for_tiles(a.ntiles));
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_out), be = !(flags & SML_FLAG_PAYLOAD_LE);
     const bool nt = 4 * numel >= g_nt_threshold.load(std::memory_order_relaxed);   // output plane past the Infinity Cache
-    if (al) { if (be) launch_deq_w<true, true>(packet_numel, nt, grid, st, a); else launch_deq_w<true, false>(packet_numel, nt, grid, st, a); }
-    else    { if (be) launch_deq_w<false, true>(packet_numel, nt, grid, st, a); else launch_deq_w<false, false>(packet_numel, nt, grid, st, a); }
+    if (al) { if (be) launch_deq_w<true, true>(packet_numel, U, nt, grid, st, a); else launch_deq_w<true, false>(packet_numel, U, nt, grid, st, a); }
+    else    { if (be) launch_deq_w<false, true>(packet_numel, U, nt, grid, st, a); else launch_deq_w<false, false>(packet_numel, U, nt, grid, st, a); }
     return launch_check();
 }
 
@@ -653,12 +681,13 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
     if (!d_in || !d_out || !aligned4(d_in) || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
     if (d_payload && !aligned16(d_payload)) return SML_ERR_ALIGNMENT;
     RoundTripArgs a;
-    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    const uint32_t U = packet_numel > 512 ? 4u : stream_slices(4);   // a tile holds whole packets
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);
     a.in = d_in;
     a.out = d_out;
     a.numel = numel;
     a.nblocks = sml_num_blocks(numel, packet_numel);
-    a.ntiles = (a.nblocks * packet_numel + kTileElems - 1) / kTileElems;
+    a.ntiles = (a.nblocks * packet_numel + 256 * U - 1) / (256 * U);
     a.payload = reinterpret_cast<u4*>(d_payload);
     a.exps_out = d_exps_out;
     a.W = num_workers;
@@ -669,8 +698,8 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
     const bool al = aligned16(d_in) && aligned16(d_out);
     const bool be = !(flags & SML_FLAG_PAYLOAD_LE), rne = flags & SML_FLAG_ROUND_RNE;
     const bool nt = 4 * numel >= g_nt_threshold.load(std::memory_order_relaxed);   // output plane past the Infinity Cache
-    if (al) launch_rt_a<true>(be, rne, nt, packet_numel, grid, st, a);
-    else launch_rt_a<false>(be, rne, nt, packet_numel, grid, st, a);
+    if (al) launch_rt_a<true>(be, rne, nt, packet_numel, U, grid, st, a);
+    else launch_rt_a<false>(be, rne, nt, packet_numel, U, grid, st, a);
     return launch_check();
 }
 

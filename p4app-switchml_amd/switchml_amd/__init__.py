@@ -129,6 +129,8 @@ def lib():
     L.sml_quantize_pack_frames.argtypes = [vp, u64, u32, u16, vp, u32, ctypes.POINTER(FrameParams), vp, u64, vp]
     L.sml_set_quantize_tile_slices.restype = u32
     L.sml_set_quantize_tile_slices.argtypes = [u32]
+    L.sml_set_stream_tile_slices.restype = u32
+    L.sml_set_stream_tile_slices.argtypes = [u32]
     L.sml_set_payload_nt_threshold.restype = u64
     L.sml_set_payload_nt_threshold.argtypes = [u64]
     L.sml_set_xcd_chunk.restype = u32
@@ -232,6 +234,12 @@ def set_quantize_tile_slices(slices: int) -> int:
     kernel (never below P/256), or 0 = by kernel (the default: K1 2, K2/K3
     4); returns the previous setting."""
     return int(lib().sml_set_quantize_tile_slices(slices))
+
+
+def set_stream_tile_slices(slices: int) -> int:
+    """Slices of 256 elements per K4 / fused round-trip wave tile: 4 or 2,
+    or 0 = the default; returns the previous setting."""
+    return int(lib().sml_set_stream_tile_slices(slices))
 
 
 def set_xcd_chunk(chunk: int) -> int:

@@ -163,3 +163,48 @@ def test_output_store_policy_invariant(sw, P):
                 assert np.array_equal(rt.cpu().numpy().view(np.uint32), dq.view(np.uint32)), (off, nt)
     finally:
         sw.set_payload_nt_threshold(orig)
+
+
+@pytest.mark.parametrize("P", [64, 256, 512, 1024])
+def test_stream_tile_slices_invariant(sw, P):
+    """K4 and the fused round trip with 2- and 4-slice wave tiles
+    (sml_set_stream_tile_slices; P = 1024 keeps 4 in the round trip), both
+    store policies, capped grids and XCD orders, aligned and 4-byte-offset
+    slices, W = 3 (IEEE division) and W = 4 (exact reciprocal): the oracle's
+    bytes, and the round trip's payload and exponent planes too."""
+    import torch
+    n = 200_003
+    x_np = O.splitmix_normal(P + 91, n + 1)
+    xd = torch.from_numpy(x_np).cuda()
+    orig = sw.set_payload_nt_threshold(2 ** 64 - 1)
+    try:
+        for W in (3, 4):
+            for off in (0, 1):
+                xs, xn = xd[off:off + n], x_np[off:off + n]
+                q, e = O.quantize(xn, P, W), O.exponents(xn, P)
+                dq = O.dequantize(O.loopback_aggregate(q, W), e, n, P, W)
+                for sl, nt in ((2, 0), (4, 0), (2, 2 ** 64 - 1), (0, 0)):
+                    sw.set_stream_tile_slices(sl)
+                    sw.set_payload_nt_threshold(nt)
+                    for cap, chunk in GEOMETRIES[:2] + GEOMETRIES[6:8]:
+                        sw.set_grid_limit(cap)
+                        sw.set_xcd_chunk(chunk)
+                        payload, exps = sw.quantize_pack(xs, P, W)
+                        sw.loopback_aggregate(payload, W)
+                        out = torch.empty(n + 1, device="cuda")[off:off + n]
+                        sw.dequantize(payload, exps, n, P, W, out=out)
+                        rt = torch.empty(n + 1, device="cuda")[off:off + n]
+                        rt_q = torch.empty_like(payload)
+                        rt_e = torch.empty_like(exps)
+                        sw.roundtrip_loopback(xs, P, W, out=rt, payload=rt_q, exps_out=rt_e)
+                        torch.cuda.synchronize()
+                        tag = (W, off, sl, nt, cap, chunk)
+                        assert np.array_equal(out.cpu().numpy().view(np.uint32), dq.view(np.uint32)), tag
+                        assert np.array_equal(rt.cpu().numpy().view(np.uint32), dq.view(np.uint32)), tag
+                        assert np.array_equal(rt_q.cpu().numpy().view(np.uint32), q), tag
+                        assert np.array_equal(rt_e.cpu().numpy(), e), tag
+    finally:
+        sw.set_stream_tile_slices(0)
+        sw.set_grid_limit(0)
+        sw.set_xcd_chunk(64)
+        sw.set_payload_nt_threshold(orig)
