@@ -392,8 +392,8 @@ sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t num_blocks, uint32_t ba
                           uint32_t* d_imm, void* stream);
 
 /* Measurement probe (not part of the PPP): copy `bytes` (a multiple of 4 KiB,
- * 16-B aligned buffers) with the quantize kernel's tile shape and access
- * policy (non-temporal loads; non-temporal stores from the payload
+ * 16-B aligned buffers) with the quantize kernel's tile shape (K1's slices
+ * per wave tile) and access policy (non-temporal loads; non-temporal stores from the payload
  * non-temporal threshold on, default-policy stores below it — the store
  * policy sml_quantize_pack uses for an output plane of `bytes`) — the
  * practical HBM ceiling bench.py reports. */
@@ -419,8 +419,9 @@ uint32_t sml_set_quantize_tile_slices(uint32_t slices);
 
 /* Tuning knob: slices of 256 elements per wave tile in sml_dequantize (K4)
  * and sml_roundtrip_loopback (the fused round trip; P = 1024 keeps 4): 4 or
- * 2, or 0 = the default.  Results are identical for every
- * size.  Returns the previous value. */
+ * 2 for both, or 0 = by kernel (the default, as measured: K4 2, the round
+ * trip 4).  Results are identical for every size.  Returns
+ * the previous value. */
 uint32_t sml_set_stream_tile_slices(uint32_t slices);
 
 /* Tuning knob: output planes of at least `bytes` bytes are written with

@@ -340,17 +340,18 @@ struct BswapOp {
 // (non-temporal from g_nt_threshold bytes on, default policy below) — no
 // arithmetic: the practical HBM ceiling the quantize kernel is compared
 // against.
-template <bool NTS>
+template <bool NTS, int U>
 __global__ __launch_bounds__(kBlockThreads) void k_stream_copy(const u4* in, u4* out, uint64_t ntiles, uint32_t xcd) {
     struct { uint32_t xcd; } a{xcd};
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    constexpr uint64_t kVecs = tile_elems<U>() / 4;
     for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < ntiles; t += nwaves) {
-        u4 v[kU];
+        u4 v[U];
 #pragma unroll
-        for (int u = 0; u < kU; u++) v[u] = __builtin_nontemporal_load(in + t * (kTileElems / 4) + u * kWave + lane);
+        for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(in + t * kVecs + u * kWave + lane);
 #pragma unroll
-        for (int u = 0; u < kU; u++) store_payload_as<NTS>(out + t * (kTileElems / 4) + u * kWave + lane, v[u]);
+        for (int u = 0; u < U; u++) store_payload_as<NTS>(out + t * kVecs + u * kWave + lane, v[u]);
     }
 }
 
@@ -430,7 +431,8 @@ static std::atomic<uint32_t> g_quant_slices{0};
 static std::atomic<uint64_t> g_nt_threshold{64ull << 20};
 
 // Slices per K4 / fused round-trip tile: 4 or 2 (sml_set_stream_tile_slices;
-// 0 = the measured default below).
+// 0 = by kernel, measured on the bench workload, profiles/r04/ab_stream_slices.json:
+// K4 2, the round trip 4).
 static std::atomic<uint32_t> g_stream_slices{0};
 
 static uint32_t stream_slices(uint32_t dflt) {
@@ -654,7 +656,7 @@ sml_status_t sml_dequantize(const int32_t* d_payload, const int8_t* d_exps, uint
     if (!d_payload || !d_exps || !d_out || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
     if (!aligned16(d_payload)) return SML_ERR_ALIGNMENT;
     DequantArgs a;
-    const uint32_t U = stream_slices(4);
+    const uint32_t U = stream_slices(2);   // measured: 2-slice tiles +0.6 / +2.8 / +3.3 % at 128 / 256 / 512 MiB
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);   // XCD runs keep their byte length
     a.payload = reinterpret_cast<const u4*>(d_payload);
     a.exps = d_exps;
@@ -681,7 +683,9 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
     if (!d_in || !d_out || !aligned4(d_in) || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
     if (d_payload && !aligned16(d_payload)) return SML_ERR_ALIGNMENT;
     RoundTripArgs a;
-    const uint32_t U = packet_numel > 512 ? 4u : stream_slices(4);   // a tile holds whole packets
+    // a tile holds whole packets; 2-slice tiles measured level (+0.7 / -0.2 /
+    // +0.2 % at 128 / 256 / 512 MiB), so 4 stays the default
+    const uint32_t U = packet_numel > 512 ? 4u : stream_slices(4);
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);
     a.in = d_in;
     a.out = d_out;
@@ -750,15 +754,21 @@ sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t B, uint32_t batch_max, 
 sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void* stream) {
     if (bytes == 0) return SML_OK;
     if (!d_in || !d_out || !aligned16(d_in) || !aligned16(d_out) || bytes % (kTileElems * 4)) return SML_ERR_ALIGNMENT;
-    const uint64_t ntiles = bytes / (kTileElems * 4);
-    const uint32_t xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    // K1's tile shape (its slices per tile at P = 256) and store policy for an
+    // output plane of `bytes` (sml_quantize_pack)
+    const uint32_t U = quant_slices(256, true);
+    const uint64_t ntiles = bytes / (256 * U * 4);
+    const uint32_t xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);
     auto in = reinterpret_cast<const u4*>(d_in);
     auto out = reinterpret_cast<u4*>(d_out);
-    // K1's store policy for an output plane of `bytes` (sml_quantize_pack)
-    if (bytes >= g_nt_threshold.load(std::memory_order_relaxed))
-        k_stream_copy<true><<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(in, out, ntiles, xcd);
-    else
-        k_stream_copy<false><<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(in, out, ntiles, xcd);
+    const bool nts = bytes >= g_nt_threshold.load(std::memory_order_relaxed);
+    const dim3 grid(grid_for_tiles(ntiles));
+    hipStream_t st = (hipStream_t)stream;
+#define SML_COPY(U_)                                                                     \
+    if (nts) k_stream_copy<true, U_><<<grid, kBlockThreads, 0, st>>>(in, out, ntiles, xcd); \
+    else k_stream_copy<false, U_><<<grid, kBlockThreads, 0, st>>>(in, out, ntiles, xcd);
+    if (U == 1) { SML_COPY(1) } else if (U == 2) { SML_COPY(2) } else { SML_COPY(4) }
+#undef SML_COPY
     return launch_check();
 }
 
