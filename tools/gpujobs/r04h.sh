@@ -10,5 +10,7 @@ rc=$?; echo "tests rc=$rc"; tail -3 $OUT/tests.log
 case $rc in 0) ;; *) exit $rc;; esac
 timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --no-rccl-collnet > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; case $rc in 0|1) ;; *) exit $rc;; esac
+PROBE_SET=nt timeout -k 10 120 p4app-switchml_amd/bin/hbm_probe 1024 7 > $OUT/hbm_probe_nt_1024MiB.json 2> $OUT/hbm_probe.err
+rc=$?; echo "probe rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac
 timeout -k 10 700 bash profiles/run_profiles.sh r04
 rc=$?; echo "profiles rc=$rc"

@@ -198,6 +198,17 @@ int main(int argc, char** argv) {
         COPY(256, 1, 1, 0, 256);
         READ(256, 4, 1);
         WRITE(256, 4, 0);
+    } else if (set && std::string(set) == "nt") {
+        // round 4: the read-only and write-only rates behind the copy
+        // ceiling, with K1's store policy (non-temporal) and tile shapes
+        COPY(256, 4, 1, 1, 64);
+        COPY(256, 2, 1, 1, 64);
+        COPY(256, 4, 1, 0, 64);
+        READ(256, 4, 1);
+        READ(256, 2, 1);
+        WRITE(256, 4, 1);
+        WRITE(256, 2, 1);
+        WRITE(256, 4, 0);
     } else {
         COPY(256, 4, 1, 0, 64);  // == K1 now
         MULTI(1, 64);
