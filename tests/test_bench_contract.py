@@ -80,3 +80,24 @@ def test_bench_bucket_on_gpu_hashes_to_digest(cuda):
         sw.quantize_pack(x, 256, 1, payload=pl, exps_out=ex)
         torch.cuda.synchronize()
         assert bench.planes_sha256(torch, ex, pl, N, 256) == d["bucket_T1"][b]
+
+
+def test_switch_verdicts_fatal_only_for_switchsim_unless_strict():
+    """bench.py's N > 1 switch checks: a path that ran and gave
+    wrong bits fails the run for switchsim (always) and for the peer-memory
+    paths only with --strict-switch; a path that could not run is
+    diagnostic."""
+    ok = {"verified": True, "within_quantization_bound": True, "timed_calls_equal_first": True}
+    bad = {"verified": False, "within_quantization_bound": True, "timed_calls_equal_first": True,
+           "bit_equal_to_switchsim": False}
+    fields = {"switchsim": ok, "p2p_switch": bad, "xgmi_switch": {"error": "boom"}, "xgmi_switch_push": ok}
+    fatal, diag = bench.switch_verdicts(fields)
+    assert fatal == [] and len(diag) == 2
+    assert any(d.startswith("p2p_switch: not verified") for d in diag)
+    assert any(d.startswith("xgmi_switch: ") and "boom" in d for d in diag)
+    fatal, diag = bench.switch_verdicts(fields, strict=True)
+    assert len(fatal) == 1 and fatal[0].startswith("p2p_switch") and len(diag) == 1
+    fatal, _ = bench.switch_verdicts(dict(fields, switchsim=dict(bad, bit_equal_to_other_paths=False)))
+    assert len(fatal) == 1 and fatal[0].startswith("switchsim")
+    fatal, diag = bench.switch_verdicts({})
+    assert fatal == [] and len(diag) == 4
