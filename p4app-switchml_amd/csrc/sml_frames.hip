@@ -268,7 +268,7 @@ __device__ __forceinline__ bool rx_winner(unsigned long long sw, uint64_t nframe
     return hi != 0u && hi != kRxDone && f < nframes;
 }
 
-template <int P>
+template <int P, bool NT = false>
 __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     __shared__ float lut[256];
     // power-of-two W: the table holds exact reciprocals and dequantize multiplies
@@ -354,7 +354,10 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             const uint64_t off = t * kRxTileElems + 4ull * (u * kWave + lane);
             if (off >= a.numel) continue;
             float* p = a.out + off;
-            if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) *reinterpret_cast<f4*>(p) = o[u];
+            if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) {
+                if constexpr (NT) __builtin_nontemporal_store(o[u], reinterpret_cast<f4*>(p));
+                else *reinterpret_cast<f4*>(p) = o[u];
+            }
             else store4_guarded(p, o[u], 0, a.numel - off);
         }
         // The commit, folded in (it was a third launch): the lane that owns
@@ -390,14 +393,22 @@ static void launch_frames_p(uint32_t P, dim3 grid, hipStream_t st, const FrameAr
     }
 }
 
-static void launch_rx_apply(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
+template <bool NT>
+static void launch_rx_apply_nt(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
     switch (P) {
-        case 64:   k_rx_apply<64><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_rx_apply<128><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_rx_apply<256><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_rx_apply<512><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_rx_apply<1024><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   k_rx_apply<64, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_rx_apply<128, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_rx_apply<256, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_rx_apply<512, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_rx_apply<1024, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
     }
+}
+
+// The fp32 output of a slice from the non-temporal threshold on takes
+// non-temporal stores, as K4's does (sml_set_payload_nt_threshold).
+static void launch_rx_apply(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
+    if (4 * a.numel >= g_nt_threshold.load(std::memory_order_relaxed)) launch_rx_apply_nt<true>(P, grid, st, a);
+    else launch_rx_apply_nt<false>(P, grid, st, a);
 }
 
 }  // namespace sml

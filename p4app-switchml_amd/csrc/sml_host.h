@@ -20,6 +20,7 @@ namespace sml {
 extern thread_local char g_last_error[256];
 extern std::atomic<uint32_t> g_grid_limit;
 extern std::atomic<uint32_t> g_xcd_chunk;
+extern std::atomic<uint64_t> g_nt_threshold;   // output planes from this size on: non-temporal stores
 
 inline sml_status_t hip_check(hipError_t err) {
     if (err == hipSuccess) return SML_OK;

@@ -428,7 +428,7 @@ static std::atomic<uint32_t> g_quant_slices{0};
 // quarter of the Infinity Cache on stream non-temporally; smaller ones (a
 // framework's 25 MiB gradient buckets) keep the default policy, so their
 // next reader can find them in the cache.  Bytes are identical either way.
-static std::atomic<uint64_t> g_nt_threshold{64ull << 20};
+std::atomic<uint64_t> g_nt_threshold{64ull << 20};
 
 // Slices per K4 / fused round-trip tile: 4 or 2 (sml_set_stream_tile_slices;
 // 0 = by kernel, measured on the bench workload, profiles/r04/ab_stream_slices.json:

@@ -204,12 +204,20 @@ def test_frames_tx_rx_round_trip_equals_fused_loopback(cuda, W):
     v = (v.view(torch.uint8).view(F, P, 4).flip(-1).contiguous().view(torch.int32) * W)   # ntohl, x W (wraps)
     v = v.view(torch.uint8).view(F, P, 4).flip(-1).contiguous().view(F, 4 * P)           # htonl
     fr.view(F, stride)[:, 52:52 + 4 * P] = v
-    rx = sw.RxSlice(n, P, bm, device=dev)
-    sw.dequantize_frames(fr, F, rx, num_workers=W, job_id=4)
     ref = sw.roundtrip_loopback(x, P, W)
-    torch.cuda.synchronize()
-    assert torch.equal(rx.out.view(torch.int32), ref.view(torch.int32))
-    assert rx.counts.tolist() == [F, 0]
+    # both output store policies of the apply pass (non-temporal from the
+    # threshold on — 0 here — or default): the same bytes
+    orig = sw.set_payload_nt_threshold(0)
+    try:
+        for thr in (0, 2 ** 64 - 1):
+            sw.set_payload_nt_threshold(thr)
+            rx = sw.RxSlice(n, P, bm, device=dev)
+            sw.dequantize_frames(fr, F, rx, num_workers=W, job_id=4)
+            torch.cuda.synchronize()
+            assert torch.equal(rx.out.view(torch.int32), ref.view(torch.int32)), thr
+            assert rx.counts.tolist() == [F, 0]
+    finally:
+        sw.set_payload_nt_threshold(orig)
 
 
 # ------------------------------------------------------ randomized (GPU) --
