@@ -80,3 +80,19 @@ def test_installed_rccl_has_no_collnet_allreduce_device_code():
         assert rep["device_functions"] > 100, lib
         assert "RING" in rep["allreduce_algorithms_with_device_code"], lib
         assert rep["collnet_allreduce_device_functions"] == [], lib
+
+
+def test_same_gpu_rccl_env():
+    """W ranks sharing one GPU under RCCL (tests/test_switch_rccl_gpu.py, the
+    bench rehearsal): a distinct NCCL_HOSTID per rank, and a net between them
+    — this library's TCP net or RCCL's socket net on the loopback."""
+    sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
+    from switchml_amd import rccl_collnet as R
+    a, b = R.same_gpu_rccl_env(0, "s"), R.same_gpu_rccl_env(1, "s")
+    assert a["NCCL_HOSTID"] != b["NCCL_HOSTID"]
+    assert a["NCCL_NET_PLUGIN"].endswith("librccl-net-switchml.so") and "NCCL_COLLNET_ENABLE" not in a
+    s = R.same_gpu_rccl_env(1, "s", net="socket")
+    assert s["NCCL_NET"] == "Socket" and s["NCCL_SOCKET_IFNAME"] == "lo" and s["NCCL_NET_PLUGIN"] == "none"
+    assert all(e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" for e in (a, b, s))
+    with pytest.raises(ValueError):
+        R.same_gpu_rccl_env(0, "s", net="ib")
