@@ -8,6 +8,10 @@
 // and parity notes: sml_device.h; DPDK frames: sml_frames.hip.
 #include "sml_host.h"
 
+#ifndef SML_LUT_EARLY
+#define SML_LUT_EARLY 0
+#endif
+
 namespace sml {
 
 thread_local char g_last_error[256] = "";
@@ -94,9 +98,28 @@ __device__ __forceinline__ void quant_tile(const QuantArgs& a, uint64_t base, in
 template <int P, bool ALIGNED, bool GLOBAL, bool BE, bool RNE, int U, bool NTS = false>
 __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
     __shared__ float lut[256];
-    if (a.payload) build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+#if SML_LUT_EARLY
+    // The wave's first tile is loaded BEFORE the workgroup builds its scale
+    // table: the table and its barrier run while the loads are in flight (a
+    // plain s_barrier does not wait for them), instead of delaying the first
+    // HBM request of every workgroup of the one-shot grid.
+    uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
+    f4 v[U];
+    if (t < a.ntiles) load_tile<ALIGNED>(a, t * tile_elems<U>(), lane, v);
+    if (a.payload) build_lut(lut, a.W);
+    while (t < a.ntiles) {
+        const uint64_t base = t * tile_elems<U>();
+        int e[U];
+        // K3: the exponent dword is read after the data loads are in flight
+        if constexpr (GLOBAL) global_tile_exponents<P>(a, base, lane, e);
+        quant_tile<P, GLOBAL, BE, RNE, U, NTS>(a, base, lane, v, lut, e);
+        t += nwaves;
+        if (t < a.ntiles) load_tile<ALIGNED>(a, t * tile_elems<U>(), lane, v);
+    }
+#else
+    if (a.payload) build_lut(lut, a.W);
     for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
         const uint64_t base = t * tile_elems<U>();
         f4 v[U];
@@ -107,6 +130,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_quantize_pack(QuantArgs a) {
         if constexpr (GLOBAL) global_tile_exponents<P>(a, base, lane, e);
         quant_tile<P, GLOBAL, BE, RNE, U, NTS>(a, base, lane, v, lut, e);
     }
+#endif
 }
 
 // ntohl (BE) -> int -> float, divided by the scale (or multiplied by its
