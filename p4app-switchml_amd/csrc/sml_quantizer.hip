@@ -8,9 +8,6 @@
 // and parity notes: sml_device.h; DPDK frames: sml_frames.hip.
 #include "sml_host.h"
 
-#ifndef SML_LUT_EARLY2
-#define SML_LUT_EARLY2 1
-#endif
 
 namespace sml {
 
@@ -152,30 +149,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_dequantize(DequantArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     constexpr int kElems = tile_elems<U>();
     uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
-#if SML_LUT_EARLY2
-    // As K1: a full first tile's payload words are requested before the
-    // workgroup builds its scale table (the s_barrier does not wait for them).
-    if (t < a.ntiles && t * kElems + kElems <= a.numel && slice_exps_scalar_ok<P>(a.exps)) {
-        const uint64_t base = t * kElems;
-        u4 w[U];
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            w[u] = __builtin_nontemporal_load(a.payload + (base + (uint64_t)(u * kWave + lane) * 4) / 4);
-        if constexpr (RCP) build_rcp_lut(lut, a.W);
-        else build_lut(lut, a.W);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
-            const float s = lut[slice_exponent_byte<P>(a.exps, base, u, lane)];
-            store4<ALIGNED, NT>(a.out + idx, dequant_words<BE, RCP>(w[u], s));
-        }
-        t += nwaves;
-    } else
-#endif
-    {
-        if constexpr (RCP) build_rcp_lut(lut, a.W);
-        else build_lut(lut, a.W);
-    }
+    if constexpr (RCP) build_rcp_lut(lut, a.W);
+    else build_lut(lut, a.W);
     for (; t < a.ntiles; t += nwaves) {
         const uint64_t base = t * kElems;
         const bool full = base + kElems <= a.numel;
@@ -317,8 +292,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
-#if SML_LUT_EARLY2
-    // As K1: the first tile's loads go out before the scale table is built.
+    // As K1: the first tile's loads go out before the scale table is built
+    // (measured level here, +0.1-0.3 %: profiles/r04/ab_lut_early2.json).
     f4 v[U];
     if (t < a.ntiles) roundtrip_load<ALIGNED, U>(a, t, lane, v);
     build_lut(lut, a.W);
@@ -327,10 +302,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip(RoundTripArgs a) {
         t += nwaves;
         if (t < a.ntiles) roundtrip_load<ALIGNED, U>(a, t, lane, v);
     }
-#else
-    build_lut(lut, a.W);
-    for (; t < a.ntiles; t += nwaves) roundtrip_tile<P, ALIGNED, BE, RNE, NT, U>(a, t, lut, lane);
-#endif
 }
 
 // The fused round trip over a batch of slices (of one or several jobs) in ONE
