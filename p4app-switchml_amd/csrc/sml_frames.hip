@@ -75,7 +75,6 @@ template <int P, bool ALIGNED, bool GLOBAL>
 __global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(kBlockThreads)
 void k_quantize_frames(FrameArgs a) {
     __shared__ float lut[256];
-    build_lut(lut, a.W);
     const int lane = threadIdx.x & (kWave - 1);
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t padded = a.nblocks * P;
@@ -87,14 +86,18 @@ void k_quantize_frames(FrameArgs a) {
 #pragma unroll
     for (int i = 1; i < 11; i++) hconst = hd == i ? a.hdr[i] : hconst;
     const uint32_t m2 = 2u * a.mop;
-    for (uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index(); t < a.ntiles; t += nwaves) {
+    QuantArgs qa;                                          // reuse the K1 tile loader
+    qa.in = a.in;
+    qa.numel = a.numel;
+    // As K1: the first tile's loads go out before the scale table is built.
+    uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
+    f4 v[kU];
+    if (t < a.ntiles) load_tile<ALIGNED>(qa, t * kTileElems, lane, v);
+    build_lut(lut, a.W);
+    for (bool first = true; t < a.ntiles; t += nwaves, first = false) {
         const uint64_t base = t * kTileElems;
         const uint64_t pk0 = base / P;                     // first block of the tile
-        QuantArgs qa;                                      // reuse the K1 tile loader
-        qa.in = a.in;
-        qa.numel = a.numel;
-        f4 v[kU];
-        load_tile<ALIGNED>(qa, base, lane, v);
+        if (!first) load_tile<ALIGNED>(qa, base, lane, v); // later tiles (grid-stride)
         int eloc[kU];
         tile_exponents<P>(v, eloc);
         // exponent of packet j of the tile: slice j*P/256, lane (j*P/4) % 64
