@@ -5,6 +5,10 @@
 // with PostprocessSingle per accepted frame), and their C-ABI entry points.
 #include "sml_host.h"
 
+#ifndef SML_FRAMES_NT
+#define SML_FRAMES_NT 0
+#endif
+
 namespace sml {
 
 // ---------------------------------------------------------- DPDK frames
@@ -118,14 +122,24 @@ void k_quantize_frames(FrameArgs a) {
             if (lane < 48) {
                 if (j < kPk && pk0 + j < a.nblocks) {
                     const uint64_t f = pk0 + j + a.b;
+#if SML_FRAMES_NT >= 2
+                    __builtin_nontemporal_store(hd == 11 ? (uint32_t)f : hconst,
+                                                reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 4 * hd));
+#else
                     *reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 4 * hd) = hd == 11 ? (uint32_t)f : hconst;
+#endif
                 }
             } else if (lane < 52 && !extra) {
                 if (j < kPk && pk0 + j < a.nblocks) {
                     uint32_t e = 0;
 #pragma unroll
                     for (int jj = 0; jj < kPk; jj++) e = j == jj ? ej[jj] : e;
+#if SML_FRAMES_NT >= 2
+                    __builtin_nontemporal_store(pool_dword(a, (r + (uint32_t)j) % m2, e),
+                                                reinterpret_cast<uint32_t*>(a.frames + (pk0 + j) * a.stride + 48));
+#else
                     *reinterpret_cast<uint32_t*>(a.frames + (pk0 + j) * a.stride + 48) = pool_dword(a, (r + (uint32_t)j) % m2, e);
+#endif
                 }
             }
         }
@@ -163,7 +177,11 @@ void k_quantize_frames(FrameArgs a) {
             if constexpr (GLOBAL) e = a.gexp[k];
             const u4 q = quantize4<false>(v[u], lut[(uint8_t)e], idx, 0);
             uint32_t* dst = reinterpret_cast<uint32_t*>(a.frames + (k + a.b) * a.stride + 52) + (idx - k * P);
+#if SML_FRAMES_NT >= 1
+            __builtin_nontemporal_store(u4a{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)}, reinterpret_cast<u4a*>(dst));
+#else
             *reinterpret_cast<u4a*>(dst) = u4a{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)};
+#endif
         }
     }
 }
