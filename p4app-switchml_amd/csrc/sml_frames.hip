@@ -5,10 +5,6 @@
 // with PostprocessSingle per accepted frame), and their C-ABI entry points.
 #include "sml_host.h"
 
-#ifndef SML_FRAMES_NT
-#define SML_FRAMES_NT 0
-#endif
-
 namespace sml {
 
 // ---------------------------------------------------------- DPDK frames
@@ -75,7 +71,12 @@ __device__ __forceinline__ uint32_t pool_dword(const FrameArgs& a, uint32_t i, u
 // caps it at 7; at 8 (a few SGPRs live in VGPR lanes, no scratch) the
 // 256 MiB bucket's frames take 4 % less time (profiles/r02c/ab_frames_occupancy.json).
 // The rx apply pass measured 1.6 % slower the same way and is left alone.
-template <int P, bool ALIGNED, bool GLOBAL>
+// NTS: the payload words take non-temporal stores (frames in device memory
+// from the non-temporal threshold on).  Measured on cold frame sets (4
+// cycled, 256 MiB bucket, profiles/r04/ab_frames_nt.json): 98.1 -> 86.4 us;
+// non-temporal header dwords as well: 109.6 us (partial-line stores), so
+// headers keep the default policy.
+template <int P, bool ALIGNED, bool GLOBAL, bool NTS = false>
 __global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(kBlockThreads)
 void k_quantize_frames(FrameArgs a) {
     __shared__ float lut[256];
@@ -122,24 +123,14 @@ void k_quantize_frames(FrameArgs a) {
             if (lane < 48) {
                 if (j < kPk && pk0 + j < a.nblocks) {
                     const uint64_t f = pk0 + j + a.b;
-#if SML_FRAMES_NT >= 2
-                    __builtin_nontemporal_store(hd == 11 ? (uint32_t)f : hconst,
-                                                reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 4 * hd));
-#else
                     *reinterpret_cast<uint32_t*>(a.frames + f * a.stride + 4 * hd) = hd == 11 ? (uint32_t)f : hconst;
-#endif
                 }
             } else if (lane < 52 && !extra) {
                 if (j < kPk && pk0 + j < a.nblocks) {
                     uint32_t e = 0;
 #pragma unroll
                     for (int jj = 0; jj < kPk; jj++) e = j == jj ? ej[jj] : e;
-#if SML_FRAMES_NT >= 2
-                    __builtin_nontemporal_store(pool_dword(a, (r + (uint32_t)j) % m2, e),
-                                                reinterpret_cast<uint32_t*>(a.frames + (pk0 + j) * a.stride + 48));
-#else
                     *reinterpret_cast<uint32_t*>(a.frames + (pk0 + j) * a.stride + 48) = pool_dword(a, (r + (uint32_t)j) % m2, e);
-#endif
                 }
             }
         }
@@ -177,11 +168,9 @@ void k_quantize_frames(FrameArgs a) {
             if constexpr (GLOBAL) e = a.gexp[k];
             const u4 q = quantize4<false>(v[u], lut[(uint8_t)e], idx, 0);
             uint32_t* dst = reinterpret_cast<uint32_t*>(a.frames + (k + a.b) * a.stride + 52) + (idx - k * P);
-#if SML_FRAMES_NT >= 1
-            __builtin_nontemporal_store(u4a{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)}, reinterpret_cast<u4a*>(dst));
-#else
-            *reinterpret_cast<u4a*>(dst) = u4a{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)};
-#endif
+            const u4a wq{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)};
+            if constexpr (NTS) __builtin_nontemporal_store(wq, reinterpret_cast<u4a*>(dst));
+            else *reinterpret_cast<u4a*>(dst) = wq;
         }
     }
 }
@@ -404,14 +393,18 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
 // ------------------------------------------------------------ host side
 
 template <bool ALIGNED, bool GLOBAL>
-static void launch_frames_p(uint32_t P, dim3 grid, hipStream_t st, const FrameArgs& a) {
+static void launch_frames_p(uint32_t P, bool nts, dim3 grid, hipStream_t st, const FrameArgs& a) {
+#define SML_FR(PN)                                                                                   \
+    if (nts) k_quantize_frames<PN, ALIGNED, GLOBAL, true><<<grid, kBlockThreads, 0, st>>>(a);        \
+    else k_quantize_frames<PN, ALIGNED, GLOBAL, false><<<grid, kBlockThreads, 0, st>>>(a);
     switch (P) {
-        case 64:   k_quantize_frames<64, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_quantize_frames<128, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_quantize_frames<256, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_quantize_frames<512, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_quantize_frames<1024, ALIGNED, GLOBAL><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   SML_FR(64) break;
+        case 128:  SML_FR(128) break;
+        case 256:  SML_FR(256) break;
+        case 512:  SML_FR(512) break;
+        default:   SML_FR(1024) break;
     }
+#undef SML_FR
 }
 
 template <bool NT>
@@ -492,8 +485,21 @@ sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_
     dim3 grid(grid_for_tiles(a.ntiles));
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_in);
-    if (d_global_exps) { if (al) launch_frames_p<true, true>(P, grid, st, a); else launch_frames_p<false, true>(P, grid, st, a); }
-    else               { if (al) launch_frames_p<true, false>(P, grid, st, a); else launch_frames_p<false, false>(P, grid, st, a); }
+    // payload store policy: non-temporal for a frame set in device memory from
+    // the threshold on (written once, handed on); host frames (a NIC's pinned
+    // mbufs) keep the default policy
+    bool nts = (a.nblocks + a.b) * stride >= g_nt_threshold.load(std::memory_order_relaxed);
+    if (nts) {
+        hipPointerAttribute_t pa;
+        if (hipPointerGetAttributes(&pa, frames) != hipSuccess) {
+            (void)hipGetLastError();
+            nts = false;
+        } else {
+            nts = pa.type == hipMemoryTypeDevice;
+        }
+    }
+    if (d_global_exps) { if (al) launch_frames_p<true, true>(P, nts, grid, st, a); else launch_frames_p<false, true>(P, nts, grid, st, a); }
+    else               { if (al) launch_frames_p<true, false>(P, nts, grid, st, a); else launch_frames_p<false, false>(P, nts, grid, st, a); }
     return launch_check();
 }
 

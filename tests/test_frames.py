@@ -80,7 +80,20 @@ def test_pool_index_alternates_shadow_pools():
 @pytest.mark.parametrize("P", [64, 256, 1024])
 @pytest.mark.parametrize("n", [1, 300, 50_003])
 @pytest.mark.parametrize("where", ["device", "pinned"])
-def test_frames_match_oracle(cuda, P, n, where):
+@pytest.mark.parametrize("nt", [False, True])
+def test_frames_match_oracle(cuda, P, n, where, nt):
+    """nt: the non-temporal payload-store policy (device frame sets from the
+    threshold on; threshold 0 here) — the same bytes."""
+    import torch
+    import switchml_amd as sw
+    orig = sw.set_payload_nt_threshold(0 if nt else 2 ** 64 - 1)
+    try:
+        _frames_match_oracle(cuda, P, n, where)
+    finally:
+        sw.set_payload_nt_threshold(orig)
+
+
+def _frames_match_oracle(cuda, P, n, where):
     import torch
     import switchml_amd as sw
     W, bm = 3, 16
