@@ -1069,6 +1069,27 @@ def extra_measurements(sw, torch, x, P, stream, reps=20):
         t = timeit(rx_once)
     res["frames_rx_device_GBps"] = round((4 * N + fbytes) / t / 1e9, 1)
     del frames, rx
+    # the same two calls cycling 4 frame sets (and rx outputs): a stream of
+    # received frames, past the Infinity Cache, as the headline cycles buckets
+    fsets = [torch.empty(fbytes, dtype=torch.uint8, device=x.device) for _ in range(4)]
+    rxs = [sw.RxSlice(N, P, 64, device=x.device) for _ in range(4)]
+    k = [0]
+
+    def tx_cycle():
+        sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=fsets[k[0] % 4], stream=stream)
+        k[0] += 1
+
+    def rx_cycle():
+        r = rxs[k[0] % 4]
+        r.reset(stream)
+        sw.dequantize_frames(fsets[k[0] % 4], fbytes // sw.frame_bytes(P), r, num_workers=1, stream=stream)
+        k[0] += 1
+    t = timeit(tx_cycle)
+    res["frames_device_4sets_GBps"] = round((4 * N + fbytes) / t / 1e9, 1)
+    with torch.cuda.stream(stream):
+        t = timeit(rx_cycle)
+    res["frames_rx_device_4sets_GBps"] = round((4 * N + fbytes) / t / 1e9, 1)
+    del fsets, rxs
     hframes = torch.empty(fbytes, dtype=torch.uint8).pin_memory()
     t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=hframes, stream=stream))
     res["frames_to_pinned_host_input_GBps"] = round(4 * N / t / 1e9, 2)
