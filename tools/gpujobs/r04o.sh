@@ -12,3 +12,5 @@ case $rc in 0) ;; *) exit $rc;; esac
 timeout -k 10 900 python -u bench.py --steps 20 --warmup 5 --extra --no-cpu-baseline --no-rccl-collnet \
   > $OUT/bench_extra.json 2> $OUT/bench_extra.err
 rc=$?; echo "bench extra rc=$rc"
+PROBE_SET=cpol timeout -k 10 120 p4app-switchml_amd/bin/hbm_probe 1024 7 > $OUT/hbm_probe_cpol_1024MiB.json 2> $OUT/hbm_probe_cpol.err
+echo "probe rc=$?"

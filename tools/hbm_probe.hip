@@ -148,6 +148,40 @@ __global__ __launch_bounds__(WG) void k_write(u4* __restrict__ out) {
     }
 }
 
+// Round 4: explicit cache-policy bits on buffer loads / stores (aux: 1 sc0,
+// 2 nt, 16 sc1; __builtin_nontemporal_* emit nt alone).  One descriptor per
+// workgroup over its own 16 KiB (WG 256 x U 4), so offsets stay 32-bit.
+template <int LAUX, int SAUX>
+__global__ __launch_bounds__(256) void k_copy_cp(const u4* __restrict__ in, u4* __restrict__ out) {
+    const unsigned long long r = blockIdx.x / 8, C = 64, span = 8 * C;
+    unsigned long long b = blockIdx.x;
+    if (b < gridDim.x / span * span) b = (r / C) * span + (b % 8) * C + r % C;
+    const unsigned long long wgb = b * 1024ull;   // u4 index of this workgroup's 16 KiB
+    __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void*)(in + wgb), 0, 16384, 0x00020000);
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)(out + wgb), 0, 16384, 0x00020000);
+    const int off = ((threadIdx.x / 64) * 256 + (threadIdx.x % 64)) * 16;
+    u4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) v[u] = __builtin_amdgcn_raw_buffer_load_b128(ri, off + 1024 * u, 0, LAUX);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        v[u].x ^= 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(v[u], ro, off + 1024 * u, 0, SAUX);
+    }
+}
+
+template <int SAUX>
+__global__ __launch_bounds__(256) void k_write_cp(u4* __restrict__ out) {
+    const unsigned long long wgb = blockIdx.x * 1024ull;
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)(out + wgb), 0, 16384, 0x00020000);
+    const int off = ((threadIdx.x / 64) * 256 + (threadIdx.x % 64)) * 16;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        u4 v = {(unsigned)wgb, (unsigned)u, 1u, 2u};
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, off + 1024 * u, 0, SAUX);
+    }
+}
+
 struct Variant {
     std::string name;
     double bytes_per_vec;   // bytes moved per 16-B vector of the buffer
@@ -182,6 +216,10 @@ int main(int argc, char** argv) {
     [=](hipStream_t s) { unsigned long long g = nvec / (WG * U); k_write<WG, U, SN><<<g, WG, 0, s>>>(out); }, {}})
 #define MULTI(IT, C) vs.push_back({"copy multi iter" #IT " xcd" #C, 32.0, \
     [=](hipStream_t s) { k_copy_multi<IT, C><<<nvec / (1024 * IT), 256, 0, s>>>(in, out); }, {}})
+#define COPYCP(L, S) vs.push_back({"copy cpol load" #L " store" #S, 32.0, \
+    [=](hipStream_t s) { k_copy_cp<L, S><<<nvec / 1024, 256, 0, s>>>(in, out); }, {}})
+#define WRITECP(S) vs.push_back({"write cpol store" #S, 16.0, \
+    [=](hipStream_t s) { k_write_cp<S><<<nvec / 1024, 256, 0, s>>>(out); }, {}})
     const char* set = getenv("PROBE_SET");
     if (set && std::string(set) == "tiles") {
         // tile size (U f4 per lane) x workgroup size x XCD run length
@@ -209,6 +247,30 @@ int main(int argc, char** argv) {
         WRITE(256, 4, 1);
         WRITE(256, 2, 1);
         WRITE(256, 4, 0);
+    } else if (set && std::string(set) == "cpol") {
+        // round 4: store (and load) cache-policy bits beyond nt; aux 1 sc0,
+        // 2 nt, 16 sc1
+        COPY(256, 4, 1, 1, 64);   // K1's policy through global_* (reference row)
+        COPYCP(2, 2);
+        COPYCP(2, 0);
+        COPYCP(2, 1);
+        COPYCP(2, 3);
+        COPYCP(2, 16);
+        COPYCP(2, 17);
+        COPYCP(2, 18);
+        COPYCP(2, 19);
+        COPYCP(0, 2);
+        COPYCP(19, 2);
+        COPYCP(3, 2);
+        WRITE(256, 4, 1);
+        WRITECP(2);
+        WRITECP(0);
+        WRITECP(1);
+        WRITECP(3);
+        WRITECP(16);
+        WRITECP(17);
+        WRITECP(18);
+        WRITECP(19);
     } else {
         COPY(256, 4, 1, 0, 64);  // == K1 now
         MULTI(1, 64);
