@@ -160,15 +160,40 @@ __device__ __forceinline__ f4 load4_guarded(const float* p, uint64_t idx, uint64
     return v;
 }
 
+// The non-temporal 16-byte store of every streaming kernel's large-output
+// path (planes and fp32 outputs from g_nt_threshold on).  Aligned
+// destinations take `sc1 nt` (device coherence scope, streaming): on cold
+// buckets K1 -1.3 %, K4 -2.4 %, the round trip -1.4 % time against plain nt
+// (profiles/r04/ab_cpol.json; `sc0 sc1 nt` is level with `sc1 nt`).  The
+// compiler has no builtin for these bits, hence the asm: a plain vector store
+// (operands in VGPRs; the "memory" clobber keeps it ordered).  Frame payloads
+// sit at byte 52 of a frame, unaligned: there `sc1` halves the rate (86.7 ->
+// 183 us per 256 MiB frame set, ab_frames_cpol.json) and plain nt stays.
+// SML_NT_CPOL=0 builds plain nt everywhere (A/B builds only).
+#ifndef SML_NT_CPOL
+#define SML_NT_CPOL 2
+#endif
+#if SML_NT_CPOL == 0
+#define SML_NT_STORE16(v, p) __builtin_nontemporal_store((v), (p))
+#else
+template <typename V>
+__device__ __forceinline__ void nt_store16_sc1(V v, void* p) {
+    static_assert(sizeof(V) == 16, "16-byte stores only");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+#define SML_NT_STORE16(v, p) nt_store16_sc1((v), (void*)(p))
+#endif
+#define SML_NT_STORE16_UNALIGNED(v, p) __builtin_nontemporal_store((v), (p))
+
 // NT: non-temporal (for output planes larger than the Infinity Cache: see
 // g_nt_threshold in sml_quantizer.hip); default policy otherwise.
 template <bool ALIGNED, bool NT = false>
 __device__ __forceinline__ void store4(float* p, f4 v) {
     if constexpr (ALIGNED) {
-        if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p));
+        if constexpr (NT) SML_NT_STORE16(v, reinterpret_cast<f4*>(p));
         else *reinterpret_cast<f4*>(p) = v;   // default policy: faster than nt stores up to 256 MiB
     } else {
-        if constexpr (NT) __builtin_nontemporal_store(f4a{v.x, v.y, v.z, v.w}, reinterpret_cast<f4a*>(p));
+        if constexpr (NT) SML_NT_STORE16_UNALIGNED((f4a{v.x, v.y, v.z, v.w}), reinterpret_cast<f4a*>(p));
         else *reinterpret_cast<f4a*>(p) = f4a{v.x, v.y, v.z, v.w};
     }
 }
@@ -189,7 +214,7 @@ __device__ __forceinline__ void store_payload(u4* dst, u4 q) { *dst = q; }
 // plane size (sml_set_payload_nt_threshold).
 template <bool NT>
 __device__ __forceinline__ void store_payload_as(u4* dst, u4 q) {
-    if constexpr (NT) __builtin_nontemporal_store(q, dst);
+    if constexpr (NT) SML_NT_STORE16(q, dst);
     else *dst = q;
 }
 

@@ -169,7 +169,7 @@ void k_quantize_frames(FrameArgs a) {
             const u4 q = quantize4<false>(v[u], lut[(uint8_t)e], idx, 0);
             uint32_t* dst = reinterpret_cast<uint32_t*>(a.frames + (k + a.b) * a.stride + 52) + (idx - k * P);
             const u4a wq{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)};
-            if constexpr (NTS) __builtin_nontemporal_store(wq, reinterpret_cast<u4a*>(dst));
+            if constexpr (NTS) SML_NT_STORE16_UNALIGNED(wq, reinterpret_cast<u4a*>(dst));
             else *reinterpret_cast<u4a*>(dst) = wq;
         }
     }
@@ -365,7 +365,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             if (off >= a.numel) continue;
             float* p = a.out + off;
             if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) {
-                if constexpr (NT) __builtin_nontemporal_store(o[u], reinterpret_cast<f4*>(p));
+                if constexpr (NT) SML_NT_STORE16(o[u], reinterpret_cast<f4*>(p));
                 else *reinterpret_cast<f4*>(p) = o[u];
             }
             else store4_guarded(p, o[u], 0, a.numel - off);
