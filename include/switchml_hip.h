@@ -427,7 +427,9 @@ uint32_t sml_set_stream_tile_slices(uint32_t slices);
 /* Tuning knob: output planes of at least `bytes` bytes are written with
  * non-temporal stores — the payload plane of sml_quantize_pack (K1/K3), the
  * fp32 output of sml_dequantize (K4), sml_roundtrip_loopback and
- * sml_roundtrip_loopback_batch (by the batch's total output) and the
+ * sml_roundtrip_loopback_batch (by the batch's total output), the fp32
+ * output of sml_dequantize_frames, the payloads of a device-memory frame set
+ * of sml_quantize_pack_frames (host frame sets keep default stores) and the
  * sml_stream_copy probe; default 64 MiB, a quarter of the 256 MiB Infinity
  * Cache — DESIGN.md §4); UINT64_MAX = never, 0 = always.
  * Results are identical either way.  Returns the previous value. */
