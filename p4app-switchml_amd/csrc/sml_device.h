@@ -161,27 +161,34 @@ __device__ __forceinline__ f4 load4_guarded(const float* p, uint64_t idx, uint64
 }
 
 // The non-temporal 16-byte store of every streaming kernel's large-output
-// path (planes and fp32 outputs from g_nt_threshold on).  Aligned
-// destinations take `sc1 nt` (device coherence scope, streaming): on cold
-// buckets K1 -1.3 %, K4 -2.4 %, the round trip -1.4 % time against plain nt
-// (profiles/r04/ab_cpol.json; `sc0 sc1 nt` is level with `sc1 nt`).  The
-// compiler has no builtin for these bits, hence the asm: a plain vector store
-// (operands in VGPRs; the "memory" clobber keeps it ordered).  Frame payloads
-// sit at byte 52 of a frame, unaligned: there `sc1` halves the rate (86.7 ->
-// 183 us per 256 MiB frame set, ab_frames_cpol.json) and plain nt stays.
-// SML_NT_CPOL=0 builds plain nt everywhere (A/B builds only).
+// path (planes and fp32 outputs from g_nt_threshold on): `nt`
+// (__builtin_nontemporal_store).  SML_NT_CPOL=3 (A/B builds only) writes
+// `sc1 nt` through a buffer store the compiler sees — a per-store descriptor
+// based 1 GiB below the first active lane's address (every lane of a wave
+// stores within a few KiB of it), the lane's byte offset from that base.  An
+// inline-asm store must not be used for this: the compiler's hazard
+// recognizer cannot see into it and let a VALU overwrite the store's address
+// and data VGPRs in the next cycles.
 #ifndef SML_NT_CPOL
-#define SML_NT_CPOL 2
+#define SML_NT_CPOL 0
 #endif
-#if SML_NT_CPOL == 0
-#define SML_NT_STORE16(v, p) __builtin_nontemporal_store((v), (p))
-#else
+#if SML_NT_CPOL == 3
 template <typename V>
 __device__ __forceinline__ void nt_store16_sc1(V v, void* p) {
     static_assert(sizeof(V) == 16, "16-byte stores only");
-    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+    typedef uint32_t w4 __attribute__((ext_vector_type(4)));
+    const uint64_t a = reinterpret_cast<uint64_t>(p);
+    const uint64_t f = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
+                       __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint64_t base = f - (1ull << 30);
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(w4, v), r, (int)(uint32_t)(a - base), 0,
+                                           18 /* sc1 nt */);
 }
 #define SML_NT_STORE16(v, p) nt_store16_sc1((v), (void*)(p))
+#else
+#define SML_NT_STORE16(v, p) __builtin_nontemporal_store((v), (p))
 #endif
 #define SML_NT_STORE16_UNALIGNED(v, p) __builtin_nontemporal_store((v), (p))
 
@@ -419,8 +426,21 @@ struct QuantArgs {
 template <bool ALIGNED, int U>
 __device__ __forceinline__ void load_tile(const QuantArgs& a, uint64_t base, int lane, f4 (&v)[U]) {
     if (base + tile_elems<U>() <= a.numel) {
+#ifdef SML_LOAD_CPOL
+        // A/B builds only: buffer loads with explicit cache-policy bits
+        const uint64_t tb = reinterpret_cast<uint64_t>(a.in + base);
+        const uint64_t ub = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32)) << 32) |
+                            __builtin_amdgcn_readfirstlane((uint32_t)tb);
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ub), 0, tile_elems<U>() * 4, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (u * kWave + lane) * 16, 0,
+                                                                                 SML_LOAD_CPOL));
+#else
 #pragma unroll
         for (int u = 0; u < U; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
+#endif
     } else {
 #pragma unroll
         for (int u = 0; u < U; u++) {
