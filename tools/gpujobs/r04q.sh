@@ -1,5 +1,5 @@
-# round 4, job q: final kernels with `sc1 nt` stores on aligned large outputs
-# (K1 / K4 / round trip / copy / rx apply) — whole GPU suite, smoke, the driver's N=1 command, rocprofv3 evidence.
+# round 4, job q: final kernels (plain nt stores again) — whole GPU suite, smoke, the driver's N=1 command, rocprofv3 evidence; then
+# the A/B of `sc1 nt` through buffer stores (SML_NT_CPOL=3) vs plain nt.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 OUT=$GRAFT_REPO_ROOT/gpurun_out/r04q
@@ -13,4 +13,7 @@ case $rc in 0) ;; *) exit $rc;; esac
 timeout -k 10 600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; case $rc in 0|1) ;; *) exit $rc;; esac
 timeout -k 10 700 bash profiles/run_profiles.sh r04
-rc=$?; echo "profiles rc=$rc"
+rc=$?; echo "profiles rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac
+AB=p4app-switchml_amd/bin/ab
+AB_KINDS=K1,K4,RT timeout -k 10 400 python -u tools/ab_libs_cold.py $AB/cpol0.so $AB/cpol3.so > $OUT/ab_cpol_buffer.json 2> $OUT/ab_cpol_buffer.err
+echo "ab cpol buffer rc=$?"
