@@ -172,14 +172,21 @@ __device__ __forceinline__ f4 load4_guarded(const float* p, uint64_t idx, uint64
 #ifndef SML_NT_CPOL
 #define SML_NT_CPOL 0
 #endif
+// The first active lane's 64-bit value, in SGPRs.  readfirstlane returns a
+// signed int: each half goes through uint32_t before it is widened (a sign-
+// extended low half corrupts the high one).
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
 #if SML_NT_CPOL == 3
 template <typename V>
 __device__ __forceinline__ void nt_store16_sc1(V v, void* p) {
     static_assert(sizeof(V) == 16, "16-byte stores only");
     typedef uint32_t w4 __attribute__((ext_vector_type(4)));
     const uint64_t a = reinterpret_cast<uint64_t>(p);
-    const uint64_t f = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a >> 32)) << 32) |
-                       __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint64_t f = uniform_u64(a);
     const uint64_t base = f - (1ull << 30);
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
@@ -429,8 +436,7 @@ __device__ __forceinline__ void load_tile(const QuantArgs& a, uint64_t base, int
 #ifdef SML_LOAD_CPOL
         // A/B builds only: buffer loads with explicit cache-policy bits
         const uint64_t tb = reinterpret_cast<uint64_t>(a.in + base);
-        const uint64_t ub = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tb >> 32)) << 32) |
-                            __builtin_amdgcn_readfirstlane((uint32_t)tb);
+        const uint64_t ub = uniform_u64(tb);
         const __amdgpu_buffer_rsrc_t r =
             __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ub), 0, tile_elems<U>() * 4, 0x00020000);
 #pragma unroll
