@@ -161,16 +161,18 @@ __device__ __forceinline__ f4 load4_guarded(const float* p, uint64_t idx, uint64
 }
 
 // The non-temporal 16-byte store of every streaming kernel's large-output
-// path (planes and fp32 outputs from g_nt_threshold on): `nt`
-// (__builtin_nontemporal_store).  SML_NT_CPOL=3 (A/B builds only) writes
-// `sc1 nt` through a buffer store the compiler sees — a per-store descriptor
-// based 1 GiB below the first active lane's address (every lane of a wave
-// stores within a few KiB of it), the lane's byte offset from that base.  An
-// inline-asm store must not be used for this: the compiler's hazard
-// recognizer cannot see into it and let a VALU overwrite the store's address
-// and data VGPRs in the next cycles.
+// path (planes and fp32 outputs from g_nt_threshold on, 16-byte aligned):
+// `sc1 nt` (device coherence scope, streaming).  On cold buckets against the
+// `nt` of __builtin_nontemporal_store: K1 -1.2 %, K4 -2.8 %, the round trip
+// -0.9 % at 256 MiB, K4 -3.2 % at 128 MiB (profiles/r04/ab_bufpol.json).
+// No builtin sets these bits on a global store, so it is a buffer store the
+// compiler schedules (hazards, waits): a descriptor based 1 GiB below the
+// first active lane's address — every lane of a wave stores within a few KiB
+// of it — and the lane's byte offset from that base.  Never inline asm: the
+// hazard recognizer cannot see into it.  SML_NT_CPOL=0 builds
+// plain `nt` (A/B builds).
 #ifndef SML_NT_CPOL
-#define SML_NT_CPOL 0
+#define SML_NT_CPOL 3
 #endif
 // The first active lane's 64-bit value, in SGPRs.  readfirstlane returns a
 // signed int: each half goes through uint32_t before it is widened (a sign-
@@ -186,8 +188,7 @@ __device__ __forceinline__ void nt_store16_sc1(V v, void* p) {
     static_assert(sizeof(V) == 16, "16-byte stores only");
     typedef uint32_t w4 __attribute__((ext_vector_type(4)));
     const uint64_t a = reinterpret_cast<uint64_t>(p);
-    const uint64_t f = uniform_u64(a);
-    const uint64_t base = f - (1ull << 30);
+    const uint64_t base = uniform_u64(a) - (1ull << 30);
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(w4, v), r, (int)(uint32_t)(a - base), 0,
@@ -433,20 +434,8 @@ struct QuantArgs {
 template <bool ALIGNED, int U>
 __device__ __forceinline__ void load_tile(const QuantArgs& a, uint64_t base, int lane, f4 (&v)[U]) {
     if (base + tile_elems<U>() <= a.numel) {
-#ifdef SML_LOAD_CPOL
-        // A/B builds only: buffer loads with explicit cache-policy bits
-        const uint64_t tb = reinterpret_cast<uint64_t>(a.in + base);
-        const uint64_t ub = uniform_u64(tb);
-        const __amdgpu_buffer_rsrc_t r =
-            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ub), 0, tile_elems<U>() * 4, 0x00020000);
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            v[u] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (u * kWave + lane) * 16, 0,
-                                                                                 SML_LOAD_CPOL));
-#else
 #pragma unroll
         for (int u = 0; u < U; u++) v[u] = load4<ALIGNED>(a.in + base + (u * kWave + lane) * 4);
-#endif
     } else {
 #pragma unroll
         for (int u = 0; u < U; u++) {
