@@ -517,7 +517,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": load_traffic(N, P, "quantize_pack" if nb == 1 else "quantize_pack_cold"),
-                "kernel": f"sml::k_quantize_pack<{P},aligned,fused,BE,half-away> (K1: 2-slice wave tiles, non-temporal payload stores at >= 64 MiB)",
+                "kernel": f"sml::k_quantize_pack<{P},aligned,fused,BE,half-away> (K1: 2-slice wave tiles, sc1 nt payload stores at >= 64 MiB)",
             },
             "self_check": ok,
             "self_check_detail": {"what": check_note, "buckets_checked_min_over_ranks": checked},
@@ -764,7 +764,7 @@ def copy_ceiling(sw, torch, N, stream, nbuf=4, reps=200, k1_ms=None):
            "frac_of_peak": round(8 * N / t / 1e9 / HBM_PEAK_GBPS, 4)}
     if k1_ms:
         out["k1_time_over_copy_time"] = round(k1_ms / (t * 1e3), 4)
-    out["note"] = ("a plain non-temporal copy of the same bytes in K1's tile shape, steps cycling the same buckets: "
+    out["note"] = ("a plain copy of the same bytes in K1's tile shape and store policy, steps cycling the same buckets: "
                    "what the HBM delivers to this access pattern")
     return out
 
