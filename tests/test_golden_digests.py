@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
+from mp_ranks import collect
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 with open(os.path.join(HERE, "golden", "digests.json")) as _f:
@@ -171,9 +172,7 @@ def test_switch_sim_w8_reproduces_digests(cuda, name):
     procs = [ctx.Process(target=_switch_rank, args=(r, world, port, name, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
+    res = collect(q, procs, timeout=300, what=f"switch W={world} {name}")
     want = c["sha256"]
     for rank, got, err in res:
         assert got is not None, (rank, err)

@@ -26,6 +26,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
+from mp_ranks import collect
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HUGE = np.float32(1.5 * 2.0 ** 127)     # exponent field 254 -> e = 128 -> int8 -128 (ppp.cc:148-156)
@@ -184,13 +185,7 @@ def _run(world, n, P, net, digest_name=None, timeout=300):
              for r in range(world)]
     for p in procs:
         p.start()
-    try:
-        res = [q.get(timeout=timeout) for _ in procs]
-    finally:
-        for p in procs:
-            p.join(timeout=60)
-            if p.is_alive():
-                p.kill()
+    res = collect(q, procs, timeout=timeout, what=f"rccl switch W={world} {net}")
     for rank, r, err in res:
         assert r is not None, (rank, err)
         assert r.pop("backend") == "nccl"

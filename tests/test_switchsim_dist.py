@@ -19,6 +19,7 @@ import torch
 import torch.multiprocessing as mp
 
 from oracle import oracle as O
+from mp_ranks import collect
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -39,7 +40,9 @@ def _init(rank, world, port):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+    # a rank blocked on a failed peer raises instead of waiting gloo's 30 min
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
     return dist
 
 
@@ -81,9 +84,7 @@ def test_exchange_gloo_cpu(world):
     procs = [ctx.Process(target=_cpu_exchange, args=(r, world, port, n, P, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
+    res = collect(q, procs, timeout=120)
     for rank, ok_e, ok_p, rel in res:
         assert ok_e and ok_p, (rank, rel)
         assert rel < 1e-6
@@ -117,9 +118,7 @@ def test_switchsim_allreduce_two_workers_one_gpu(cuda, P):
     procs = [ctx.Process(target=_gpu_switchsim, args=(r, world, port, n, P, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
+    res = collect(q, procs, timeout=240)
     for rank, ok, err in res:
         assert ok, (rank, err)
 
@@ -179,9 +178,7 @@ def test_p2p_switch_int32_ranks_one_gpu(cuda, world, n, P):
     procs = [ctx.Process(target=_gpu_p2p_int32, args=(r, world, port, n, P, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
+    res = collect(q, procs, timeout=240)
     for rank, ok, err in res:
         assert ok, (rank, err)
 
@@ -200,9 +197,7 @@ def test_p2p_switch_ranks_one_gpu(cuda, world, n, P):
     procs = [ctx.Process(target=_gpu_p2p, args=(r, world, port, n, P, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
+    res = collect(q, procs, timeout=240)
     for rank, ok, err in res:
         assert ok, (rank, err)
 
@@ -259,9 +254,7 @@ def test_sharding_mode_ranks_one_gpu(cuda, world):
     procs = [ctx.Process(target=_gpu_shard, args=(r, world, port, n, P, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
+    res = collect(q, procs, timeout=240)
     for rank, ok, err in res:
         assert ok, (rank, err)
 
@@ -330,8 +323,6 @@ def test_p2p_switch_nccl_multi_gpu(cuda, n, P):
     procs = [ctx.Process(target=_nccl_p2p, args=(r, world, port, n, P, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
+    res = collect(q, procs, timeout=240)
     for rank, ok, err in res:
         assert ok, (rank, err)
