@@ -365,6 +365,10 @@ def main():
         total_alg = world * (8 * N + sw.num_blocks(N, P))
     B = sw.num_blocks(N, P)
     alg_bytes = 8 * N + B
+    if args.graph_steps > 1:
+        # hipGraph capture needs a non-default stream: the whole run (launchers,
+        # capture, replays, the timing events) moves to one
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     stream = torch.cuda.current_stream()
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
