@@ -411,16 +411,16 @@ uint32_t sml_set_xcd_chunk(uint32_t chunk);
 
 /* Tuning knob: slices of 256 elements per wave tile in sml_exponents /
  * sml_quantize_pack (K1/K2/K3): 4, 2 or 1 for every kernel — never below
- * P / 256 — or 0 (the default; any other value restores it): by kernel, as
- * measured fastest — K1 (fused, exponents computed) 2, K2 and K3 4.
+ * P / 256 — or 0 (the default; any other value restores it): 2, measured
+ * fastest for all three on the final kernels.
  * Results are identical for every size.  Returns the
  * previous value. */
 uint32_t sml_set_quantize_tile_slices(uint32_t slices);
 
 /* Tuning knob: slices of 256 elements per wave tile in sml_dequantize (K4)
  * and sml_roundtrip_loopback (the fused round trip; P = 1024 keeps 4): 4 or
- * 2 for both, or 0 = by kernel (the default, as measured: K4 2, the round
- * trip 4).  Results are identical for every size.  Returns
+ * 2 for both, or 0 = the default, 2 for both (as measured).
+ * Results are identical for every size.  Returns
  * the previous value. */
 uint32_t sml_set_stream_tile_slices(uint32_t slices);
 

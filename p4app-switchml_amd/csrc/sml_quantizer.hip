@@ -436,8 +436,11 @@ static void launch_quant_p(uint32_t P, uint32_t U, bool nts, dim3 grid, hipStrea
 }
 
 // Slices per K1/K2/K3 tile: 4 (1024-element tiles), 2 or 1 (never below
-// P / 256), or 0 = by kernel (the default): K1 2, K2 / K3 4.
-// sml_set_quantize_tile_slices.  Measured with non-temporal payload stores
+// P / 256), or 0 = the default, 2 for every kernel (sml_set_quantize_tile_slices).
+// Final kernels (early loads, sc1 nt stores; profiles/r04/ab_slices_final.json,
+// 4 cold buckets, interleaved medians): 2-slice tiles against 4 at 256 MiB
+// K1 -3.1 %, K3 -2.0 %, K2 -3.2 % time (K1 -4.9 % at 128 MiB).  Before the
+// early loads and sc1 (round 4's first sweep), measured with non-temporal payload stores
 // on the bench workload, steps cycling 4 buckets (round 4,
 // profiles/r04/ab_slices_nt.json, interleaved medians): K1 with 2-slice tiles
 // +1.3 / +0.6 / +3.8 / +0.9 % at 128 / 256 / 512 / 1024 MiB, K3 -2.8 % and
@@ -462,8 +465,11 @@ static std::atomic<uint32_t> g_quant_slices{0};
 std::atomic<uint64_t> g_nt_threshold{64ull << 20};
 
 // Slices per K4 / fused round-trip tile: 4 or 2 (sml_set_stream_tile_slices;
-// 0 = by kernel, measured on the bench workload, profiles/r04/ab_stream_slices.json:
-// K4 2, the round trip 4).
+// 0 = the default, 2 for both — a round-trip tile holds whole packets, so
+// P = 1024 keeps 4.  Final kernels, profiles/r04/ab_stream_slices_final.json:
+// 2 against 4 at 256 / 128 MiB, K4 -0.8 / -1.9 %, the round trip -3.4 / -3.6 %
+// time; round 4's first sweep, before the early loads and sc1 stores, had
+// the round trip level).
 static std::atomic<uint32_t> g_stream_slices{0};
 
 static uint32_t stream_slices(uint32_t dflt) {
@@ -474,7 +480,8 @@ static uint32_t stream_slices(uint32_t dflt) {
 static uint32_t quant_slices(uint32_t P, bool fused_k1) {
     const uint32_t need = P > 256 ? P / 256 : 1;
     uint32_t want = g_quant_slices.load(std::memory_order_relaxed);
-    if (want == 0) want = fused_k1 ? 2u : 4u;
+    if (want == 0) want = 2u;
+    (void)fused_k1;
     return want > need ? want : need;
 }
 
@@ -714,9 +721,8 @@ sml_status_t sml_roundtrip_loopback(const float* d_in, float* d_out, uint64_t nu
     if (!d_in || !d_out || !aligned4(d_in) || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
     if (d_payload && !aligned16(d_payload)) return SML_ERR_ALIGNMENT;
     RoundTripArgs a;
-    // a tile holds whole packets; 2-slice tiles measured level (+0.7 / -0.2 /
-    // +0.2 % at 128 / 256 / 512 MiB), so 4 stays the default
-    const uint32_t U = packet_numel > 512 ? 4u : stream_slices(4);
+    // a tile holds whole packets: P = 1024 needs 4 slices
+    const uint32_t U = packet_numel > 512 ? 4u : stream_slices(2);
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);
     a.in = d_in;
     a.out = d_out;

@@ -96,7 +96,7 @@ def test_misaligned_slice_geometry_invariant(sw):
 @pytest.mark.parametrize("P", [64, 128, 256, 512, 1024])
 def test_quantize_tile_slices_invariant(sw, P):
     """K1 / K2 / K3 with every wave-tile size (sml_set_quantize_tile_slices:
-    0 = by kernel (the default: K1 2, K2/K3 4), 1, 2, 4 slices of 256 elements, never
+    0 = the default (2), 1, 2, 4 slices of 256 elements, never
     below P / 256) under capped grids
     and XCD orders, aligned and 4-byte-offset slices, RNE and LE flags: the
     same bytes as the oracle."""
