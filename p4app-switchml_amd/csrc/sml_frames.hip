@@ -269,8 +269,12 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
 // contiguously.  No header is read again; pkt_ids without a winner in this
 // call (not received, or received earlier) write nothing; the same pass then
 // retires the winners.
-constexpr int kRxU = 4;                        // 16-B chunks per lane per iteration
-constexpr int kRxTileElems = kRxU * kWave * 4;
+// 16-B chunks per lane per tile (slices of 256 elements); a tile holds whole
+// packets, so never below P / 256.  SML_RX_SLICES: A/B builds only.
+#ifndef SML_RX_SLICES
+#define SML_RX_SLICES 4
+#endif
+__host__ __device__ constexpr int rx_slices(int P) { return P / 256 > SML_RX_SLICES ? P / 256 : SML_RX_SLICES; }
 
 __device__ __forceinline__ bool rx_winner(unsigned long long sw, uint64_t nframes, uint64_t& f) {
     const uint32_t hi = (uint32_t)(sw >> 32);
@@ -286,6 +290,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     const bool pow2 = (a.W & (a.W - 1)) == 0;
     if (pow2) build_rcp_lut(lut, a.W);
     else build_lut(lut, a.W);
+    constexpr int kRxU = rx_slices(P);
+    constexpr int kRxTileElems = kRxU * kWave * 4;
     constexpr int kChunksPerFrame = P / 4;     // 16-B chunks per payload
     constexpr int kBlocksPerTile = kRxTileElems / P;
     const int lane = threadIdx.x & (kWave - 1);
@@ -515,7 +521,9 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     if (!aligned4(frames) || !aligned4(d_out) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
     if (((uintptr_t)d_state & 7u) || (d_counts && ((uintptr_t)d_counts & 7u))) return SML_ERR_ALIGNMENT;
     RxArgs a;
-    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    const uint32_t U = (uint32_t)rx_slices((int)P);
+    a.xcd = U < 4 ? g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U)   // XCD runs keep their byte length
+                  : g_xcd_chunk.load(std::memory_order_relaxed);
     a.frames = static_cast<const uint8_t*>(frames);
     a.nframes = num_frames;
     a.stride = stride;
@@ -530,7 +538,8 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     a.job = (uint8_t)job_id;
     hipStream_t st = (hipStream_t)stream;
     k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
-    const uint64_t ntiles = (a.nblocks * P + kRxTileElems - 1) / kRxTileElems;
+    const uint64_t tile = (uint64_t)U * kWave * 4;
+    const uint64_t ntiles = (a.nblocks * P + tile - 1) / tile;
     if (ntiles) launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
     return launch_check();
 }
