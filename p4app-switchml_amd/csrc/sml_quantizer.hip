@@ -477,11 +477,10 @@ static uint32_t stream_slices(uint32_t dflt) {
     return want ? want : dflt;
 }
 
-static uint32_t quant_slices(uint32_t P, bool fused_k1) {
+static uint32_t quant_slices(uint32_t P) {
     const uint32_t need = P > 256 ? P / 256 : 1;
     uint32_t want = g_quant_slices.load(std::memory_order_relaxed);
     if (want == 0) want = 2u;
-    (void)fused_k1;
     return want > need ? want : need;
 }
 
@@ -641,7 +640,7 @@ static sml_status_t quantize_common(const float* d_in, uint64_t numel, uint32_t 
     if (!d_in || !aligned4(d_in)) return SML_ERR_INVALID_ARG;
     if (d_payload && !aligned16(d_payload)) return SML_ERR_ALIGNMENT;
     QuantArgs a;
-    const uint32_t U = quant_slices(P, d_payload && !d_gexp);
+    const uint32_t U = quant_slices(P);
     // XCD runs keep their byte length (C workgroups of 4 U-slice tiles)
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);
     a.in = d_in;
@@ -793,7 +792,7 @@ sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void
     if (!d_in || !d_out || !aligned16(d_in) || !aligned16(d_out) || bytes % (kTileElems * 4)) return SML_ERR_ALIGNMENT;
     // K1's tile shape (its slices per tile at P = 256) and store policy for an
     // output plane of `bytes` (sml_quantize_pack)
-    const uint32_t U = quant_slices(256, true);
+    const uint32_t U = quant_slices(256);
     const uint64_t ntiles = bytes / (256 * U * 4);
     const uint32_t xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);
     auto in = reinterpret_cast<const u4*>(d_in);
