@@ -320,7 +320,7 @@ struct RoundTripBatchArgs {
     uint32_t xcd;
 };
 
-template <int P, bool RNE, bool NT = false>
+template <int P, bool RNE, bool NT = false, int U = kU>
 __global__ __launch_bounds__(kBlockThreads) void k_roundtrip_batch(RoundTripBatchArgs a) {
     __shared__ float lut[256];
     build_lut(lut, a.W);
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_roundtrip_batch(RoundTripBatc
         r.exps_out = nullptr;
         r.W = a.W;
         r.xcd = a.xcd;
-        roundtrip_tile<P, false, true, RNE, NT>(r, t - t0, lut, lane);
+        roundtrip_tile<P, false, true, RNE, NT, U>(r, t - t0, lut, lane);
     }
 }
 
@@ -548,7 +548,17 @@ static void launch_rt_p(uint32_t P, uint32_t U, bool nt, dim3 grid, hipStream_t 
 }
 
 template <bool RNE, bool NT>
-static void launch_rtb_pn(uint32_t P, dim3 grid, hipStream_t st, const RoundTripBatchArgs& a) {
+static void launch_rtb_pn(uint32_t P, uint32_t U, dim3 grid, hipStream_t st, const RoundTripBatchArgs& a) {
+    // a tile holds whole packets: P = 1024 runs 4 slices
+    if (U == 2) {
+        switch (P) {
+            case 64:   k_roundtrip_batch<64, RNE, NT, 2><<<grid, kBlockThreads, 0, st>>>(a); return;
+            case 128:  k_roundtrip_batch<128, RNE, NT, 2><<<grid, kBlockThreads, 0, st>>>(a); return;
+            case 256:  k_roundtrip_batch<256, RNE, NT, 2><<<grid, kBlockThreads, 0, st>>>(a); return;
+            case 512:  k_roundtrip_batch<512, RNE, NT, 2><<<grid, kBlockThreads, 0, st>>>(a); return;
+            default:   break;
+        }
+    }
     switch (P) {
         case 64:   k_roundtrip_batch<64, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
         case 128:  k_roundtrip_batch<128, RNE, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
@@ -559,9 +569,9 @@ static void launch_rtb_pn(uint32_t P, dim3 grid, hipStream_t st, const RoundTrip
 }
 
 template <bool RNE>
-static void launch_rtb_p(uint32_t P, bool nt, dim3 grid, hipStream_t st, const RoundTripBatchArgs& a) {
-    if (nt) launch_rtb_pn<RNE, true>(P, grid, st, a);
-    else launch_rtb_pn<RNE, false>(P, grid, st, a);
+static void launch_rtb_p(uint32_t P, uint32_t U, bool nt, dim3 grid, hipStream_t st, const RoundTripBatchArgs& a) {
+    if (nt) launch_rtb_pn<RNE, true>(P, U, grid, st, a);
+    else launch_rtb_pn<RNE, false>(P, U, grid, st, a);
 }
 
 template <bool ALIGNED>
@@ -748,7 +758,10 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
     if (!valid_packet(packet_numel)) return SML_ERR_UNSUPPORTED;
     if (num_workers == 0 || num_slices > SML_MAX_BATCH_SLICES || (num_slices && !slices)) return SML_ERR_INVALID_ARG;
     RoundTripBatchArgs a;
-    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
+    // the single-slice round trip's tile (2 slices; P = 1024: 4)
+    const uint32_t U = packet_numel > 512 ? 4u : (stream_slices(2) == 4 ? 4u : 2u);
+    const uint64_t tile = (uint64_t)U * kWave * 4;
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);   // XCD runs keep their byte length
     a.W = num_workers;
     a.nslices = 0;
     uint64_t tiles = 0;
@@ -756,7 +769,7 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
         const sml_slice& sl = slices[i];
         if (sl.numel == 0) continue;                      // empty slices touch nothing
         if (!sl.in || !sl.out || !aligned4(sl.in) || !aligned4(sl.out)) return SML_ERR_INVALID_ARG;
-        tiles += (sml_num_blocks(sl.numel, packet_numel) * packet_numel + kTileElems - 1) / kTileElems;
+        tiles += (sml_num_blocks(sl.numel, packet_numel) * packet_numel + tile - 1) / tile;
         if (tiles > 0xFFFFFFFFull) return SML_ERR_UNSUPPORTED;
         a.in[a.nslices] = sl.in;
         a.out[a.nslices] = sl.out;
@@ -774,8 +787,8 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
     uint64_t out_bytes = 0;
     for (uint32_t i = 0; i < a.nslices; i++) out_bytes += 4 * a.numel[i];
     const bool nt = out_bytes >= g_nt_threshold.load(std::memory_order_relaxed);
-    if (flags & SML_FLAG_ROUND_RNE) launch_rtb_p<true>(packet_numel, nt, grid, st, a);
-    else launch_rtb_p<false>(packet_numel, nt, grid, st, a);
+    if (flags & SML_FLAG_ROUND_RNE) launch_rtb_p<true>(packet_numel, U, nt, grid, st, a);
+    else launch_rtb_p<false>(packet_numel, U, nt, grid, st, a);
     return launch_check();
 }
 
