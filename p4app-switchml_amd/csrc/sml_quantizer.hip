@@ -758,8 +758,12 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
     if (!valid_packet(packet_numel)) return SML_ERR_UNSUPPORTED;
     if (num_workers == 0 || num_slices > SML_MAX_BATCH_SLICES || (num_slices && !slices)) return SML_ERR_INVALID_ARG;
     RoundTripBatchArgs a;
-    // the single-slice round trip's tile (2 slices; P = 1024: 4)
-    const uint32_t U = packet_numel > 512 ? 4u : (stream_slices(2) == 4 ? 4u : 2u);
+    // tile slices (P = 1024: 4).  SML_BATCH_SLICES=2 gives the batch the
+    // single-slice round trip's 2-slice tiles: an A/B build until measured.
+#ifndef SML_BATCH_SLICES
+#define SML_BATCH_SLICES 4
+#endif
+    const uint32_t U = packet_numel > 512 ? 4u : (uint32_t)SML_BATCH_SLICES;
     const uint64_t tile = (uint64_t)U * kWave * 4;
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);   // XCD runs keep their byte length
     a.W = num_workers;
