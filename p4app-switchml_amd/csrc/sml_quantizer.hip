@@ -758,10 +758,12 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
     if (!valid_packet(packet_numel)) return SML_ERR_UNSUPPORTED;
     if (num_workers == 0 || num_slices > SML_MAX_BATCH_SLICES || (num_slices && !slices)) return SML_ERR_INVALID_ARG;
     RoundTripBatchArgs a;
-    // tile slices (P = 1024: 4).  SML_BATCH_SLICES=2 gives the batch the
-    // single-slice round trip's 2-slice tiles: an A/B build until measured.
+    // tile slices (P = 1024: 4): the single-slice round trip's 2 — against 4
+    // on 4 cold jobs: a 256 MiB job as 4 FIFO slices 86.22 -> 85.86 us, 4 x
+    // 25 MiB buckets 36.10 -> 35.32 us (profiles/r04/ab_batch_slices.json).
+    // SML_BATCH_SLICES: A/B builds.
 #ifndef SML_BATCH_SLICES
-#define SML_BATCH_SLICES 4
+#define SML_BATCH_SLICES 2
 #endif
     const uint32_t U = packet_numel > 512 ? 4u : (uint32_t)SML_BATCH_SLICES;
     const uint64_t tile = (uint64_t)U * kWave * 4;
