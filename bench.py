@@ -30,15 +30,14 @@ configs4_plugin: the ResNet-50 buckets through the CollNet plugin table on an
 N-rank communicator over the xgmi backend (device and pinned host buffers).
 The exit status is 1 when the headline's own check fails (the timed planes
 differ from the committed digests), when the headline cannot be measured, or
-when the RCCL switch (switchsim) RAN and gave wrong bits (not within the
-quantization bound, not bit-equal to the other paths, or timed calls that
-differ from the first): a correctness regression there is fatal; with
---strict-switch so is one of the peer-memory paths (p2p_switch, xgmi_switch,
-xgmi_switch_push), whose mismatch is otherwise reported under
-"diagnostic_failures" — they first meet real xGMI in the driver's node run.  A diagnostic field that could
-not run or timed out (switch paths, plugin, rccl_collnet) is reported in the
-line under "diagnostic_failures" and in its own field, so one path that
-cannot start cannot void the measured headline.
+when ANY switch path (switchsim, p2p_switch, xgmi_switch, xgmi_switch_push)
+RAN and gave wrong bits — not within the quantization bound, timed calls that
+differ from the first, or a peer-memory path not bit-equal to switchsim: wrong
+bits are a correctness failure wherever they come from (--lenient-switch
+demotes the peer-memory paths' mismatch to a diagnostic, for bring-up only).
+A field that could not run or timed out (switch paths, plugin,
+rccl_collnet) is reported in the line under "diagnostic_failures" and in its
+own field, so one path that cannot start cannot void the measured headline.
 
 Units: value / roofline.achieved = ALGORITHMIC bytes per second: 4N read
 (fp32 in) + 4N written (int32 payload) + B written (int8 exponents),
@@ -49,7 +48,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import subprocess
 import sys
 import threading
@@ -84,9 +82,10 @@ def parse(argv=None):
     ap.add_argument("--exchange-timeout", type=float, default=300.0,
                     help="N > 1: seconds the switch / plugin phase may take before the run reports what it has "
                          "measured, with a failure, and exits 1 (a hang would otherwise print nothing)")
-    ap.add_argument("--strict-switch", action="store_true",
-                    help="N > 1: a switch path that runs but is not verified fails the run for every path "
-                         "(default: only switchsim's failure is fatal; the peer-memory paths' are diagnostic)")
+    ap.add_argument("--lenient-switch", action="store_true",
+                    help="N > 1, bring-up only: a peer-memory switch path (p2p_switch, xgmi_switch, "
+                         "xgmi_switch_push) that runs and gives wrong bits is reported under diagnostic_failures "
+                         "instead of failing the run (default: wrong bits from any path fail the run)")
     ap.add_argument("--no-plugin", action="store_true",
                     help="N > 1: skip the configs4_plugin field (ResNet-50 buckets through the CollNet table per rank)")
     ap.add_argument("--buckets", type=int, default=4,
@@ -108,21 +107,15 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def launch_ranks(n):
     """`bench.py --gpus N` without a launcher: start N rank processes with
-    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) as CHILD
-    processes and exit with their status.  Runs before anything touches the
-    GPU (no exec from a GPU-initialised process)."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    torch.distributed.run (one per GPU) as CHILD processes and exit with their
+    status.  --standalone: the launcher's own store binds an OS-chosen port on
+    127.0.0.1 and hands it to the ranks (no port picked here and bound later,
+    which another process could take in between).  Runs before anything
+    touches the GPU (no exec from a GPU-initialised process)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes=1", f"--nproc-per-node={n}", os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.call(cmd)
 
 
@@ -480,7 +473,10 @@ def main():
         if job_numel:
             workload = (f"configs[3]: one {job_numel * 4 >> 20} MiB fp32 job sharded over {world} GPU(s) by the FIFO "
                         f"rule ({N} elements on rank 0), fused exponent+quantize+BE pack (sml_quantize_pack, K1), "
-                        "loopback exponents (W=1)")
+                        "loopback exponents (W=1); `value` is this job's STRONG-scaling rate (total work fixed, "
+                        "each GPU's slice shrinks as N grows)" +
+                        ("; `weak_256MiB_value` is the WEAK-scaling rate (256 MiB per GPU at every N)"
+                         if world > 1 else ""))
         else:
             workload = (f"configs[2]-sized bucket: {N * 4 >> 20} MiB fp32 per GPU, fused exponent+quantize+BE pack "
                         "(sml_quantize_pack, K1), loopback exponents (W=1)")
@@ -532,6 +528,10 @@ def main():
         if "frac" in side.get("resident", {}):
             line["roofline"]["frac_resident"] = side["resident"]["frac"]
             line["roofline"]["traffic_resident"] = load_traffic(args.numel, P, "quantize_pack")
+        readings = weak_readings(side.get("weak_256MiB_per_gpu", {}), world)
+        if readings:
+            line["config"]["readings"] = readings.pop("readings")
+            line.update(readings)
         line.update(fields)
         if side:
             line["side"] = side
@@ -590,7 +590,7 @@ def main():
             fields.update(exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev))
         except Exception as e:  # noqa: BLE001 - recorded as a diagnostic failure below
             fields["switchsim"] = {"error": repr(e)[:400]}
-        fatal, diag = switch_verdicts(fields, args.strict_switch)
+        fatal, diag = switch_verdicts(fields, lenient=args.lenient_switch)
         failures.extend(fatal)
         diag_failures.extend(diag)
     if world > 1 and not args.no_plugin:
@@ -628,25 +628,46 @@ def main():
         sys.exit(1)
 
 
+def weak_readings(wk, world):
+    """The N > 1 line's two readings, both named: `value` is
+    configs[3]'s 1 GiB job strong-scaled over the N GPUs; `weak_256MiB_value`
+    (with its own roofline) the metric's 256 MiB bucket on EVERY GPU.  `wk` is
+    weak_measure's result; {} at N = 1 or when it did not run."""
+    if world <= 1 or "value_GBps" not in wk:
+        return {}
+    return {
+        "weak_256MiB_value": wk["value_GBps"],
+        "weak_256MiB": {
+            "value": wk["value_GBps"], "unit": "GB/s", "scaling": "weak", "n_gpus": world,
+            "ms_per_step": wk["ms_per_step"], "numel_per_gpu": wk["numel_per_gpu"],
+            "buckets_cycled": wk["buckets"],
+            "roofline": {"bound": "hbm", "achieved": wk["kernel_GBps_per_gpu"], "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": wk["frac_per_gpu"],
+                         "note": "per GPU: algorithmic bytes / HIP-event kernel time, max over ranks"}},
+        "readings": {
+            "value": "strong scaling: configs[3]'s one 1 GiB job split over the N GPUs",
+            "weak_256MiB_value": "weak scaling: every GPU quantizes its own 256 MiB buckets (4 cycled)"},
+    }
+
+
 SWITCH_PATHS = ("switchsim", "p2p_switch", "xgmi_switch", "xgmi_switch_push")
 
 
-def switch_verdicts(fields, strict=False):
+def switch_verdicts(fields, lenient=False):
     """(fatal, diagnostic) failure lines for the N > 1 switch fields.  A path
-    that could not run (an error, missing) is diagnostic.  A path that RAN and
-    was not verified (outside the quantization bound, timed calls differing
-    from the first, or — for the peer-memory paths — not bit-equal to
-    switchsim) is fatal for switchsim, the RCCL switch tested under RCCL on
-    MI355X, and for every path with `strict`; the peer-memory paths first meet
-    real xGMI in the driver's node run, so by default their mismatch is
-    reported, not fatal."""
+    that could not run (an error, a timeout, missing) is diagnostic.  A path
+    that RAN and was not verified — outside the quantization bound, timed
+    calls differing from the first, or (peer-memory paths) not bit-equal to
+    switchsim — is fatal, for every path: wrong bits are a correctness
+    failure.  `lenient` (bring-up only) demotes the peer-memory paths'
+    mismatch to a diagnostic; switchsim's stays fatal."""
     fatal, diag = [], []
     for k in SWITCH_PATHS:
         f = fields.get(k, {})
         if "error" in f or "verified" not in f:
             diag.append(f"{k}: {f.get('error', 'not run')}")
         elif not f["verified"]:
-            (fatal if k == "switchsim" or strict else diag).append(
+            (diag if lenient and k != "switchsim" else fatal).append(
                 f"{k}: not verified (within bound {f.get('within_quantization_bound')}, bit-equal "
                 f"{f.get('bit_equal_to_switchsim', f.get('bit_equal_to_other_paths'))}, timed calls equal "
                 f"{f.get('timed_calls_equal_first')})")
@@ -790,36 +811,50 @@ def job_measure(sw, torch, job_numel, P, stream, dev, reps=50):
             "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}
 
 
-def weak_measure(sw, torch, dist, N, P, stream, dev, world, reps=200):
+def weak_measure(sw, torch, dist, N, P, stream, dev, world, reps=200, nbuf=4):
     """Weak scaling beside the strong-scaling headline at N > 1: every rank
-    runs K1 over its own resident N-element bucket (the metric's 256 MiB per
-    GPU, as at N = 1), launches bracketed by a barrier and a device sync;
-    aggregate = world x (8N + B) / max-over-ranks time per step."""
+    runs K1 over its own N-element buckets (the metric's 256 MiB per GPU, as
+    at N = 1), the steps cycling `nbuf` distinct buckets + planes like the
+    headline (HBM proper), launches bracketed by a barrier and a device sync;
+    aggregate = world x (8N + B) / max-over-ranks time per step.  The kernel
+    time (HIP events on the launch stream, max over ranks) gives the per-GPU
+    roofline fraction."""
     B = sw.num_blocks(N, P)
     g = torch.Generator(device=dev)
     g.manual_seed(4343 + dist.get_rank())
-    x = torch.randn(N, device=dev, generator=g)
-    pl = torch.empty(B * P, dtype=torch.int32, device=dev)
-    ex = torch.empty(B, dtype=torch.int8, device=dev)
-    fn = lambda: sw.quantize_pack(x, P, 1, payload=pl, exps_out=ex, stream=stream)  # noqa: E731
+    xs = [torch.randn(N, device=dev, generator=g) for _ in range(nbuf)]
+    pls = [torch.empty(B * P, dtype=torch.int32, device=dev) for _ in range(nbuf)]
+    exs = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nbuf)]
+    i = [0]
+
+    def fn():
+        k = i[0]
+        i[0] = (k + 1) % nbuf
+        sw.quantize_pack(xs[k], P, 1, payload=pls[k], exps_out=exs[k], stream=stream)
+
     settle(fn, 30.0)
     for _ in range(20):
         fn()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for _ in range(reps):
         fn()
+    ev1.record(stream)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0          # the closing barrier is not a step (see main)
     dist.barrier()
-    t = torch.tensor([el / reps], dtype=torch.float64, device=dev)
+    t = torch.tensor([el / reps, ev0.elapsed_time(ev1) * 1e-3 / reps], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t = float(t[0])
+    t, tk = float(t[0]), float(t[1])
     alg = 8 * N + B
-    return {"numel_per_gpu": N, "ms_per_step": round(t * 1e3, 5), "value_GBps": round(world * alg / t / 1e9, 1),
-            "per_gpu_GBps": round(alg / t / 1e9, 1), "frac_per_gpu": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
-            "note": "every GPU quantizes its own resident 256 MiB bucket (weak scaling); the headline "
+    return {"numel_per_gpu": N, "buckets": nbuf, "ms_per_step": round(t * 1e3, 5),
+            "value_GBps": round(world * alg / t / 1e9, 1), "per_gpu_GBps": round(alg / t / 1e9, 1),
+            "kernel_ms": round(tk * 1e3, 5), "kernel_GBps_per_gpu": round(alg / tk / 1e9, 1),
+            "frac_per_gpu": round(alg / tk / 1e9 / HBM_PEAK_GBPS, 4),
+            "note": "every GPU quantizes its own 256 MiB buckets, 4 cycled (weak scaling); the headline "
                     "shards one 1 GiB job (strong scaling, configs[3])"}
 
 

@@ -17,8 +17,11 @@
 //   ring and the extra-info slots in two separate hipHostRegister'd
 //   allocations — a NIC pool whose device addresses need not equal its host
 //   addresses, and whose extras are another registration.
-// Exit 0: done; 3: the PPP refused per-packet calls (message on stdout);
-// 1: any other failure.
+// Exit 0: done; 3: per-packet calls refused (message on stdout) — at setup,
+// before any packet, when the configured name takes only the bulk / burst
+// hooks (PrePostProcessor::PerLtuCalls, what a packet-driven backend asks at
+// configuration time), or by the PPP itself on the data path
+// (PER_LTU_NO_SETUP_CHECK=1 skips the setup check); 1: any other failure.
 #include <hip/hip_runtime_api.h>
 
 #include <cstdio>
@@ -48,6 +51,28 @@ int main(int argc, char** argv) {
     }
     const uint64_t numel = std::strtoull(argv[2], nullptr, 10);
     const uint64_t P = 256, batch_max = 64;
+    if (mode == "single" && !std::getenv("PER_LTU_NO_SETUP_CHECK")) {
+        // a per-packet worker asks the factory's policy at setup, so a name that
+        // refuses per-packet calls fails here, not at its first packet
+        int per_ltu = -1;
+        try {
+            per_ltu = PrePostProcessor::PerLtuCalls(argv[1]);
+        } catch (const SwitchMLFatal& e) {
+            printf("FAILED %s\n", e.what());
+            return 1;
+        }
+        if (per_ltu < 0) {
+            printf("FAILED '%s' is not a valid prepostprocessor.\n", argv[1]);
+            return 1;
+        }
+        if (per_ltu == 0) {
+            printf("REFUSED at setup: prepostprocessor '%s' takes the bulk hooks (PreprocessBulk / "
+                   "PostprocessBulk) or the burst hooks (PreprocessBurst / PostprocessBurst / "
+                   "PostprocessReuseBurst), not one PreprocessSingle / PostprocessSingle per packet; set "
+                   "prepostprocessor = hip_exponent_quantizer to accept per-packet launches\n", argv[1]);
+            return 3;
+        }
+    }
     Config cfg;
     cfg.general_.prepostprocessor = argv[1];
     cfg.general_.packet_numel = P;

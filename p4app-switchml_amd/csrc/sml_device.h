@@ -169,11 +169,7 @@ __device__ __forceinline__ f4 load4_guarded(const float* p, uint64_t idx, uint64
 // compiler schedules (hazards, waits): a descriptor based 1 GiB below the
 // first active lane's address — every lane of a wave stores within a few KiB
 // of it — and the lane's byte offset from that base.  Never inline asm: the
-// hazard recognizer cannot see into it.  SML_NT_CPOL=0 builds
-// plain `nt` (A/B builds).
-#ifndef SML_NT_CPOL
-#define SML_NT_CPOL 3
-#endif
+// hazard recognizer cannot see into it.
 // The first active lane's 64-bit value, in SGPRs.  readfirstlane returns a
 // signed int: each half goes through uint32_t before it is widened (a sign-
 // extended low half corrupts the high one).
@@ -182,7 +178,6 @@ __device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
     return ((uint64_t)hi << 32) | lo;
 }
-#if SML_NT_CPOL == 3
 template <typename V>
 __device__ __forceinline__ void nt_store16_sc1(V v, void* p) {
     static_assert(sizeof(V) == 16, "16-byte stores only");
@@ -195,9 +190,6 @@ __device__ __forceinline__ void nt_store16_sc1(V v, void* p) {
                                            18 /* sc1 nt */);
 }
 #define SML_NT_STORE16(v, p) nt_store16_sc1((v), (void*)(p))
-#else
-#define SML_NT_STORE16(v, p) __builtin_nontemporal_store((v), (p))
-#endif
 #define SML_NT_STORE16_UNALIGNED(v, p) __builtin_nontemporal_store((v), (p))
 
 // NT: non-temporal (for output planes larger than the Infinity Cache: see

@@ -272,11 +272,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_claim(RxArgs a) {
 // 16-B chunks per lane per tile (slices of 256 elements); a tile holds whole
 // packets, so never below P / 256.  2 against 4 on 4 cycled 256 MiB frame
 // sets: 97.63 -> 95.59 us per rx call (profiles/r04/ab_rx_slices.json), as
-// the plane kernels moved to 2-slice tiles.  SML_RX_SLICES: A/B builds.
-#ifndef SML_RX_SLICES
-#define SML_RX_SLICES 2
-#endif
-__host__ __device__ constexpr int rx_slices(int P) { return P / 256 > SML_RX_SLICES ? P / 256 : SML_RX_SLICES; }
+// the plane kernels moved to 2-slice tiles.
+__host__ __device__ constexpr int rx_slices(int P) { return P / 256 > 2 ? P / 256 : 2; }
 
 __device__ __forceinline__ bool rx_winner(unsigned long long sw, uint64_t nframes, uint64_t& f) {
     const uint32_t hi = (uint32_t)(sw >> 32);

@@ -761,11 +761,7 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
     // tile slices (P = 1024: 4): the single-slice round trip's 2 — against 4
     // on 4 cold jobs: a 256 MiB job as 4 FIFO slices 86.22 -> 85.86 us, 4 x
     // 25 MiB buckets 36.10 -> 35.32 us (profiles/r04/ab_batch_slices.json).
-    // SML_BATCH_SLICES: A/B builds.
-#ifndef SML_BATCH_SLICES
-#define SML_BATCH_SLICES 2
-#endif
-    const uint32_t U = packet_numel > 512 ? 4u : (uint32_t)SML_BATCH_SLICES;
+    const uint32_t U = packet_numel > 512 ? 4u : 2u;
     const uint64_t tile = (uint64_t)U * kWave * 4;
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U);   // XCD runs keep their byte length
     a.W = num_workers;

@@ -15,11 +15,6 @@
 // Bit-identical to orc_switch_payload / orc_switch_exps followed by K4.
 #include "sml_host.h"
 
-// Planes whose loads are issued together per loop trip (A/B knob).
-#ifndef SML_SWITCH_UNROLL
-#define SML_SWITCH_UNROLL 2
-#endif
-
 namespace sml {
 
 // The reader's half of a hand-off from other GPUs (SML_FLAG_PEER_PLANES):
@@ -87,7 +82,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_switch_aggregate(SwitchArgs a
         u4 acc[kU];
 #pragma unroll
         for (int u = 0; u < kU; u++) acc[u] = mku4(0, 0, 0, 0);
-#pragma unroll SML_SWITCH_UNROLL
+#pragma unroll 2   // two planes' loads issued together per trip (profiles/r01/ab11_switch_unroll.json)
         for (uint32_t w = 0; w < a.nw; w++) {
             u4 v[kU];
 #pragma unroll

@@ -4,6 +4,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <signal.h>
+#include <sys/file.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -27,8 +28,26 @@ bool pid_alive(int32_t pid) { return pid > 0 && (kill(pid, 0) == 0 || errno == E
 // mmap of a segment worker 0 creates: it is sized (ftruncate) only after the
 // O_EXCL create, so a file opened in between is 0 bytes and touching the
 // mapping would raise SIGBUS.  Shorter than OrderShm: not ready (or stale) —
-// nullptr.  Closes fd.
-OrderShm* map_sized(int fd, int prot);
+// nullptr.  Closes fd unless keep_fd.
+OrderShm* map_sized(int fd, int prot, bool keep_fd = false);
+
+// Remove `name` if it still names the segment open on `fd`, holding an
+// exclusive flock on that segment.  Both parties that remove a name — worker
+// 0 replacing a segment of its own, and the last worker to close a segment —
+// do it through here, so each one's "is the name still that segment?" check
+// and its unlink are a single step for the other (the last
+// detacher's generation check, then worker 0 replacing the segment, then the
+// detacher's unlink would remove the NEW communicator's segment).
+void unlink_if_named(const std::string& name, int fd) {
+    if (flock(fd, LOCK_EX) != 0) return;
+    struct stat a, b;
+    const int cur = shm_open(name.c_str(), O_RDONLY, 0600);
+    const bool same = cur >= 0 && fstat(fd, &a) == 0 && fstat(cur, &b) == 0 && a.st_ino == b.st_ino &&
+                      a.st_dev == b.st_dev;
+    if (cur >= 0) close(cur);
+    if (same) shm_unlink(name.c_str());
+    flock(fd, LOCK_UN);
+}
 
 struct alignas(64) Counter {
     std::atomic<uint64_t> v;
@@ -50,12 +69,12 @@ struct OrderShm {
 
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
 
-OrderShm* map_sized(int fd, int prot) {
+OrderShm* map_sized(int fd, int prot, bool keep_fd) {
     struct stat st;
     void* m = MAP_FAILED;
     if (fstat(fd, &st) == 0 && (uint64_t)st.st_size >= sizeof(OrderShm))
         m = mmap(nullptr, sizeof(OrderShm), prot, MAP_SHARED, fd, 0);
-    close(fd);
+    if (!keep_fd) close(fd);
     return m == MAP_FAILED ? nullptr : static_cast<OrderShm*>(m);
 }
 
@@ -92,15 +111,18 @@ JobOrder::JobOrder(const std::string& session, int rank, int nworkers, uint64_t 
             // earlier communicator's that was never closed)
             const int fe = shm_open(name_.c_str(), O_RDWR, 0600);
             if (fe >= 0) {
-                if (OrderShm* o = map_sized(fe, PROT_READ)) {
+                if (OrderShm* o = map_sized(fe, PROT_READ, true)) {
                     const int32_t pid = o->creator_pid.load();
                     munmap(o, sizeof(OrderShm));
-                    if (pid_alive(pid) && pid != getpid())
+                    if (pid_alive(pid) && pid != getpid()) {
+                        close(fe);
                         throw std::runtime_error("job order: session " + name_ + " is in use by process " +
                                                  std::to_string(pid));
+                    }
                 }
+                unlink_if_named(name_, fe);
+                close(fe);
             }
-            shm_unlink(name_.c_str());
         }
         shm_ = static_cast<OrderShm*>(m);
         shm_->generation = gen_ = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() ^
@@ -148,7 +170,9 @@ JobOrder::JobOrder(const std::string& session, int rank, int nworkers, uint64_t 
 
 // The last worker to close removes the name — if the name still is ITS
 // segment: worker 0 may already have replaced it with a reconnected
-// communicator's (a new generation), which stays.
+// communicator's (a new generation), which stays.  The generation says the
+// fd is this communicator's segment; unlink_if_named makes "the name still
+// refers to it" and the unlink one step against worker 0's replacement.
 JobOrder::~JobOrder() {
     if (!shm_) return;
     const bool last = shm_->detached.fetch_add(1) + 1 == (uint32_t)nworkers_;
@@ -156,11 +180,12 @@ JobOrder::~JobOrder() {
     if (!last) return;
     const int fd = shm_open(name_.c_str(), O_RDONLY, 0600);
     if (fd < 0) return;
-    if (OrderShm* s = map_sized(fd, PROT_READ)) {
+    if (OrderShm* s = map_sized(fd, PROT_READ, true)) {
         const bool mine = s->generation == gen_;
         munmap(s, sizeof(OrderShm));
-        if (mine) shm_unlink(name_.c_str());
+        if (mine) unlink_if_named(name_, fd);   // still this segment under the lock worker 0 replaces with
     }
+    close(fd);
 }
 
 bool JobOrder::Append(const CallKey& k) {

@@ -231,8 +231,8 @@ def set_payload_nt_threshold(nbytes: int) -> int:
 
 def set_quantize_tile_slices(slices: int) -> int:
     """Slices of 256 elements per K1/K2/K3 wave tile: 4, 2 or 1 for every
-    kernel (never below P/256), or 0 = by kernel (the default: K1 2, K2/K3
-    4); returns the previous setting."""
+    kernel (never below P/256), or 0 = the default, 2 slices for every kernel
+    (never below P/256); returns the previous setting."""
     return int(lib().sml_set_quantize_tile_slices(slices))
 
 

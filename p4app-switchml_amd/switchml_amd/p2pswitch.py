@@ -21,10 +21,19 @@ result is bit-identical to SwitchSimAllReduce (and to the oracle switch).
 Shards: block ranges of S = ceil(B / W) blocks, rank r owns blocks
 [r*S, min((r+1)*S, B)); `out` is padded to W*S*P elements internally so the
 all-gather moves equal shards.
+
+Every wait is bounded (the round-4 hang): the host waits for
+the device at each hand-off by polling an event against `sync_timeout`
+(a named TimeoutError, never an unbounded stream synchronize); the rendezvous
+collectives carry the process group's timeout; and a rank whose peer mapping
+fails says so to its peers in the same collective that publishes the
+mappings, so every rank raises together instead of one of them waiting in
+the next barrier for a peer that has already given up.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 
 import torch
@@ -88,15 +97,40 @@ class _Ptr:
         return False
 
 
+def wait_device(stream: torch.cuda.Stream, what: str, timeout_s: float) -> None:
+    """Wait until the work queued on `stream` so far has finished, or raise
+    TimeoutError naming `what` after timeout_s (a device that never finishes
+    is reported, not waited on forever)."""
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    t0 = time.monotonic()
+    spin_until = t0 + 0.002
+    while not ev.query():
+        now = time.monotonic()
+        if now - t0 > timeout_s:
+            raise TimeoutError(f"p2p switch: device work before '{what}' not finished after {timeout_s:g} s")
+        if now > spin_until:
+            time.sleep(50e-6)
+
+
+def _sync_timeout_default() -> float:
+    return float(os.environ.get("SML_P2P_SYNC_TIMEOUT_S", "120"))
+
+
 class PeerSwitchAllReduce:
     """Reusable planes + peer mappings for repeated all-reduces of one bucket
     size.  Needs one GPU per rank (or ranks sharing one GPU, for tests) and a
     process group whose backend can all_reduce int8 and all_gather fp32
     tensors on the device ("nccl" = RCCL); with "gloo" those two small /
-    final collectives go through host memory (CPU tests of the plumbing)."""
+    final collectives go through host memory (CPU tests of the plumbing).
+    sync_timeout: seconds any host wait for this rank's device work may take
+    (default SML_P2P_SYNC_TIMEOUT_S or 120)."""
 
-    def __init__(self, numel: int, packet_numel: int = 256, device=None, group=None):
+    def __init__(self, numel: int, packet_numel: int = 256, device=None, group=None,
+                 sync_timeout: float | None = None):
         self.numel, self.P, self.group = numel, packet_numel, group
+        self.sync_timeout = _sync_timeout_default() if sync_timeout is None else float(sync_timeout)
+        self.peers = {}
         self.W = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.B = num_blocks(numel, packet_numel)
@@ -106,16 +140,34 @@ class PeerSwitchAllReduce:
         self.exps = torch.empty(self.B, dtype=torch.int8, device=self.dev)
         self.payload = torch.empty(self.B * packet_numel, dtype=torch.int32, device=self.dev)
         self.out_pad = torch.empty(self.W * self.S * packet_numel, dtype=torch.float32, device=self.dev)
-        torch.cuda.synchronize(self.dev)
-        mine = _handle_of(self.payload)
+        self.phases = None      # diagnostics: see SwitchSimAllReduce.phases
+        wait_device(torch.cuda.current_stream(self.dev), "publish planes", self.sync_timeout)
+        # publish this rank's plane; a rank that cannot export still takes
+        # part in the collective (with its error), so no peer waits on it
+        try:
+            mine = ("ok",) + _handle_of(self.payload)
+        except Exception as e:  # noqa: BLE001 - reported to every rank below
+            mine = ("error", repr(e)[:300], 0)
         allh = [None] * self.W
         dist.all_gather_object(allh, mine, group=group)
-        self.phases = None      # diagnostics: see SwitchSimAllReduce.phases
-        self.peers = {}
-        for w, (h, off) in enumerate(allh):
-            if w != self.rank:
-                self.peers[w] = _PeerPlane(h, off)
-        dist.barrier(group=group)
+        err = None
+        bad = [(w, h[1]) for w, h in enumerate(allh) if h[0] != "ok"]
+        if bad:
+            err = f"rank(s) could not export their plane: {bad}"
+        else:
+            try:
+                for w, (_, h, off) in enumerate(allh):
+                    if w != self.rank:
+                        self.peers[w] = _PeerPlane(h, off)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {self.rank} could not map a peer plane: {e!r}"[:300]
+        # agree on the outcome before anyone uses (or gives up on) the mappings
+        verdicts = [None] * self.W
+        dist.all_gather_object(verdicts, err, group=group)
+        errs = [v for v in verdicts if v]
+        if errs:
+            self._unmap()
+            raise RuntimeError("PeerSwitchAllReduce setup failed: " + "; ".join(errs))
 
     def _plane(self, w: int, blk0: int, nblk: int):
         if w == self.rank:
@@ -128,18 +180,20 @@ class PeerSwitchAllReduce:
         kernels that then read peer planes acquire (FLAG_PEER_PLANES)."""
         if release:
             release_to_peers(device=self.dev)
-        torch.cuda.current_stream(self.dev).synchronize()
+        wait_device(torch.cuda.current_stream(self.dev), "barrier", self.sync_timeout)
         dist.barrier(group=self.group)
 
     def _mark(self, name: str):
         if self.phases is not None:
-            torch.cuda.current_stream(self.dev).synchronize()
+            wait_device(torch.cuda.current_stream(self.dev), name, self.sync_timeout)
             self.phases[name] = time.perf_counter()
 
     def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """All-reduce (SUM) of a FLOAT32 bucket (quantized, as the exponent
         quantizer PPP does) or an INT32 bucket (byte order only: ppp.cc:158-190,
         262-298; no exponents, no extra batch)."""
+        if self.peers is None:
+            raise RuntimeError("PeerSwitchAllReduce is closed")
         if x.numel() != self.numel:
             raise ValueError("bucket size changed; build a new PeerSwitchAllReduce")
         if x.dtype not in (torch.float32, torch.int32):
@@ -193,11 +247,28 @@ class PeerSwitchAllReduce:
         self._mark("gather")
         return out
 
+    def _unmap(self) -> list:
+        """Close every peer mapping; return the errors (each is attempted)."""
+        errs = []
+        for w, p in self.peers.items():
+            try:
+                p.close()
+            except Exception as e:  # noqa: BLE001
+                errs.append(f"peer {w}: {e!r}"[:200])
+        self.peers = {}
+        return errs
+
     def close(self):
         """Unmap the peers' planes; collective (every rank calls it), so no
-        rank frees its own plane while a peer still has it mapped."""
-        torch.cuda.current_stream(self.dev).synchronize()
-        for p in self.peers.values():
-            p.close()
-        self.peers = {}
+        rank frees its own plane while a peer still has it mapped: this
+        rank's reads of the peers' planes are done before its mappings go,
+        and the closing barrier holds every plane until all peers have
+        unmapped it.  Idempotent."""
+        if self.peers is None:
+            return
+        wait_device(torch.cuda.current_stream(self.dev), "close", self.sync_timeout)
+        errs = self._unmap()
+        self.peers = None
         dist.barrier(group=self.group)
+        if errs:
+            raise RuntimeError("PeerSwitchAllReduce.close: " + "; ".join(errs))

@@ -164,7 +164,10 @@ def rank_main(a):
 
     dev = torch.device("cuda", a.device)
     torch.cuda.set_device(dev)
-    port = a.port
+    # rendezvous: a FileStore the launcher named (no port chosen by one
+    # process and bound by another later), or tcp on --port
+    inits = ([f"file://{a.init}", f"file://{a.init}.2"] if a.init else
+             [f"tcp://127.0.0.1:{a.port}", f"tcp://127.0.0.1:{a.port + 1}"])
     topo = None
     if a.switch_topo:
         # RCCL 7.2 runs AllReduce on CollNet only as CollNetDirect, which its
@@ -178,15 +181,14 @@ def rank_main(a):
         dump = os.path.join(a.topo_dir, f"detected.rank{a.rank}.xml")
         os.environ["NCCL_TOPO_DUMP_FILE"] = dump
         os.environ["NCCL_TOPO_DUMP_FILE_RANK"] = str(a.rank)
-        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=a.rank, world_size=a.world,
+        dist.init_process_group("nccl", init_method=inits.pop(0), rank=a.rank, world_size=a.world,
                                 device_id=dev)
         dist.destroy_process_group()
         del os.environ["NCCL_TOPO_DUMP_FILE"]
         topo = os.path.join(a.topo_dir, f"with_switch.rank{a.rank}.xml")
         add_switch_node(dump, topo)
         os.environ["NCCL_TOPO_FILE"] = topo
-        port += 1
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=a.rank, world_size=a.world,
+    dist.init_process_group("nccl", init_method=inits[0], rank=a.rank, world_size=a.world,
                             device_id=dev)
     out = {"rank": a.rank, "device": a.device, "topology_file": topo}
     W = a.world
@@ -295,17 +297,21 @@ def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, cha
         switch_topo = True
         extra_env = dict(extra_env or {}, SWITCHML_COLLNET_RCCL="1")
     session = uuid.uuid4().hex[:10]
-    port = port or (20000 + os.getpid() % 20000)
     if log_dir:
         os.makedirs(log_dir, exist_ok=True)
     import tempfile
     out_dir = log_dir or tempfile.mkdtemp(prefix="sml_rccl_collnet_")
+    # rendezvous through a FileStore in a fresh directory unless a port is
+    # asked for (a port picked here and bound by rank 0 later can be taken
+    # in between)
+    store_dir = tempfile.mkdtemp(prefix="sml_rccl_pg_")
+    rdzv = ["--port", str(port)] if port else ["--init", os.path.join(store_dir, "store")]
     procs, files = [], []
     for r in range(world):
         env = worker_env(os.environ, r, world, 0 if same_gpu else r, session, channels, algo, log_dir, extra_env)
         cmd = [sys.executable, "-u", "-m", "switchml_amd.rccl_collnet", "--rank", str(r), "--world", str(world),
-               "--device", str(0 if same_gpu else r), "--port", str(port), "--numel", str(numel),
-               "--iters", str(iters), "--topo-dir", out_dir]
+               "--device", str(0 if same_gpu else r), "--numel", str(numel),
+               "--iters", str(iters), "--topo-dir", out_dir] + rdzv
         if switch_topo:
             cmd.append("--switch-topo")
         f = open(os.path.join(out_dir, f"rank{r}.out"), "w+")
@@ -337,6 +343,8 @@ def launch(world: int, same_gpu: bool, numel: int = 1 << 22, iters: int = 5, cha
         time.sleep(0.2)
     for p in procs:
         p.wait()
+    import shutil
+    shutil.rmtree(store_dir, ignore_errors=True)
     outs = []
     for f in files:
         with open(f.name, errors="replace") as g:
@@ -371,6 +379,7 @@ def main(argv=None):
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--port", type=int, default=29655)
+    ap.add_argument("--init", default="", help="(rank) FileStore path for the rendezvous (instead of --port)")
     ap.add_argument("--numel", type=int, default=1 << 22)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--same-gpu", action="store_true")

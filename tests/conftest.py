@@ -11,6 +11,10 @@ for p in (ROOT, os.path.join(ROOT, "p4app-switchml_amd")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+    # heartbeats of long multi-process tests go past pytest's output capture
+    # (tests/mp_ranks.py heartbeat): a slow test stays visibly alive
+    import mp_ranks
+    mp_ranks.CAPTURE_MANAGER = config.pluginmanager.getplugin("capturemanager")
 
 
 @pytest.fixture(scope="session")

@@ -82,22 +82,44 @@ def test_bench_bucket_on_gpu_hashes_to_digest(cuda):
         assert bench.planes_sha256(torch, ex, pl, N, 256) == d["bucket_T1"][b]
 
 
-def test_switch_verdicts_fatal_only_for_switchsim_unless_strict():
-    """bench.py's N > 1 switch checks: a path that ran and gave
-    wrong bits fails the run for switchsim (always) and for the peer-memory
-    paths only with --strict-switch; a path that could not run is
-    diagnostic."""
+def test_switch_verdicts_wrong_bits_fatal_for_every_path():
+    """bench.py's N > 1 switch checks: a path that RAN and is
+    not verified fails the run, whichever path it is; a path that could not
+    run (error, timeout, missing) is diagnostic; --lenient-switch demotes
+    only the peer-memory paths' mismatch."""
     ok = {"verified": True, "within_quantization_bound": True, "timed_calls_equal_first": True}
     bad = {"verified": False, "within_quantization_bound": True, "timed_calls_equal_first": True,
            "bit_equal_to_switchsim": False}
     fields = {"switchsim": ok, "p2p_switch": bad, "xgmi_switch": {"error": "boom"}, "xgmi_switch_push": ok}
     fatal, diag = bench.switch_verdicts(fields)
+    assert len(fatal) == 1 and fatal[0].startswith("p2p_switch: not verified") and len(diag) == 1
+    assert diag[0].startswith("xgmi_switch: ") and "boom" in diag[0]
+    for k in ("xgmi_switch", "xgmi_switch_push"):
+        f2 = dict(fields, p2p_switch=ok, **{k: dict(bad, timed_calls_equal_first=False)})
+        fatal, diag = bench.switch_verdicts(f2)
+        assert [x.split(":")[0] for x in fatal] == [k]
+    fatal, diag = bench.switch_verdicts(fields, lenient=True)
     assert fatal == [] and len(diag) == 2
-    assert any(d.startswith("p2p_switch: not verified") for d in diag)
-    assert any(d.startswith("xgmi_switch: ") and "boom" in d for d in diag)
-    fatal, diag = bench.switch_verdicts(fields, strict=True)
-    assert len(fatal) == 1 and fatal[0].startswith("p2p_switch") and len(diag) == 1
-    fatal, _ = bench.switch_verdicts(dict(fields, switchsim=dict(bad, bit_equal_to_other_paths=False)))
+    fatal, _ = bench.switch_verdicts(dict(fields, switchsim=dict(bad, bit_equal_to_other_paths=False)),
+                                     lenient=True)
     assert len(fatal) == 1 and fatal[0].startswith("switchsim")
     fatal, diag = bench.switch_verdicts({})
     assert fatal == [] and len(diag) == 4
+    fatal, diag = bench.switch_verdicts({k: ok for k in bench.SWITCH_PATHS})
+    assert fatal == [] and diag == []
+
+
+def test_n_gt1_line_names_both_readings():
+    """at N > 1 the line carries the strong-scaling `value`
+    and the weak-scaling 256 MiB-per-GPU figure as a named top-level field
+    with its own roofline, and config.readings says which is which."""
+    wk = {"numel_per_gpu": 67_108_864, "buckets": 4, "ms_per_step": 0.0835, "value_GBps": 51_000.0,
+          "per_gpu_GBps": 6375.0, "kernel_ms": 0.0820, "kernel_GBps_per_gpu": 6550.0, "frac_per_gpu": 0.8188}
+    r = bench.weak_readings(wk, 8)
+    assert r["weak_256MiB_value"] == 51_000.0
+    w = r["weak_256MiB"]
+    assert w["scaling"] == "weak" and w["unit"] == "GB/s" and w["n_gpus"] == 8 and w["buckets_cycled"] == 4
+    assert w["roofline"]["frac"] == 0.8188 and w["roofline"]["peak"] == bench.HBM_PEAK_GBPS
+    assert set(r["readings"]) == {"value", "weak_256MiB_value"}
+    assert "strong" in r["readings"]["value"] and "weak" in r["readings"]["weak_256MiB_value"]
+    assert bench.weak_readings(wk, 1) == {} and bench.weak_readings({"error": "x"}, 8) == {}

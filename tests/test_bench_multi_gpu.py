@@ -1,0 +1,80 @@
+"""The driver's N > 1 bench command, observed by the GPU suite (VERDICT r4
+#2): `bench.py --gpus 2 --steps 4 --warmup 2` as a fresh child process on a
+one-GPU box, under SML_BENCH_REHEARSE=1 — both ranks on cuda:0, each an RCCL
+host of its own, so every collective runs in RCCL's kernels as on a node
+(bench.py main).  The line must parse and carry: n_gpus 2, the nccl (RCCL)
+backend, the headline's self-check against the committed digests, every
+switch path verified bit for bit (p4/exponents.p4:48-54,
+p4/processor.p4:48-54 via the oracle digests and the cross-path equality),
+both N > 1 readings, and a timed region that fits inside the child's wall
+time."""
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import pytest
+
+from mp_ranks import heartbeat
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def run_child(cmd, env, out_dir, timeout, what):
+    """Run `cmd` in its own session with stdout / stderr to files; heartbeat
+    every 20 s; kill the whole process group at the timeout.  Returns
+    (returncode, stdout text, stderr tail, wall seconds)."""
+    out_p, err_p = os.path.join(out_dir, "stdout"), os.path.join(out_dir, "stderr")
+    t0 = time.monotonic()
+    with open(out_p, "w") as fo, open(err_p, "w") as fe:
+        p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=fo, stderr=fe, start_new_session=True)
+        last = t0
+        while p.poll() is None:
+            now = time.monotonic()
+            if now - t0 > timeout:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                break
+            if now - last >= 20:
+                heartbeat(f"{what}: running for {now - t0:.0f} s")
+                last = now
+            time.sleep(0.5)
+    wall = time.monotonic() - t0
+    with open(out_p) as f:
+        out = f.read()
+    with open(err_p, errors="replace") as f:
+        err = f.read()[-3000:]
+    return p.returncode, out, err, wall
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_bench_n2_rehearsal_line(cuda, tmp_path):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+           and not k.startswith("TORCHELASTIC_")}
+    env["SML_BENCH_REHEARSE"] = "1"
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2"]
+    rc, out, err, wall = run_child(cmd, env, str(tmp_path), 800, "bench.py --gpus 2 (rehearsal)")
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert lines, f"no JSON line (rc {rc}); stderr tail:\n{err}"
+    line = json.loads(lines[-1])
+    assert rc == 0, (rc, line.get("failures"), line.get("diagnostic_failures"), err[-1500:])
+    assert line["n_gpus"] == 2 and line["steps"] == 4 and line["warmup"] == 2
+    assert line["config"]["process_group"]["backend"] == "nccl"
+    assert line["config"]["process_group"]["rehearsal"]
+    assert line["self_check"] is True and line["self_check_detail"]["buckets_checked_min_over_ranks"] == 4
+    for k in bench.SWITCH_PATHS:
+        assert line[k].get("verified") is True, (k, line[k])
+        assert line[k]["workers"] == 2
+    assert line["p2p_switch"]["bit_equal_to_switchsim"] and line["xgmi_switch"]["bit_equal_to_switchsim"]
+    assert line["ms_per_step"] * line["steps"] / 1e3 < wall
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    assert line["weak_256MiB_value"] > 0 and line["weak_256MiB"]["roofline"]["frac"] > 0
+    assert set(line["config"]["readings"]) == {"value", "weak_256MiB_value"}
+    assert line["scaling"] == "strong"

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from mp_ranks import collect
+from mp_ranks import spawn
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 with open(os.path.join(HERE, "golden", "digests.json")) as _f:
@@ -115,42 +115,37 @@ def test_oracle_reproduces_switch_digests(name):
     assert got == c["sha256"]
 
 
-def _switch_rank(rank, world, port, name, q):
+def _switch_rank(rank, world, init, name):
     """One worker of configs[3]'s switch simulation: its own 64 MiB bucket
     through SwitchSimAllReduce (K2 -> int8 MAX -> K3 -> int32 SUM -> K4) and
     PeerSwitchAllReduce (K2 -> int8 MAX -> K3 -> K6 over the peers' planes ->
     all_gather); digests of what this worker ends with."""
-    try:
-        from test_switchsim_dist import _init
-        dist = _init(rank, world, port)
-        import torch
-        import switchml_amd as sw
-        from switchml_amd.p2pswitch import PeerSwitchAllReduce
-        from switchml_amd.switchsim import SwitchSimAllReduce
-        m = _gen()
-        c = DIGESTS_SWITCH[name]
-        n, P = c["numel"], c["packet_numel"]
-        dev = torch.device("cuda:0")
-        x = torch.from_numpy(m.switch_input(c["gen"], c["seed"], rank, n)).to(dev)
-        ss = SwitchSimAllReduce(n, P, dev)
-        out = ss(x)
+    from test_switchsim_dist import _init
+    _init(rank, world, init)
+    import torch
+    import switchml_amd as sw
+    from switchml_amd.p2pswitch import PeerSwitchAllReduce
+    from switchml_amd.switchsim import SwitchSimAllReduce
+    m = _gen()
+    c = DIGESTS_SWITCH[name]
+    n, P = c["numel"], c["packet_numel"]
+    dev = torch.device("cuda:0")
+    x = torch.from_numpy(m.switch_input(c["gen"], c["seed"], rank, n)).to(dev)
+    ss = SwitchSimAllReduce(n, P, dev)
+    out = ss(x)
+    torch.cuda.synchronize()
+    got = {"global_exps": hashlib.sha256(ss.exps.cpu().numpy().tobytes()).hexdigest(),
+           # the exchange ran on host-order words; the switch's wire words are their byteswap
+           "payload": hashlib.sha256(sw.bswap_i32(ss.payload).cpu().numpy().tobytes()).hexdigest(),
+           "out": hashlib.sha256(m.canonical_nan(out.cpu().numpy()).tobytes()).hexdigest()}
+    del ss, out
+    ar = PeerSwitchAllReduce(n, P, dev)
+    for i in range(2):   # planes and peer mappings reused across calls
+        o2 = ar(x)
         torch.cuda.synchronize()
-        got = {"global_exps": hashlib.sha256(ss.exps.cpu().numpy().tobytes()).hexdigest(),
-               # the exchange ran on host-order words; the switch's wire words are their byteswap
-               "payload": hashlib.sha256(sw.bswap_i32(ss.payload).cpu().numpy().tobytes()).hexdigest(),
-               "out": hashlib.sha256(m.canonical_nan(out.cpu().numpy()).tobytes()).hexdigest()}
-        del ss, out
-        ar = PeerSwitchAllReduce(n, P, dev)
-        for i in range(2):   # planes and peer mappings reused across calls
-            o2 = ar(x)
-            torch.cuda.synchronize()
-            got[f"p2p_out_{i}"] = hashlib.sha256(m.canonical_nan(o2.cpu().numpy()).tobytes()).hexdigest()
-        ar.close()
-        q.put((rank, got, ""))
-        dist.destroy_process_group()
-    except Exception as ex:  # pragma: no cover - reported to the parent
-        import traceback
-        q.put((rank, None, traceback.format_exc()[-1500:]))
+        got[f"p2p_out_{i}"] = hashlib.sha256(m.canonical_nan(o2.cpu().numpy()).tobytes()).hexdigest()
+    ar.close()
+    return got
 
 
 @pytest.mark.gpu
@@ -162,17 +157,9 @@ def test_switch_sim_w8_reproduces_digests(cuda, name):
     — through the RCCL-style ring switch and through the peer-to-peer switch
     — hash to the oracle's digests (p4/exponents.p4:48-54,
     p4/processor.p4:48-54, ppp.cc:194-251)."""
-    import torch.multiprocessing as mp
-    from test_switchsim_dist import _free_port
     c = DIGESTS_SWITCH[name]
     world = c["num_workers"]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_switch_rank, args=(r, world, port, name, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = collect(q, procs, timeout=300, what=f"switch W={world} {name}")
+    res = spawn(_switch_rank, world, (name,), timeout=300, what=f"switch W={world} {name}")
     want = c["sha256"]
     for rank, got, err in res:
         assert got is not None, (rank, err)

@@ -139,6 +139,42 @@ int main(int argc, char** argv) {
         waitpid(p, &st, 0);
         return WIFEXITED(st) ? WEXITSTATUS(st) : 1;
     }
+    if (mode == "late_detach") {
+        // ADVICE r4: worker 1 detaches from communicator A AFTER worker 0 has
+        // closed A and created B under the same session.  Only worker 0
+        // removes the name, so B's segment survives and a fresh worker 1
+        // joins B; when worker 0 closes B, the name is gone.
+        int to_child[2], to_parent[2];
+        if (pipe(to_child) || pipe(to_parent)) return 9;
+        char c;
+        pid_t p = fork();
+        if (p == 0) {
+            {
+                JobOrder a(session, 1, 2, 20000);
+                if (write(to_parent[1], "a", 1) != 1) _exit(8);
+                if (read(to_child[0], &c, 1) != 1) _exit(8);     // B exists now
+            }                                                // late detach from A
+            if (write(to_parent[1], "d", 1) != 1) _exit(8);
+            _exit(0);
+        }
+        int st;
+        {
+            JobOrder a(session, 0, 2, 20000);
+            if (read(to_parent[0], &c, 1) != 1) return 7;   // worker 1 attached to A
+        }
+        JobOrder* b = new JobOrder(session, 0, 2, 20000);
+        if (write(to_child[1], "b", 1) != 1) return 7;
+        if (read(to_parent[0], &c, 1) != 1) return 7;       // worker 1 detached from A
+        waitpid(p, &st, 0);
+        pid_t q = fork();
+        if (q == 0) {
+            try { { JobOrder j(session, 1, 2, 2000); printf("joined B\n"); fflush(stdout); } _exit(0); }
+            catch (const std::exception& e) { printf("lost B: %s\n", e.what()); fflush(stdout); _exit(6); }
+        }
+        waitpid(q, &st, 0);
+        delete b;
+        return WIFEXITED(st) ? WEXITSTATUS(st) : 1;
+    }
     try {                                            // "join": a second leader for the session
         JobOrder o(session, 0, 2, 2000);
         printf("joined\n");
@@ -212,6 +248,16 @@ def test_reconnect_same_session(driver):
     r = subprocess.run([driver, "reconnect", session], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "starts with comm 1" in r.stdout
+    assert not os.path.exists(f"/dev/shm/switchml-collnet-{session}")
+
+
+def test_late_detach_keeps_the_new_segment(driver):
+    """a worker that detaches from an old communicator after
+    worker 0 has reconnected under the same session never removes the new
+    communicator's segment (worker 0 alone owns the name)."""
+    session = f"late-{os.getpid()}"
+    r = subprocess.run([driver, "late_detach", session], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "joined B" in r.stdout, r.stdout + r.stderr
     assert not os.path.exists(f"/dev/shm/switchml-collnet-{session}")
 
 

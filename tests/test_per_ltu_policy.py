@@ -36,10 +36,28 @@ def test_per_ltu_worker_is_built():
     assert os.access(BIN, os.X_OK), "build() makes bin/per_ltu_worker"
 
 
-@pytest.mark.gpu
-def test_reference_per_packet_caller_is_refused(cuda, tmp_path):
+def test_per_packet_worker_refused_at_setup(tmp_path):
+    """a per-packet worker asks the factory's policy at setup
+    (sml_ppp_per_ltu_calls / PrePostProcessor::PerLtuCalls), so the
+    reference's default name fails at configuration time — before any HIP
+    call or packet (this runs without a GPU) — naming the hooks to use."""
     r = subprocess.run([BIN, "cpu_exponent_quantizer", "70001", str(tmp_path / "o.f32")], capture_output=True,
                        text=True, timeout=120)
+    assert r.returncode == 3, r.stdout + r.stderr
+    assert r.stdout.startswith("REFUSED at setup:")
+    assert "hip_exponent_quantizer" in r.stdout and "PreprocessBurst" in r.stdout
+    assert not (tmp_path / "o.f32").exists()
+    r = subprocess.run([BIN, "gpu_magic", "70001", str(tmp_path / "o.f32")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 1 and "not a valid prepostprocessor" in r.stdout
+
+
+@pytest.mark.gpu
+def test_reference_per_packet_caller_is_refused(cuda, tmp_path):
+    """The data-path trap behind the setup check: a worker that skips it
+    still gets the PPP's refusal at its first packet."""
+    r = subprocess.run([BIN, "cpu_exponent_quantizer", "70001", str(tmp_path / "o.f32")], capture_output=True,
+                       text=True, timeout=120, env=dict(os.environ, PER_LTU_NO_SETUP_CHECK="1"))
     assert r.returncode == 3, r.stdout + r.stderr
     assert r.stdout.startswith("REFUSED PreprocessSingle:")
     assert "hip_exponent_quantizer" in r.stdout and "PreprocessBurst" in r.stdout

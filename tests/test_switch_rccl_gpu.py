@@ -26,7 +26,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from mp_ranks import collect
+from mp_ranks import init_pg, spawn
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HUGE = np.float32(1.5 * 2.0 ** 127)     # exponent field 254 -> e = 128 -> int8 -128 (ppp.cc:148-156)
@@ -96,96 +96,77 @@ def test_wrap_case_wraps_and_needs_signed_max(world, P):
     assert np.all(out[:P][np.arange(P) != 7] < 0)         # the wrapped positive sums come back negative
 
 
-def _rank(rank, world, port, session, net, n, P, digest_name, q):
-    try:
-        import sys
-        for p in (ROOT, os.path.join(ROOT, "p4app-switchml_amd")):
-            if p not in sys.path:
-                sys.path.insert(0, p)
-        from switchml_amd.rccl_collnet import same_gpu_rccl_env
-        os.environ.update(same_gpu_rccl_env(rank, session, net))
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        import torch
-        import torch.distributed as dist
-        dev = torch.device("cuda", 0)
-        torch.cuda.set_device(dev)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-        import switchml_amd as sw
-        from switchml_amd.p2pswitch import PeerSwitchAllReduce
-        from switchml_amd.switchsim import SwitchSimAllReduce
-        res = {"backend": dist.get_backend()}
+def _rank(rank, world, init, session, net, n, P, digest_name):
+    from switchml_amd.rccl_collnet import same_gpu_rccl_env
+    os.environ.update(same_gpu_rccl_env(rank, session, net))
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    init_pg("nccl", init, rank, world, device_id=dev)
+    import switchml_amd as sw
+    from switchml_amd.p2pswitch import PeerSwitchAllReduce
+    from switchml_amd.switchsim import SwitchSimAllReduce
+    res = {"backend": dist.get_backend()}
 
-        def u32(t):
-            return t.cpu().numpy().view(np.uint32)
+    def u32(t):
+        return t.cpu().numpy().view(np.uint32)
 
-        if digest_name is None:
-            xs = [wrap_case(r, world, n, P) for r in range(world)]
-            g, agg, ref = oracle_switch(xs, P)
-            x = torch.from_numpy(xs[rank]).to(dev)
-            ss = SwitchSimAllReduce(n, P, dev)
-            out = ss(x)
-            torch.cuda.synchronize()
-            res["ss_exps"] = bool(np.array_equal(ss.exps.cpu().numpy(), g))
-            res["ss_payload"] = bool(np.array_equal(u32(sw.bswap_i32(ss.payload)), agg))
-            res["ss_out"] = bool(np.array_equal(u32(out), ref.view(np.uint32)))
-            ar = PeerSwitchAllReduce(n, P, dev)
-            res["p2p_out"] = True
-            for _ in range(2):    # planes and peer mappings reused across calls
-                res["p2p_out"] &= bool(np.array_equal(u32(ar(x)), ref.view(np.uint32)))
-            res["p2p_exps"] = bool(np.array_equal(ar.exps.cpu().numpy(), g))
-            ar.close()
-            # INT32 buckets: htonl, the switch's wrapping sum, ntohl (ppp.cc:158-190, 262-298)
-            xi = [int32_wrap_case(r, n) for r in range(world)]
-            refi = O.bswap32(O.switch_payload([O.bswap32(v) for v in xi]))
-            ti = torch.from_numpy(xi[rank]).to(dev)
-            res["ss_int32"] = bool(np.array_equal(u32(SwitchSimAllReduce(n, P, dev)(ti)), refi))
-            ar = PeerSwitchAllReduce(n, P, dev)
-            res["p2p_int32"] = bool(np.array_equal(u32(ar(ti)), refi))
-            ar.close()
-        else:
-            import importlib.util
-            import json
-            gd = os.path.join(ROOT, "tests", "golden")
-            spec = importlib.util.spec_from_file_location("make_digests", os.path.join(gd, "make_digests.py"))
-            m = importlib.util.module_from_spec(spec)
-            spec.loader.exec_module(m)
-            with open(os.path.join(gd, "digests_switch.json")) as f:
-                c = json.load(f)[digest_name]
-            x = torch.from_numpy(m.switch_input(c["gen"], c["seed"], rank, n)).to(dev)
-            want = c["sha256"]
+    if digest_name is None:
+        xs = [wrap_case(r, world, n, P) for r in range(world)]
+        g, agg, ref = oracle_switch(xs, P)
+        x = torch.from_numpy(xs[rank]).to(dev)
+        ss = SwitchSimAllReduce(n, P, dev)
+        out = ss(x)
+        torch.cuda.synchronize()
+        res["ss_exps"] = bool(np.array_equal(ss.exps.cpu().numpy(), g))
+        res["ss_payload"] = bool(np.array_equal(u32(sw.bswap_i32(ss.payload)), agg))
+        res["ss_out"] = bool(np.array_equal(u32(out), ref.view(np.uint32)))
+        ar = PeerSwitchAllReduce(n, P, dev)
+        res["p2p_out"] = True
+        for _ in range(2):    # planes and peer mappings reused across calls
+            res["p2p_out"] &= bool(np.array_equal(u32(ar(x)), ref.view(np.uint32)))
+        res["p2p_exps"] = bool(np.array_equal(ar.exps.cpu().numpy(), g))
+        ar.close()
+        # INT32 buckets: htonl, the switch's wrapping sum, ntohl (ppp.cc:158-190, 262-298)
+        xi = [int32_wrap_case(r, n) for r in range(world)]
+        refi = O.bswap32(O.switch_payload([O.bswap32(v) for v in xi]))
+        ti = torch.from_numpy(xi[rank]).to(dev)
+        res["ss_int32"] = bool(np.array_equal(u32(SwitchSimAllReduce(n, P, dev)(ti)), refi))
+        ar = PeerSwitchAllReduce(n, P, dev)
+        res["p2p_int32"] = bool(np.array_equal(u32(ar(ti)), refi))
+        ar.close()
+    else:
+        import importlib.util
+        import json
+        gd = os.path.join(ROOT, "tests", "golden")
+        spec = importlib.util.spec_from_file_location("make_digests", os.path.join(gd, "make_digests.py"))
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        with open(os.path.join(gd, "digests_switch.json")) as f:
+            c = json.load(f)[digest_name]
+        x = torch.from_numpy(m.switch_input(c["gen"], c["seed"], rank, n)).to(dev)
+        want = c["sha256"]
 
-            def sha(a):
-                return hashlib.sha256(a.tobytes()).hexdigest()
+        def sha(a):
+            return hashlib.sha256(a.tobytes()).hexdigest()
 
-            ss = SwitchSimAllReduce(n, P, dev)
-            out = ss(x)
-            torch.cuda.synchronize()
-            res["ss_exps"] = sha(ss.exps.cpu().numpy()) == want["global_exps"]
-            res["ss_payload"] = sha(sw.bswap_i32(ss.payload).cpu().numpy()) == want["payload"]
-            res["ss_out"] = sha(m.canonical_nan(out.cpu().numpy())) == want["out"]
-            del ss, out
-            ar = PeerSwitchAllReduce(n, P, dev)
-            res["p2p_out"] = all(sha(m.canonical_nan(ar(x).cpu().numpy())) == want["out"] for _ in range(2))
-            ar.close()
-        q.put((rank, res, ""))
-        dist.destroy_process_group()
-    except Exception:  # pragma: no cover - reported to the parent
-        import traceback
-        q.put((rank, None, traceback.format_exc()[-2000:]))
+        ss = SwitchSimAllReduce(n, P, dev)
+        out = ss(x)
+        torch.cuda.synchronize()
+        res["ss_exps"] = sha(ss.exps.cpu().numpy()) == want["global_exps"]
+        res["ss_payload"] = sha(sw.bswap_i32(ss.payload).cpu().numpy()) == want["payload"]
+        res["ss_out"] = sha(m.canonical_nan(out.cpu().numpy())) == want["out"]
+        del ss, out
+        ar = PeerSwitchAllReduce(n, P, dev)
+        res["p2p_out"] = all(sha(m.canonical_nan(ar(x).cpu().numpy())) == want["out"] for _ in range(2))
+        ar.close()
+    return res
 
 
 def _run(world, n, P, net, digest_name=None, timeout=300):
-    import torch.multiprocessing as mp
-    from test_switchsim_dist import _free_port
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port, session = _free_port(), uuid.uuid4().hex[:8]
-    procs = [ctx.Process(target=_rank, args=(r, world, port, session, net, n, P, digest_name, q))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    res = collect(q, procs, timeout=timeout, what=f"rccl switch W={world} {net}")
+    res = spawn(_rank, world, (uuid.uuid4().hex[:8], net, n, P, digest_name), timeout=timeout,
+                what=f"rccl switch W={world} {net}")
     for rank, r, err in res:
         assert r is not None, (rank, err)
         assert r.pop("backend") == "nccl"

@@ -11,39 +11,21 @@ all-reduce — K2, exchange, K3, exchange, K4 — bit-exact against the oracle's
 lockstep W-worker restatement.
 """
 import os
-import socket
+import time
 
 import numpy as np
 import pytest
 import torch
-import torch.multiprocessing as mp
 
 from oracle import oracle as O
-from mp_ranks import collect
+from mp_ranks import init_pg, spawn
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _init(rank, world, port):
-    import sys
-    for p in (ROOT, os.path.join(ROOT, "p4app-switchml_amd")):
-        if p not in sys.path:
-            sys.path.insert(0, p)
-    import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    import datetime
-    # a rank blocked on a failed peer raises instead of waiting gloo's 30 min
-    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
-    return dist
+def _init(rank, world, init):
+    """gloo over the test's FileStore (tests/mp_ranks.py), 120 s timeout."""
+    return init_pg("gloo", init, rank, world)
 
 
 def worker_data(rank, n):
@@ -51,120 +33,88 @@ def worker_data(rank, n):
     return O.splitmix_normal(1000 + rank, n) * np.float32(4.0 ** (rank - 1))
 
 
-def _cpu_exchange(rank, world, port, n, P, q):
-    try:
-        dist = _init(rank, world, port)
-        from switchml_amd import switchsim
-        xs = [worker_data(r, n) for r in range(world)]
-        local_exps = [O.exponents(x, P) for x in xs]
-        e = torch.from_numpy(local_exps[rank].copy())
-        switchsim.exchange_exponents(e)
-        g = O.switch_exps(local_exps)
-        ok_e = np.array_equal(e.numpy(), g)
-        pls_be = [O.quantize(x, P, world, global_exps=g) for x in xs]
-        le = torch.from_numpy(O.bswap32(pls_be[rank]).view(np.int32).copy())
-        switchsim.exchange_payload(le)
-        agg_be = O.switch_payload(pls_be)
-        ok_p = np.array_equal(O.bswap32(le.numpy().view(np.uint32)), agg_be)
-        out = O.dequantize(agg_be, g, n, P, world)
-        ref = np.sum(np.stack(xs).astype(np.float64), axis=0)
-        rel = np.max(np.abs(out - ref)) / np.max(np.abs(ref))
-        q.put((rank, ok_e, ok_p, float(rel)))
-        dist.destroy_process_group()
-    except Exception as ex:  # pragma: no cover - reported to the parent
-        q.put((rank, False, False, repr(ex)))
+def _cpu_exchange(rank, world, init, n, P):
+    dist = _init(rank, world, init)
+    from switchml_amd import switchsim
+    xs = [worker_data(r, n) for r in range(world)]
+    local_exps = [O.exponents(x, P) for x in xs]
+    e = torch.from_numpy(local_exps[rank].copy())
+    switchsim.exchange_exponents(e)
+    g = O.switch_exps(local_exps)
+    ok_e = np.array_equal(e.numpy(), g)
+    pls_be = [O.quantize(x, P, world, global_exps=g) for x in xs]
+    le = torch.from_numpy(O.bswap32(pls_be[rank]).view(np.int32).copy())
+    switchsim.exchange_payload(le)
+    agg_be = O.switch_payload(pls_be)
+    ok_p = np.array_equal(O.bswap32(le.numpy().view(np.uint32)), agg_be)
+    out = O.dequantize(agg_be, g, n, P, world)
+    ref = np.sum(np.stack(xs).astype(np.float64), axis=0)
+    rel = np.max(np.abs(out - ref)) / np.max(np.abs(ref))
+    return {"exps": bool(ok_e), "payload": bool(ok_p), "rel": float(rel)}
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_exchange_gloo_cpu(world):
     n, P = 20_011, 256
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_cpu_exchange, args=(r, world, port, n, P, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = collect(q, procs, timeout=120)
-    for rank, ok_e, ok_p, rel in res:
-        assert ok_e and ok_p, (rank, rel)
-        assert rel < 1e-6
+    for rank, r, err in spawn(_cpu_exchange, world, (n, P), timeout=120):
+        assert r["exps"] and r["payload"], (rank, r)
+        assert r["rel"] < 1e-6
 
 
-def _gpu_switchsim(rank, world, port, n, P, q):
-    try:
-        dist = _init(rank, world, port)
-        from switchml_amd import switchsim
-        dev = torch.device("cuda:0")
-        x = worker_data(rank, n)
-        out = switchsim.allreduce(torch.from_numpy(x).to(dev), P)
-        xs = [worker_data(r, n) for r in range(world)]
-        g = O.switch_exps([O.exponents(xx, P) for xx in xs])
-        agg = O.switch_payload([O.quantize(xx, P, world, global_exps=g) for xx in xs])
-        ref = O.dequantize(agg, g, n, P, world)
-        ok = np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
-        q.put((rank, ok, ""))
-        dist.destroy_process_group()
-    except Exception as ex:  # pragma: no cover
-        q.put((rank, False, repr(ex)))
+def _gpu_switchsim(rank, world, init, n, P):
+    _init(rank, world, init)
+    from switchml_amd import switchsim
+    dev = torch.device("cuda:0")
+    x = worker_data(rank, n)
+    out = switchsim.allreduce(torch.from_numpy(x).to(dev), P)
+    xs = [worker_data(r, n) for r in range(world)]
+    g = O.switch_exps([O.exponents(xx, P) for xx in xs])
+    agg = O.switch_payload([O.quantize(xx, P, world, global_exps=g) for xx in xs])
+    ref = O.dequantize(agg, g, n, P, world)
+    return bool(np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32)))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("P", [64, 256, 1024])
 def test_switchsim_allreduce_two_workers_one_gpu(cuda, P):
-    world, n = 2, 100_003
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_gpu_switchsim, args=(r, world, port, n, P, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = collect(q, procs, timeout=240)
-    for rank, ok, err in res:
+    for rank, ok, err in spawn(_gpu_switchsim, 2, (100_003, P)):
         assert ok, (rank, err)
 
 
-def _gpu_p2p(rank, world, port, n, P, q):
-    try:
-        dist = _init(rank, world, port)
-        from switchml_amd.p2pswitch import PeerSwitchAllReduce
-        dev = torch.device("cuda:0")
-        xs = [worker_data(r, n) for r in range(world)]
-        g = O.switch_exps([O.exponents(xx, P) for xx in xs])
-        agg = O.switch_payload([O.quantize(xx, P, world, global_exps=g) for xx in xs])
-        ref = O.dequantize(agg, g, n, P, world)
-        ar = PeerSwitchAllReduce(n, P, dev)
-        x = torch.from_numpy(xs[rank]).to(dev)
-        ok = True
-        for _ in range(2):   # planes and peer mappings are reused across calls
-            out = ar(x)
-            ok = ok and np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
-        ar.close()
-        q.put((rank, ok, ""))
-        dist.destroy_process_group()
-    except Exception as ex:  # pragma: no cover
-        q.put((rank, False, repr(ex)))
+def _gpu_p2p(rank, world, init, n, P):
+    _init(rank, world, init)
+    from switchml_amd.p2pswitch import PeerSwitchAllReduce
+    dev = torch.device("cuda:0")
+    xs = [worker_data(r, n) for r in range(world)]
+    g = O.switch_exps([O.exponents(xx, P) for xx in xs])
+    agg = O.switch_payload([O.quantize(xx, P, world, global_exps=g) for xx in xs])
+    ref = O.dequantize(agg, g, n, P, world)
+    ar = PeerSwitchAllReduce(n, P, dev)
+    x = torch.from_numpy(xs[rank]).to(dev)
+    ok = True
+    for _ in range(2):   # planes and peer mappings are reused across calls
+        out = ar(x)
+        ok = ok and np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    ar.close()
+    return bool(ok)
 
 
-def _gpu_p2p_int32(rank, world, port, n, P, q):
-    try:
-        dist = _init(rank, world, port)
-        from switchml_amd.p2pswitch import PeerSwitchAllReduce
-        from switchml_amd.switchsim import SwitchSimAllReduce
-        dev = torch.device("cuda:0")
-        xs = [np.random.default_rng(77 + r).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
-              for r in range(world)]
-        # INT32 jobs: htonl per word, the switch's wrapping bit<32> sum, ntohl (ppp.cc:158-190, 262-298)
-        ref = O.bswap32(O.switch_payload([O.bswap32(xx) for xx in xs]))
-        ar = PeerSwitchAllReduce(n, P, dev)
-        out = ar(torch.from_numpy(xs[rank]).to(dev))
-        ok = np.array_equal(out.cpu().numpy().view(np.uint32), ref)
-        ar.close()
-        out2 = SwitchSimAllReduce(n, P, dev)(torch.from_numpy(xs[rank]).to(dev))
-        ok = ok and np.array_equal(out2.cpu().numpy().view(np.uint32), ref)
-        q.put((rank, ok, ""))
-        dist.destroy_process_group()
-    except Exception as ex:  # pragma: no cover
-        q.put((rank, False, repr(ex)))
+def _gpu_p2p_int32(rank, world, init, n, P):
+    _init(rank, world, init)
+    from switchml_amd.p2pswitch import PeerSwitchAllReduce
+    from switchml_amd.switchsim import SwitchSimAllReduce
+    dev = torch.device("cuda:0")
+    xs = [np.random.default_rng(77 + r).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+          for r in range(world)]
+    # INT32 jobs: htonl per word, the switch's wrapping bit<32> sum, ntohl (ppp.cc:158-190, 262-298)
+    ref = O.bswap32(O.switch_payload([O.bswap32(xx) for xx in xs]))
+    ar = PeerSwitchAllReduce(n, P, dev)
+    out = ar(torch.from_numpy(xs[rank]).to(dev))
+    ok = np.array_equal(out.cpu().numpy().view(np.uint32), ref)
+    ar.close()
+    out2 = SwitchSimAllReduce(n, P, dev)(torch.from_numpy(xs[rank]).to(dev))
+    ok = ok and np.array_equal(out2.cpu().numpy().view(np.uint32), ref)
+    return bool(ok)
 
 
 @pytest.mark.gpu
@@ -172,14 +122,7 @@ def _gpu_p2p_int32(rank, world, port, n, P, q):
 def test_p2p_switch_int32_ranks_one_gpu(cuda, world, n, P):
     """INT32 buckets through the peer-to-peer switch and the ring switch-sim:
     wrapping sum, bit-exact."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_gpu_p2p_int32, args=(r, world, port, n, P, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = collect(q, procs, timeout=240)
-    for rank, ok, err in res:
+    for rank, ok, err in spawn(_gpu_p2p_int32, world, (n, P)):
         assert ok, (rank, err)
 
 
@@ -191,14 +134,7 @@ def test_p2p_switch_ranks_one_gpu(cuda, world, n, P):
     and aggregates its shard of blocks with K6; bit-exact vs the oracle switch.
     All ranks share cuda:0 here (IPC within one device); on a node each rank's
     peers are other GPUs reached over xGMI."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_gpu_p2p, args=(r, world, port, n, P, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = collect(q, procs, timeout=240)
-    for rank, ok, err in res:
+    for rank, ok, err in spawn(_gpu_p2p, world, (n, P)):
         assert ok, (rank, err)
 
 
@@ -208,35 +144,29 @@ def test_p2p_switch_ranks_one_gpu(cuda, world, n, P):
 def test_fifo_slice_matches_oracle(numel, T):
     """switchml_amd.fifo_slice (the multi-GPU shard rule) == the oracle's
     restatement of fifo_scheduler.cc:93-109."""
-    import sys
-    sys.path.insert(0, os.path.join(ROOT, "p4app-switchml_amd"))
     import switchml_amd as sw
     for t in range(T):
         assert sw.fifo_slice(numel, T, t) == O.slice_geometry(numel, T, t)
 
 
-def _gpu_shard(rank, world, port, n, P, q):
-    try:
-        dist = _init(rank, world, port)
-        import switchml_amd as sw
-        x = O.splitmix_normal(77, n)                     # the same job on every rank
-        job = torch.from_numpy(x).to("cuda:0")
-        off, payload, exps = sw.shard_quantize_pack(job, rank, world, P)
-        torch.cuda.synchronize()
-        # gather every rank's planes (gloo, CPU tensors) to check them together
-        got = [None] * world
-        dist.all_gather_object(got, (off, payload.cpu().numpy(), exps.cpu().numpy()))
-        ok = True
-        for t, (o, pl, ex) in enumerate(got):
-            ro, rn = O.slice_geometry(n, world, t)
-            sl = x[ro:ro + rn]
-            ok &= o == ro
-            ok &= np.array_equal(pl.view(np.uint32), O.quantize(sl, P))
-            ok &= np.array_equal(ex, O.exponents(sl, P))
-        q.put((rank, bool(ok), ""))
-        dist.destroy_process_group()
-    except Exception as ex:  # pragma: no cover
-        q.put((rank, False, repr(ex)))
+def _gpu_shard(rank, world, init, n, P):
+    dist = _init(rank, world, init)
+    import switchml_amd as sw
+    x = O.splitmix_normal(77, n)                     # the same job on every rank
+    job = torch.from_numpy(x).to("cuda:0")
+    off, payload, exps = sw.shard_quantize_pack(job, rank, world, P)
+    torch.cuda.synchronize()
+    # gather every rank's planes (gloo, CPU tensors) to check them together
+    got = [None] * world
+    dist.all_gather_object(got, (off, payload.cpu().numpy(), exps.cpu().numpy()))
+    ok = True
+    for t, (o, pl, ex) in enumerate(got):
+        ro, rn = O.slice_geometry(n, world, t)
+        sl = x[ro:ro + rn]
+        ok &= o == ro
+        ok &= np.array_equal(pl.view(np.uint32), O.quantize(sl, P))
+        ok &= np.array_equal(ex, O.exponents(sl, P))
+    return bool(ok)
 
 
 @pytest.mark.gpu
@@ -247,15 +177,7 @@ def test_sharding_mode_ranks_one_gpu(cuda, world):
     with num_worker_threads = world (blocks restart at every slice start).
     Ranks share one MI355X here (gloo); the driver's multi-GPU bench runs the
     same per-rank work on one GPU per rank."""
-    n, P = 100_003, 256
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_gpu_shard, args=(r, world, port, n, P, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = collect(q, procs, timeout=240)
-    for rank, ok, err in res:
+    for rank, ok, err in spawn(_gpu_shard, world, (100_003, 256)):
         assert ok, (rank, err)
 
 
@@ -272,38 +194,27 @@ def test_p2p_shards_tile_the_blocks(B, world):
     assert nxt == B
 
 
-def _nccl_p2p(rank, world, port, n, P, q):
+def _nccl_p2p(rank, world, init, n, P):
     """One GPU per rank, RCCL (backend "nccl"): the production shape of both
     switches — device all_reduce / all_gather, K6 reading the peers' planes
     over xGMI through hipIpc mappings."""
-    try:
-        import sys
-        for p in (ROOT, os.path.join(ROOT, "p4app-switchml_amd")):
-            if p not in sys.path:
-                sys.path.insert(0, p)
-        import torch.distributed as dist
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dev = torch.device("cuda", rank)
-        torch.cuda.set_device(dev)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-        from switchml_amd.p2pswitch import PeerSwitchAllReduce
-        from switchml_amd.switchsim import SwitchSimAllReduce
-        xs = [worker_data(r, n) for r in range(world)]
-        g = O.switch_exps([O.exponents(xx, P) for xx in xs])
-        agg = O.switch_payload([O.quantize(xx, P, world, global_exps=g) for xx in xs])
-        ref = O.dequantize(agg, g, n, P, world)
-        x = torch.from_numpy(xs[rank]).to(dev)
-        ok = np.array_equal(SwitchSimAllReduce(n, P, dev)(x).cpu().numpy().view(np.uint32), ref.view(np.uint32))
-        ar = PeerSwitchAllReduce(n, P, dev)
-        for _ in range(2):
-            out = ar(x)
-            ok = ok and np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
-        ar.close()
-        q.put((rank, ok, ""))
-        dist.destroy_process_group()
-    except Exception as ex:  # pragma: no cover
-        q.put((rank, False, repr(ex)))
+    dev = torch.device("cuda", rank)
+    torch.cuda.set_device(dev)
+    init_pg("nccl", init, rank, world, device_id=dev)
+    from switchml_amd.p2pswitch import PeerSwitchAllReduce
+    from switchml_amd.switchsim import SwitchSimAllReduce
+    xs = [worker_data(r, n) for r in range(world)]
+    g = O.switch_exps([O.exponents(xx, P) for xx in xs])
+    agg = O.switch_payload([O.quantize(xx, P, world, global_exps=g) for xx in xs])
+    ref = O.dequantize(agg, g, n, P, world)
+    x = torch.from_numpy(xs[rank]).to(dev)
+    ok = np.array_equal(SwitchSimAllReduce(n, P, dev)(x).cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    ar = PeerSwitchAllReduce(n, P, dev)
+    for _ in range(2):
+        out = ar(x)
+        ok = ok and np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    ar.close()
+    return bool(ok)
 
 
 @pytest.mark.gpu
@@ -316,13 +227,56 @@ def test_p2p_switch_nccl_multi_gpu(cuda, n, P):
     ndev = torch.cuda.device_count()
     if ndev < 2:
         pytest.skip("needs >= 2 GPUs (one per rank)")
-    world = min(ndev, 8)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_nccl_p2p, args=(r, world, port, n, P, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = collect(q, procs, timeout=240)
-    for rank, ok, err in res:
+    for rank, ok, err in spawn(_nccl_p2p, min(ndev, 8), (n, P)):
         assert ok, (rank, err)
+
+
+def _gpu_p2p_setup_failure(rank, world, init, n, P, where):
+    """Rank 1 cannot export (where="export") or map (where="map") a plane:
+    every rank must raise the same setup error promptly — none may be left
+    waiting in a barrier for a peer that has given up — and the process
+    group must still work afterwards."""
+    dist = _init(rank, world, init)
+    from switchml_amd import p2pswitch
+    dev = torch.device("cuda:0")
+    saved = (p2pswitch._handle_of, p2pswitch._PeerPlane)
+    if rank == 1:
+        def boom(*a, **k):
+            raise RuntimeError(f"injected {where} failure")
+        if where == "export":
+            p2pswitch._handle_of = boom
+        else:
+            p2pswitch._PeerPlane = boom
+    t0 = time.monotonic()
+    try:
+        p2pswitch.PeerSwitchAllReduce(n, P, dev)
+        return {"raised": False}
+    except RuntimeError as e:
+        msg = str(e)
+    took = time.monotonic() - t0
+    p2pswitch._handle_of, p2pswitch._PeerPlane = saved
+    dist.barrier()
+    # a good instance after the failed one: closes twice, refuses calls once closed
+    ar = p2pswitch.PeerSwitchAllReduce(n, P, dev)
+    ar.close()
+    ar.close()
+    closed_ok = False
+    try:
+        ar(torch.zeros(n, device=dev))
+    except RuntimeError:
+        closed_ok = True
+    return {"raised": "setup failed" in msg and "injected" in msg and "rank" in msg,
+            "prompt": took < 30.0, "closed_ok": closed_ok}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", ["export", "map"])
+def test_p2p_setup_failure_is_collective(cuda, where):
+    """a peer-memory setup failure on one rank is an error on
+    every rank (agreed in one collective), not a rank that dies or a peer
+    blocked in the next barrier."""
+    world = 2 if where == "export" else 3      # "map": ranks 0 and 2 map fine and must still raise
+    res = spawn(_gpu_p2p_setup_failure, world, (100_003, 256, where), timeout=120)
+    for rank, r, err in res:
+        assert r is not None, (rank, err)
+        assert r["raised"] and r["prompt"] and r["closed_ok"], (rank, r)
