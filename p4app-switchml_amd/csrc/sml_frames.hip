@@ -215,8 +215,13 @@ typedef uint32_t u3a __attribute__((ext_vector_type(3), aligned(4)));
 
 __device__ __forceinline__ RxHdr rx_header(const RxArgs& a, uint64_t f) {
     // one 12-byte load for dwords 10..12 (the compiler otherwise sinks the
-    // dword-12 load behind the job / range check: two round trips)
-    const u3a hv = __builtin_nontemporal_load(reinterpret_cast<const u3a*>(a.frames + f * a.stride + 40));
+    // dword-12 load behind the job / range check: two round trips).  Default
+    // cache policy, not non-temporal: the 128-byte line it fetches also holds
+    // the first payload bytes (offset 52), which the apply pass reads next —
+    // kept in the caches, that line is not fetched from HBM a second time
+    // (cold frame sets: 94.7 -> 91.0 us per 256 MiB rx call,
+    // profiles/r05/ab_rx_claim_policy.json).
+    const u3a hv = *reinterpret_cast<const u3a*>(a.frames + f * a.stride + 40);
     const uint32_t d10 = hv.x, d11 = hv.y, d12 = hv.z;
     RxHdr r;
     r.pid = d11;

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
-"""Frames tx + rx on the 256 MiB bucket, for rocprofv3 --kernel-trace --stats:
-quantize into DPDK frames (device), then the receive side over the same
-frames (W = 1 loopback), `reps` times each.  Prints wall-clock rates."""
+"""Frames tx + rx on the 256 MiB bucket, for rocprofv3 --kernel-trace --stats
+and the PMC passes: quantize into DPDK frames (device), then the receive side
+over the same frames (W = 1 loopback), `reps` times each, cycling `sets`
+distinct frame sets and rx slices (4 = 1.1 GB of frames, past the 256 MiB
+Infinity Cache: a receive stream's HBM-proper pattern, as bench.py's
+`frames_*_4sets` fields; 1 = one re-read set).  Prints wall-clock rates."""
 import json
 import os
 import sys
@@ -14,7 +17,7 @@ import torch  # noqa: E402
 import switchml_amd as sw  # noqa: E402
 
 
-def main(N=64 * 2 ** 20, P=256, bm=64, reps=20):
+def main(N=64 * 2 ** 20, P=256, bm=64, reps=20, sets=int(os.environ.get("FRAME_SETS", "4"))):
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(42)
@@ -22,13 +25,26 @@ def main(N=64 * 2 ** 20, P=256, bm=64, reps=20):
     B = sw.num_blocks(N, P)
     F = B + min(B, bm)
     fb = F * sw.frame_bytes(P)
-    frames = torch.empty(fb, dtype=torch.uint8, device=dev)
+    frames = [torch.empty(fb, dtype=torch.uint8, device=dev) for _ in range(sets)]
     fp = sw.frame_params(max_outstanding_pkts=bm)
-    rx = sw.RxSlice(N, P, bm, device=dev)
-    res = {}
-    for name, fn in (("tx", lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=bm, frames=frames)),
-                     ("rx", lambda: (rx.reset(), sw.dequantize_frames(frames, F, rx)))):
-        fn()
+    rxs = [sw.RxSlice(N, P, bm, device=dev) for _ in range(sets)]
+    k = [0]
+
+    def tx():
+        sw.quantize_pack_frames(x, fp, P, 1, batch_max=bm, frames=frames[k[0] % sets])
+        k[0] += 1
+
+    def rx():
+        r = rxs[k[0] % sets]
+        r.reset()
+        sw.dequantize_frames(frames[k[0] % sets], F, r)
+        k[0] += 1
+
+    res = {"frame_sets": sets}
+    for name, fn in (("tx", tx), ("rx", rx)):
+        k[0] = 0
+        for _ in range(sets):
+            fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -38,7 +54,7 @@ def main(N=64 * 2 ** 20, P=256, bm=64, reps=20):
         res[name] = {"us": round(t * 1e6, 1), "GBps": round((4 * N + fb) / t / 1e9, 1)}
     ref = sw.roundtrip_loopback(x, P, 1)
     torch.cuda.synchronize()
-    res["rx_equals_roundtrip"] = bool(torch.equal(ref.view(torch.int32), rx.out.view(torch.int32)))
+    res["rx_equals_roundtrip"] = all(bool(torch.equal(ref.view(torch.int32), r.out.view(torch.int32))) for r in rxs)
     print(json.dumps(res))
 
 
