@@ -280,3 +280,48 @@ def test_p2p_setup_failure_is_collective(cuda, where):
     for rank, r, err in res:
         assert r is not None, (rank, err)
         assert r["raised"] and r["prompt"] and r["closed_ok"], (rank, r)
+
+
+def _ipc_failure_paths(rank, world, init, n):
+    """The hipIpc calls of the p2p switch on their failure paths (VERDICT r4
+    #1: every failure returns an error, none kills the process or blocks):
+    an all-zero handle, a handle whose exporting process has exited, and a
+    close of a pointer that was never opened.  Rank 0 exports a plane and
+    exits; rank 1 opens the handle only after rank 0 is gone."""
+    import ctypes
+    dist = _init(rank, world, init)
+    import switchml_amd as sw
+    from switchml_amd.p2pswitch import _handle_of
+    L = sw.lib()
+    dev = torch.device("cuda:0")
+    plane = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    got = [None] * world
+    dist.all_gather_object(got, _handle_of(plane) if rank == 0 else None)
+    if rank == 0:
+        dist.barrier()
+        return {"exported": True}      # rank_entry reports, tears down and the process exits
+    h, off = got[0]
+    res = {}
+    base = ctypes.c_void_p()
+    zero = (ctypes.c_uint8 * L.sml_ipc_handle_bytes())()
+    res["zero_handle_status"] = int(L.sml_ipc_open_handle(zero, ctypes.byref(base)))
+    res["bad_close_status"] = int(L.sml_ipc_close_handle(ctypes.c_void_p(0x1000)))
+    dist.barrier()                     # rank 0 has its result out and is leaving
+    time.sleep(5.0)                    # ... and is gone
+    buf = (ctypes.c_uint8 * len(h)).from_buffer_copy(h)
+    st = int(L.sml_ipc_open_handle(buf, ctypes.byref(base)))
+    res["dead_exporter_status"] = st
+    if st == 0:                        # mapped after all (the buffer outlived its exporter): unmap cleanly
+        res["dead_exporter_close_status"] = int(L.sml_ipc_close_handle(base))
+    res["error_text"] = L.sml_last_error().decode()[:200]
+    return res
+
+
+@pytest.mark.gpu
+def test_ipc_failure_paths_return_errors(cuda):
+    res = spawn(_ipc_failure_paths, 2, (1 << 20,), timeout=120)
+    r1 = [r for rank, r, _ in res if rank == 1][0]
+    assert r1["zero_handle_status"] != 0, r1
+    assert r1["bad_close_status"] != 0, r1
+    assert r1["dead_exporter_status"] != 0 or r1["dead_exporter_close_status"] == 0, r1
