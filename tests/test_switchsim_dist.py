@@ -18,7 +18,7 @@ import pytest
 import torch
 
 from oracle import oracle as O
-from mp_ranks import init_pg, spawn
+from mp_ranks import heartbeat, init_pg, spawn
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -322,6 +322,7 @@ def _ipc_failure_paths(rank, world, init, n):
 def test_ipc_failure_paths_return_errors(cuda):
     res = spawn(_ipc_failure_paths, 2, (1 << 20,), timeout=120)
     r1 = [r for rank, r, _ in res if rank == 1][0]
+    heartbeat(f"hipIpc failure paths: {r1}")
     assert r1["zero_handle_status"] != 0, r1
     assert r1["bad_close_status"] != 0, r1
     assert r1["dead_exporter_status"] != 0 or r1["dead_exporter_close_status"] == 0, r1
