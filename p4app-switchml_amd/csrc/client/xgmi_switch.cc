@@ -309,8 +309,26 @@ void XgmiSwitch::Barrier(int index) {
     }
 }
 
+bool XgmiSwitch::StreamSync(hipStream_t st, bool bounded_only) {
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms_);
+    for (uint32_t spins = 0;; spins++) {
+        const hipError_t q = hipStreamQuery(st);
+        if (q == hipSuccess) return true;
+        if (q != hipErrorNotReady) {
+            if (bounded_only) return false;
+            hip_ok(q, "hipStreamQuery");
+        }
+        if (spins > 256) {
+            std::this_thread::yield();
+            if ((spins & 1023) == 0 && std::chrono::steady_clock::now() > deadline) {
+                if (bounded_only) return false;
+                throw SwitchMLFatal("xgmi switch: device work did not finish within backend.xgmi.timeout_ms");
+            }
+        }
+    }
+}
+
 namespace {
-void stream_sync(hipStream_t st) { hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize"); }
 // The writer's half of every hand-off to the peers: write
 // this GPU's L2 back before the stream sync that precedes the barrier.
 void release(hipStream_t st) { sml_ok(sml_release_to_peers(st), "sml_release_to_peers"); }
@@ -381,11 +399,11 @@ void XgmiSwitch::FloatSlice(int tid, const float* in, float* out, uint64_t numel
     auto len = [&](uint64_t c) { return std::min<uint64_t>(cap_, numel - c * cap_); };
     sml_ok(sml_exponents(in, len(0), P_, tp.exps, st), "sml_exponents");
     release(st);
-    stream_sync(st);
+    StreamSync(st);
     Barrier(tid);
     Quantize(tp, in, len(0), st);
     release(st);
-    stream_sync(st);
+    StreamSync(st);
     Barrier(tid);
     for (uint64_t c = 0; c < nchunks; c++) {
         const uint64_t n = len(c), B = sml_num_blocks(n, P_), S = (B + W_ - 1) / W_;
@@ -398,8 +416,8 @@ void XgmiSwitch::FloatSlice(int tid, const float* in, float* out, uint64_t numel
             sml_ok(sml_exponents(in_next, len(c + 1), P_, tp.exps, st), "sml_exponents");
             release(st);
         }
-        stream_sync(tp.xst);
-        stream_sync(st);
+        StreamSync(tp.xst);
+        StreamSync(st);
         Barrier(tid);
         if (push_) {   // every shard is in the own out plane now: one local copy
             const void* src = tp.out;
@@ -412,8 +430,8 @@ void XgmiSwitch::FloatSlice(int tid, const float* in, float* out, uint64_t numel
             Quantize(tp, in_next, len(c + 1), st);
             release(st);
         }
-        stream_sync(tp.xst);
-        stream_sync(st);
+        StreamSync(tp.xst);
+        StreamSync(st);
         Barrier(tid);   // peers are done reading our planes before they are written again
     }
 }
@@ -466,7 +484,7 @@ void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, 
     const uint64_t S = (B + W_ - 1) / W_;
     sml_ok(sml_copy_words(in, tp.payload, n, st), "sml_copy_words");
     release(st);
-    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    StreamSync(st);
     Barrier(tid);
     const uint64_t blk0 = std::min<uint64_t>((uint64_t)rank_ * S, B);
     const uint64_t nb = std::min<uint64_t>(S, B - blk0);
@@ -479,10 +497,10 @@ void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, 
                "sml_switch_aggregate");
         release(st);
     }
-    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    StreamSync(st);
     Barrier(tid);
     Gather(tp, out, n, B, S, st);
-    hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+    StreamSync(st);
     Barrier(tid);
 }
 
@@ -505,8 +523,8 @@ void XgmiSwitch::AllReduceSlice(int tid, const void* in, void* out, uint64_t num
         // fail the session for everyone rather than let a barrier pair
         // different phases
         Poison();
-        (void)hipStreamSynchronize(st);
-        (void)hipStreamSynchronize(planes_[tid].xst);
+        (void)StreamSync(st, true);
+        (void)StreamSync(planes_[tid].xst, true);
         throw;
     }
 }

@@ -101,6 +101,10 @@ class XgmiSwitch {
     void Setup(int device);
     void Release();
     void Barrier(int index);
+    // Wait for the work queued on `st`, polling against backend.xgmi.timeout_ms
+    // (a device that never finishes fails the slice instead of blocking the
+    // worker thread forever); `bounded_only` waits never throw (cleanup paths).
+    bool StreamSync(hipStream_t st, bool bounded_only = false);
     void FloatSlice(int tid, const float* in, float* out, uint64_t numel, hipStream_t st);
     void Aggregate(ThreadPlanes& tp, uint64_t n, hipStream_t st);
     void Quantize(ThreadPlanes& tp, const float* in, uint64_t n, hipStream_t st);
