@@ -104,13 +104,16 @@ def wait_device(stream: torch.cuda.Stream, what: str, timeout_s: float) -> None:
     ev = torch.cuda.Event()
     ev.record(stream)
     t0 = time.monotonic()
-    spin_until = t0 + 0.002
+    # spin like a stream synchronize for the first 100 ms (the hand-offs this
+    # guards take micro- to milliseconds: a sleep's wake-up latency would be
+    # timed into every all-reduce), then back off
+    spin_until = t0 + 0.1
     while not ev.query():
         now = time.monotonic()
         if now - t0 > timeout_s:
             raise TimeoutError(f"p2p switch: device work before '{what}' not finished after {timeout_s:g} s")
         if now > spin_until:
-            time.sleep(50e-6)
+            time.sleep(1e-3)
 
 
 def _sync_timeout_default() -> float:
