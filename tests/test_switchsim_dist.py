@@ -326,3 +326,21 @@ def test_ipc_failure_paths_return_errors(cuda):
     assert r1["zero_handle_status"] != 0, r1
     assert r1["bad_close_status"] != 0, r1
     assert r1["dead_exporter_status"] != 0 or r1["dead_exporter_close_status"] == 0, r1
+
+
+@pytest.mark.gpu
+def test_wait_device_times_out_with_a_named_error(cuda):
+    """The p2p switch's host waits are bounded: device work that outlasts the
+    deadline raises TimeoutError naming the hand-off (here: ~0.1 s of
+    legitimate GEMMs against a 5 ms deadline), and the same wait succeeds
+    once the work is done."""
+    from switchml_amd.p2pswitch import wait_device
+    st = torch.cuda.current_stream()
+    a = torch.randn(8192, 8192, device=cuda)
+    torch.cuda.synchronize()
+    for _ in range(30):
+        a = (a @ a) * 1e-4
+    with pytest.raises(TimeoutError, match="'k6' not finished"):
+        wait_device(st, "k6", 0.005)
+    torch.cuda.synchronize()
+    wait_device(st, "k6", 5.0)
