@@ -82,6 +82,7 @@ bool Config::LoadFromString(const std::string& ini) {
         else if (full == "backend.hip.burst_server") backend_.hip.burst_server = parse_bool(val);
         else if (full == "backend.hip.batch_jobs") backend_.hip.batch_jobs = parse_uint<uint32_t>(full, val, 0xffffffffull);
         else if (full == "backend.hip.coalesce_us") backend_.hip.coalesce_us = parse_uint<uint32_t>(full, val, 1000000ull);
+        else if (full == "backend.hip.vcl") backend_.hip.vcl = parse_bool(val);
         else fprintf(stderr, "[switchml] ignoring config key '%s' (not used by this build)\n", full.c_str());
     }
     return true;
@@ -161,6 +162,7 @@ std::string Config::ToString() const {
       << "\nburst_server = " << (backend_.hip.burst_server ? "true" : "false")
       << "\nbatch_jobs = " << backend_.hip.batch_jobs
       << "\ncoalesce_us = " << backend_.hip.coalesce_us
+      << "\nvcl = " << (backend_.hip.vcl ? "true" : "false")
       << "\n\n[backend.xgmi]\nsession = " << backend_.xgmi.session
       << "\nmax_slice_numel = " << backend_.xgmi.max_slice_numel << "\ntimeout_ms = " << backend_.xgmi.timeout_ms
       << "\npush = " << (backend_.xgmi.push ? "true" : "false")

@@ -64,6 +64,13 @@ struct HipBackendConfig {
     // that arrive within coalesce_us of the previous one join the same
     // launch (PCIe moves more bytes per second in larger launches); 0 = off.
     uint32_t coalesce_us = 20;
+    // The quantizer's rounding, as the reference's two client_lib builds do
+    // it (client_lib/Makefile:26,113-120): false = the VCL=0 build (roundf,
+    // half away from zero, every element; ppp.cc:100-109), true = the VCL=1
+    // build (round-to-nearest-even on each packet's 16-element vector body,
+    // roundf on its tail, ppp.cc:88-99; SML_FLAG_ROUND_RNE).  A caller who
+    // ran the reference's default build sets vcl = true for its bits.
+    bool vcl = false;
 };
 
 // The in-node switch (general.backend = "xgmi", xgmi_switch.h): W worker

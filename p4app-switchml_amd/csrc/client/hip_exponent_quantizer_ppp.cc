@@ -16,7 +16,8 @@ static void hip_ok(hipError_t e, const char* what) {
 
 HipExponentQuantizerPPP::HipExponentQuantizerPPP(Config& config, WorkerTid worker_tid, Numel ltu_size,
                                                  Numel batch_num_ltus, bool per_ltu_calls)
-    : PrePostProcessor(config, worker_tid, ltu_size, batch_num_ltus), per_ltu_calls_(per_ltu_calls) {
+    : PrePostProcessor(config, worker_tid, ltu_size, batch_num_ltus), per_ltu_calls_(per_ltu_calls),
+      round_flags_(config.backend_.hip.vcl ? SML_FLAG_ROUND_RNE : 0u) {
     ltu_numel_ = ltu_size / 4;
     if (ltu_size % 4 || !(ltu_numel_ == 64 || ltu_numel_ == 128 || ltu_numel_ == 256 || ltu_numel_ == 512 ||
                           ltu_numel_ == 1024))
@@ -145,7 +146,7 @@ void HipExponentQuantizerPPP::preprocess_single(uint64_t ltu_id, void* entries_p
             // only the n real ones (ppp.cc:102-109), so a partial block is staged
             int32_t* dst = (m.dev && n == P) ? static_cast<int32_t*>(m.dev) : d_stage_;
             check(sml_quantize_pack(static_cast<const float*>(s.in_ptr) + off, n, P, config_.general_.num_workers,
-                                    d_recv_exps_ + k, dst, nullptr, 0, stream_),
+                                    d_recv_exps_ + k, dst, nullptr, round_flags_, stream_),
                   "sml_quantize_pack");
             if (dst == d_stage_)
                 hip_ok(hipMemcpyAsync(entries_ptr, d_stage_, n * 4, hipMemcpyDefault, stream_), "hipMemcpyAsync");
@@ -296,12 +297,12 @@ void HipExponentQuantizerPPP::burst(BurstKind kind, uint32_t n, const uint64_t* 
     // the exchange needs the window for INT32 too (the next packet is q + b)
     b.batch_num_ltus = flt || exchange ? batch_num_ltus_ : 0;
     b.recv_exps = d_recv_exps_;
-    b.flags = kind == BurstKind::kProcessExchange ? SML_FLAG_PROCESS_PACKET : 0u;
+    b.flags = (kind == BurstKind::kProcessExchange ? SML_FLAG_PROCESS_PACKET : 0u) | round_flags_;
     const char* what = kind == BurstKind::kPre ? "sml_preprocess_burst"
                        : kind == BurstKind::kPost ? "sml_postprocess_burst" : "sml_exchange_burst";
     const bool serve = m.host && config_.backend_.hip.burst_server;
     if (serve && !server_) {
-        check(sml_burst_server_create((uint32_t)ltu_numel_, 0, 100, &server_), "sml_burst_server_create");
+        check(sml_burst_server_create((uint32_t)ltu_numel_, round_flags_, 100, &server_), "sml_burst_server_create");
     }
     if (serve && !server_synced_) {   // the server has its own stream: the slice's staged input must be there
         hip_ok(hipStreamSynchronize(stream_), "hipStreamSynchronize");
@@ -367,7 +368,7 @@ void HipExponentQuantizerPPP::PreprocessBulk(void* payload_plane, void* exps_pla
                                 config_.general_.num_workers, static_cast<const int8_t*>(global_exps),
                                 static_cast<int32_t*>(payload_plane),
                                 global_exps ? nullptr : static_cast<int8_t*>(exps_plane),
-                                payload_le ? SML_FLAG_PAYLOAD_LE : 0u, stream_),
+                                (payload_le ? SML_FLAG_PAYLOAD_LE : 0u) | round_flags_, stream_),
               "sml_quantize_pack");
     } else {
         if (payload_le)

@@ -91,6 +91,9 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     int8_t* d_stage_exp_ = nullptr;
     bool stream_ordered_ = false;
     bool per_ltu_calls_ = true;
+    // SML_FLAG_ROUND_RNE when backend.hip.vcl (the reference's VCL=1 build's
+    // rounding), else 0: or'ed into every quantizing launch
+    uint32_t round_flags_ = 0;
     // where the slice's packet pool lives (burst calls): the first buffer
     // pointer seen, and its packet_mem() answer — for the entries and, as a
     // separate query, the extra-info slots (they may be another allocation)

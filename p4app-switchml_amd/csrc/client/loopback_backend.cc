@@ -199,7 +199,7 @@ uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, J
     } else if (mode == "fused" && is_float && cfg.backend_.dummy.process_packets) {
         sml_ok(sml_roundtrip_loopback(static_cast<const float*>(staged.slice.in_ptr),
                                       static_cast<float*>(staged.slice.out_ptr), t.numel, (uint32_t)P, W, nullptr,
-                                      nullptr, 0, st),
+                                      nullptr, cfg.backend_.hip.vcl ? SML_FLAG_ROUND_RNE : 0u, st),
                "sml_roundtrip_loopback");
     } else {  // bulk
         void* payload = ws.payload.get(B * P * 4);
@@ -325,6 +325,7 @@ void LoopbackBackend::BatchMain() {
     const size_t max_jobs = std::max<size_t>(1, std::min<size_t>(config_.backend_.hip.batch_jobs,
                                                                   SML_MAX_BATCH_SLICES / std::max(1, T)));
     const uint32_t coalesce_us = config_.backend_.hip.coalesce_us;
+    const uint32_t rne = config_.backend_.hip.vcl ? SML_FLAG_ROUND_RNE : 0u;   // the VCL=1 build's rounding
     struct Piece {
         JobSlice js;
         WorkerTid tid;
@@ -410,7 +411,7 @@ void LoopbackBackend::BatchMain() {
             if (!segs.empty()) {
                 try {
                     sml_ok(sml_roundtrip_loopback_batch(segs.data(), (uint32_t)segs.size(), (uint32_t)P,
-                                                        g.num_workers, 0, hip_ppp->stream()),
+                                                        g.num_workers, rne, hip_ppp->stream()),
                            "sml_roundtrip_loopback_batch");
                 } catch (const std::exception& e) {
                     fprintf(stderr, "[switchml] batch worker: %s\n", e.what());

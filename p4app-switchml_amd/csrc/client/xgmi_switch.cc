@@ -153,6 +153,7 @@ XgmiSwitch::XgmiSwitch(const Config& config, int device) {
     P_ = (uint32_t)g.packet_numel;
     cap_ = (config.backend_.xgmi.max_slice_numel + 1023) / 1024 * 1024;
     timeout_ms_ = config.backend_.xgmi.timeout_ms;
+    round_flags_ = config.backend_.hip.vcl ? SML_FLAG_ROUND_RNE : 0u;
     push_ = config.backend_.xgmi.push;
     if (W_ < 1 || W_ > kMaxW) throw SwitchMLFatal("xgmi switch: num_workers must be 1..16");
     if (T_ < 1 || T_ > kMaxT) throw SwitchMLFatal("xgmi switch: num_worker_threads must be 1..16");
@@ -343,7 +344,8 @@ void XgmiSwitch::Quantize(ThreadPlanes& tp, const float* in, uint64_t n, hipStre
     const uint64_t B = sml_num_blocks(n, P_);
     sml_ok(sml_switch_exps(tp.peer_exps.data(), (uint16_t)W_, B, tp.gexp, kPeer, st), "sml_switch_exps");
     if (!push_) {
-        sml_ok(sml_quantize_pack(in, n, P_, (uint16_t)W_, tp.gexp, tp.payload, nullptr, 0, st), "sml_quantize_pack");
+        sml_ok(sml_quantize_pack(in, n, P_, (uint16_t)W_, tp.gexp, tp.payload, nullptr, round_flags_, st),
+               "sml_quantize_pack");
         return;
     }
     const uint64_t S = (B + W_ - 1) / W_;
@@ -353,7 +355,7 @@ void XgmiSwitch::Quantize(ThreadPlanes& tp, const float* in, uint64_t n, hipStre
         if (!nb) continue;
         const uint64_t n_el = std::min<uint64_t>(nb * P_, n - b0 * P_);
         int32_t* row = const_cast<int32_t*>(tp.peer_payload[w]) + (uint64_t)rank_ * S * P_;
-        sml_ok(sml_quantize_pack(in + b0 * P_, n_el, P_, (uint16_t)W_, tp.gexp + b0, row, nullptr, 0, st),
+        sml_ok(sml_quantize_pack(in + b0 * P_, n_el, P_, (uint16_t)W_, tp.gexp + b0, row, nullptr, round_flags_, st),
                "sml_quantize_pack");
     }
 }

@@ -116,6 +116,7 @@ class XgmiSwitch {
     uint32_t P_;
     uint64_t cap_;          // elements per chunk (multiple of 1024)
     uint64_t timeout_ms_;
+    uint32_t round_flags_ = 0;   // SML_FLAG_ROUND_RNE under backend.hip.vcl
     bool push_ = false;     // backend.xgmi.push: K3 writes into the owners' inboxes
     std::string name_;
     XgmiShm* shm_ = nullptr;

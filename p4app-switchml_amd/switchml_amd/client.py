@@ -65,7 +65,7 @@ def make_config(**kw) -> str:
         "backend", "scheduler", "prepostprocessor", "instant_job_completion")}
     dummy = {k: v for k, v in kw.items() if k in ("bandwidth", "process_packets", "fail_worker_thread")}
     hip = {k: v for k, v in kw.items() if k in ("device", "mode", "packet_ring", "burst_server", "batch_jobs",
-                                                     "coalesce_us")}
+                                                     "coalesce_us", "vcl")}
     xgmi = {k: v for k, v in kw.items() if k in ("session", "max_slice_numel", "timeout_ms", "push")}
     unknown = set(kw) - set(general) - set(dummy) - set(hip) - set(xgmi)
     if unknown:

@@ -91,6 +91,13 @@ def test_config_validation(ctx):
     C.start(C.make_config(prepostprocessor="bypass", burst_server=True, push=True, bandwidth=0))
     assert "burst_server = true" in C.config_text() and "push = true" in C.config_text()
     C.stop()
+    # the VCL=1 build's rounding (backend.hip.vcl): off by default, on when asked
+    C.start(C.make_config(prepostprocessor="bypass", bandwidth=0))
+    assert "vcl = false" in C.config_text()
+    C.stop()
+    C.start(C.make_config(prepostprocessor="bypass", vcl=True, bandwidth=0))
+    assert "vcl = true" in C.config_text()
+    C.stop()
     for bad in (dict(prepostprocessor="nope"), dict(backend="dpdk"), dict(mode="turbo"),
                 dict(num_worker_threads=8, max_outstanding_packets=4)):
         kw = dict(prepostprocessor="bypass", bandwidth=0)

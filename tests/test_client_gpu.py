@@ -252,3 +252,43 @@ def test_allreduce_waits_for_the_producing_stream(C, mode):
     ref = O.dummy_allreduce(want_in.cpu().numpy(), P=256, max_outstanding_packets=64 * T, num_worker_threads=T,
                             num_workers=W)
     assert bits_equal(out.cpu().numpy(), ref)
+
+
+def tie_bucket(n, P, W, seed):
+    """FLOAT32 bucket whose quantized values are mostly exact .5 ties: every
+    block holds a 1.0 (exponent e = 1, scale = 2^30 / W, exact for
+    power-of-two W) and elements ±(m + 0.5)·W·2^-30 (x·scale = ±(m + 0.5),
+    exact), the rest N(0, 0.25) clipped inside (-1, 1)."""
+    rng = np.random.default_rng(seed)
+    x = np.clip(rng.standard_normal(n) * 0.25, -0.99, 0.99).astype(np.float32)
+    m = rng.integers(0, 1 << 20, n)
+    ties = ((m + 0.5) * W * 2.0 ** -30 * np.where(rng.random(n) < 0.5, -1.0, 1.0)).astype(np.float32)
+    sel = rng.random(n) < 0.6
+    x[sel] = ties[sel]
+    x[::P] = 1.0
+    return x
+
+
+@pytest.mark.parametrize("mode", ["bulk", "fused", "fused-threads", "packet", "packet-pinned-server"])
+@pytest.mark.parametrize("T,W,P", [(1, 1, 256), (4, 2, 256), (3, 8, 64), (2, 2, 1024)])
+def test_vcl_rounding_through_context(C, mode, T, W, P):
+    """backend.hip.vcl = true: the reference's VCL=1 build (its default,
+    client_lib/Makefile:26,113-120) — round-to-nearest-even on each packet's
+    16-element vector body, roundf on the tail (ppp.cc:88-99) — through
+    every dispatch of the Context, bit-exact against the oracle's VCL=1
+    packet loop; on tie-heavy buckets, so the two builds' results differ."""
+    n = 100_003 if not mode.startswith("packet") else 20_011
+    kw = _mode(mode) if not mode.startswith("packet") else dict(mode="packet")
+    if mode == "packet-pinned-server":
+        kw.update(packet_ring="pinned", burst_server=True)
+    C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, max_outstanding_packets=64 * T,
+                          bandwidth=0, vcl=True, **kw))
+    assert "vcl = true" in C.config_text()
+    x = tie_bucket(n, P, W, T * 10 + W)
+    ref = O.dummy_allreduce(x, P=P, max_outstanding_packets=64 * T, num_worker_threads=T, num_workers=W, vcl=True)
+    away = O.dummy_allreduce(x, P=P, max_outstanding_packets=64 * T, num_worker_threads=T, num_workers=W)
+    assert not bits_equal(ref, away)          # the ties make the two builds differ
+    out = np.empty_like(x)
+    C.allreduce(x, out)
+    assert bits_equal(out, ref)
+    C.stop()

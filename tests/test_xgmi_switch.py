@@ -16,15 +16,16 @@ import uuid
 import numpy as np
 import pytest
 import torch
-import torch.multiprocessing as mp
 
 from oracle import oracle as O
+from mp_ranks import spawn
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def oracle_switch_allreduce(xs, P, T):
-    """W workers' buckets through the reference's switch, slice by slice."""
+def oracle_switch_allreduce(xs, P, T, rounding=O.HALF_AWAY):
+    """W workers' buckets through the reference's switch, slice by slice
+    (rounding = O.RNE_VCL: the reference's VCL=1 build)."""
     W, n = len(xs), xs[0].size
     out = np.empty(n, dtype=np.float32)
     for t in range(T):
@@ -33,7 +34,7 @@ def oracle_switch_allreduce(xs, P, T):
             continue
         parts = [x[off:off + m] for x in xs]
         g = O.switch_exps([O.exponents(p, P) for p in parts])
-        agg = O.switch_payload([O.quantize(p, P, W, global_exps=g) for p in parts])
+        agg = O.switch_payload([O.quantize(p, P, W, global_exps=g, rounding=rounding) for p in parts])
         out[off:off + m] = O.dequantize(agg, g, m, P, W)
     return out
 
@@ -42,89 +43,52 @@ def worker_bucket(rank, n, seed):
     return O.splitmix_normal(seed * 31 + rank, n) * np.float32(2.0 ** (rank % 3 - 1))
 
 
-def _paths():
-    import sys
-    for p in (ROOT, os.path.join(ROOT, "p4app-switchml_amd"), os.path.join(ROOT, "tests")):
-        if p not in sys.path:
-            sys.path.insert(0, p)
-
-
-def _client_worker(rank, W, T, P, session, cap, push, q):
-    try:
-        _paths()
-        from switchml_amd import client as C
-        C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=T, packet_numel=P,
-                              max_outstanding_packets=64 * T, mode="bulk", bandwidth=0, device=0,
-                              session=session, max_slice_numel=cap, push=push))
-        res = []
-        sizes = [100_003, 1, 3 * cap + 517, 0, 4 * P * W + 5]
-        for i, n in enumerate(sizes):
-            where = ("device", "pageable", "pinned")[i % 3]
-            xs = [worker_bucket(r, n, i) for r in range(W)]
-            x = torch.from_numpy(xs[rank].copy())
-            if where == "device":
-                x = x.cuda()
-            elif where == "pinned":
-                x = x.pin_memory()
-            inplace = i % 2 == 0
-            out = x if inplace else torch.empty_like(x)
-            C.allreduce(x, out)
-            got = out.cpu().numpy() if out.is_cuda else out.numpy()
-            ref = oracle_switch_allreduce(xs, P, T)
-            res.append(bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32))))
-        # INT32: the words' wrapping sum over the workers
-        n = 50_021
-        xi = [np.random.default_rng(5 + r).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
-              for r in range(W)]
-        t = torch.from_numpy(xi[rank].copy()).cuda()
-        C.allreduce(t)
-        ref = O.bswap32(O.switch_payload([O.bswap32(v) for v in xi]))
-        res.append(bool(np.array_equal(t.cpu().numpy().view(np.uint32), ref)))
-        # several jobs in flight at once, the same order on every worker
-        xs = [[worker_bucket(r, 70_001 + j, 100 + j) for r in range(W)] for j in range(4)]
-        ts = [torch.from_numpy(xs[j][rank].copy()).cuda() for j in range(4)]
-        jobs = [C.allreduce_async(tt) for tt in ts]
-        C.wait_for_all_jobs()
-        for j in range(4):
-            ref = oracle_switch_allreduce(xs[j], P, T)
-            res.append(jobs[j].status() == C.JOB_FINISHED and
-                       bool(np.array_equal(ts[j].cpu().numpy().view(np.uint32), ref.view(np.uint32))))
-        C.stop()
-        q.put((rank, res, ""))
-    except Exception as ex:  # pragma: no cover - reported to the parent
-        import traceback
-        q.put((rank, None, traceback.format_exc()[-2000:]))
+def _client_worker(rank, W, init, T, P, session, cap, push):
+    from switchml_amd import client as C
+    C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=T, packet_numel=P,
+                          max_outstanding_packets=64 * T, mode="bulk", bandwidth=0, device=0,
+                          session=session, max_slice_numel=cap, push=push))
+    res = []
+    sizes = [100_003, 1, 3 * cap + 517, 0, 4 * P * W + 5]
+    for i, n in enumerate(sizes):
+        where = ("device", "pageable", "pinned")[i % 3]
+        xs = [worker_bucket(r, n, i) for r in range(W)]
+        x = torch.from_numpy(xs[rank].copy())
+        if where == "device":
+            x = x.cuda()
+        elif where == "pinned":
+            x = x.pin_memory()
+        inplace = i % 2 == 0
+        out = x if inplace else torch.empty_like(x)
+        C.allreduce(x, out)
+        got = out.cpu().numpy() if out.is_cuda else out.numpy()
+        ref = oracle_switch_allreduce(xs, P, T)
+        res.append(bool(np.array_equal(got.view(np.uint32), ref.view(np.uint32))))
+    # INT32: the words' wrapping sum over the workers
+    n = 50_021
+    xi = [np.random.default_rng(5 + r).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+          for r in range(W)]
+    t = torch.from_numpy(xi[rank].copy()).cuda()
+    C.allreduce(t)
+    ref = O.bswap32(O.switch_payload([O.bswap32(v) for v in xi]))
+    res.append(bool(np.array_equal(t.cpu().numpy().view(np.uint32), ref)))
+    # several jobs in flight at once, the same order on every worker
+    xs = [[worker_bucket(r, 70_001 + j, 100 + j) for r in range(W)] for j in range(4)]
+    ts = [torch.from_numpy(xs[j][rank].copy()).cuda() for j in range(4)]
+    jobs = [C.allreduce_async(tt) for tt in ts]
+    C.wait_for_all_jobs()
+    for j in range(4):
+        ref = oracle_switch_allreduce(xs[j], P, T)
+        res.append(jobs[j].status() == C.JOB_FINISHED and
+                   bool(np.array_equal(ts[j].cpu().numpy().view(np.uint32), ref.view(np.uint32))))
+    C.stop()
+    return res
 
 
 def _run(target, W, args, timeout=240):
-    """Run `target` in W spawned worker processes; a worker that dies without
-    reporting (or a run past `timeout`) fails the test at once instead of
-    leaving the parent waiting on the queue."""
-    import queue
-    import time
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    procs = [ctx.Process(target=target, args=(r, W) + args + (q,)) for r in range(W)]
-    for p in procs:
-        p.start()
-    res, t_end = [], time.time() + timeout
-    while len(res) < W:
-        try:
-            res.append(q.get(timeout=2))
-            continue
-        except queue.Empty:
-            pass
-        reported = {r[0] for r in res}
-        dead = [(i, p.exitcode) for i, p in enumerate(procs) if p.exitcode not in (None, 0) and i not in reported]
-        if dead or time.time() > t_end:
-            for p in procs:
-                if p.is_alive():
-                    p.kill()
-            pytest.fail(f"workers failed without a result (rank, exit code: {dead}) or timed out; "
-                        f"got {len(res)} of {W}")
-    for p in procs:
-        p.join(timeout=60)
-    return res
+    """Run `target` in W spawned worker processes (tests/mp_ranks.py: the
+    first failing or dead worker ends the wait, a hung one dumps its stack)."""
+    return spawn(target, W, args, timeout=timeout, what=f"xgmi workers W={W}")
 
 
 @pytest.mark.gpu
@@ -144,36 +108,64 @@ def test_xgmi_backend_allreduce_matches_oracle_switch(cuda, W, T, P, push):
         assert all(res), (rank, res)
 
 
-def _plugin_worker(rank, W, session, q):
+def _client_vcl_worker(rank, W, init, T, P, session, push):
+    """backend.hip.vcl = true on the in-node switch: K3 with the reference's
+    VCL=1 rounding on tie-heavy buckets, every worker's result bit-exact
+    against the oracle switch in that rounding (and different from the
+    half-away result, so the flag demonstrably reached the kernel)."""
+    from test_client_gpu import tie_bucket
+    from switchml_amd import client as C
+    C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=T, packet_numel=P,
+                          max_outstanding_packets=64 * T, mode="bulk", bandwidth=0, device=0,
+                          session=session, push=push, vcl=True))
+    res = []
+    for i, n in enumerate([100_003, 3 * P + 5]):
+        xs = [tie_bucket(n, P, W, 1000 * i + r) for r in range(W)]
+        t = torch.from_numpy(xs[rank].copy()).cuda()
+        C.allreduce(t)
+        ref = oracle_switch_allreduce(xs, P, T, rounding=O.RNE_VCL)
+        away = oracle_switch_allreduce(xs, P, T)
+        got = t.cpu().numpy().view(np.uint32)
+        res.append(bool(np.array_equal(got, ref.view(np.uint32))))
+        res.append(i > 0 or not np.array_equal(ref.view(np.uint32), away.view(np.uint32)))
+    C.stop()
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,T,P,push", [(2, 2, 256, False), (4, 1, 64, True)])
+def test_xgmi_backend_vcl_rounding(cuda, W, T, P, push):
+    session = "vcl-" + uuid.uuid4().hex
+    for rank, res, err in _run(_client_vcl_worker, W, (T, P, session, push)):
+        assert res is not None, (rank, err)
+        assert all(res), (rank, res)
+
+
+def _plugin_worker(rank, W, init, session):
+    ini = ("[general]\nbackend = xgmi\nrank = %d\nnum_workers = %d\nnum_worker_threads = 2\npacket_numel = 256\n"
+           "max_outstanding_packets = 128\n[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = bulk\n"
+           "device = 0\n[backend.xgmi]\nsession = %s\n" % (rank, W, session))
+    os.environ["SWITCHML_CONFIG_INI"] = ini
+    os.environ.pop("SWITCHML_COLLNET_LOOPBACK", None)
+    from switchml_amd.collnet import CollNetComm, NCCL_FLOAT32, CollNetError
+    comm = CollNetComm(nranks=W, rank=rank)
+    sizes = [6_553_600, 5_896_232, 1000]     # ResNet-50 DDP buckets (two of them) + a small one
+    xs = [[worker_bucket(r, n, 7 + j) for r in range(W)] for j, n in enumerate(sizes)]
+    send = [torch.from_numpy(xs[j][rank].copy()).cuda() for j in range(len(sizes))]
+    recv = [torch.empty_like(s) for s in send]
+    comm.allreduce_buckets([(s.data_ptr(), r.data_ptr(), s.numel()) for s, r in zip(send, recv)], NCCL_FLOAT32)
+    ok = [bool(np.array_equal(recv[j].cpu().numpy().view(np.uint32),
+                              oracle_switch_allreduce(xs[j], 256, 2).view(np.uint32))) for j in range(len(sizes))]
+    # a communicator that is not the session's workers is refused
     try:
-        _paths()
-        ini = ("[general]\nbackend = xgmi\nrank = %d\nnum_workers = %d\nnum_worker_threads = 2\npacket_numel = 256\n"
-               "max_outstanding_packets = 128\n[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = bulk\n"
-               "device = 0\n[backend.xgmi]\nsession = %s\n" % (rank, W, session))
-        os.environ["SWITCHML_CONFIG_INI"] = ini
-        os.environ.pop("SWITCHML_COLLNET_LOOPBACK", None)
-        from switchml_amd.collnet import CollNetComm, NCCL_FLOAT32, CollNetError
-        comm = CollNetComm(nranks=W, rank=rank)
-        sizes = [6_553_600, 5_896_232, 1000]     # ResNet-50 DDP buckets (two of them) + a small one
-        xs = [[worker_bucket(r, n, 7 + j) for r in range(W)] for j, n in enumerate(sizes)]
-        send = [torch.from_numpy(xs[j][rank].copy()).cuda() for j in range(len(sizes))]
-        recv = [torch.empty_like(s) for s in send]
-        comm.allreduce_buckets([(s.data_ptr(), r.data_ptr(), s.numel()) for s, r in zip(send, recv)], NCCL_FLOAT32)
-        ok = [bool(np.array_equal(recv[j].cpu().numpy().view(np.uint32),
-                                  oracle_switch_allreduce(xs[j], 256, 2).view(np.uint32))) for j in range(len(sizes))]
-        # a communicator that is not the session's workers is refused
-        try:
-            CollNetComm(nranks=W + 1, rank=rank)
-            ok.append(False)
-        except CollNetError:
-            ok.append(True)
-        comm.close()
-        from switchml_amd import client as C
-        C.stop()
-        q.put((rank, ok, ""))
-    except Exception as ex:  # pragma: no cover
-        import traceback
-        q.put((rank, None, traceback.format_exc()[-2000:]))
+        CollNetComm(nranks=W + 1, rank=rank)
+        ok.append(False)
+    except CollNetError:
+        ok.append(True)
+    comm.close()
+    from switchml_amd import client as C
+    C.stop()
+    return ok
 
 
 @pytest.mark.gpu
@@ -200,32 +192,27 @@ def test_xgmi_config_validation():
         assert C.state() != C.RUNNING
 
 
-def _failing_worker(rank, W, session, fail_rank, q):
+def _failing_worker(rank, W, init, session, fail_rank):
     """Worker `fail_rank` injects a fault on worker thread 0 of every job
     (backend.dummy.fail_worker_thread); the session is poisoned, so every
     worker's job fails — none hangs on a barrier, none reports FINISHED —
     and the jobs after it fail too (no out-of-phase barriers)."""
-    try:
-        _paths()
-        import time
-        from switchml_amd import client as C
-        kw = dict(fail_worker_thread=0) if rank == fail_rank else {}
-        C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=2, packet_numel=256,
-                              max_outstanding_packets=128, mode="bulk", bandwidth=0, device=0, session=session,
-                              timeout_ms=30000, **kw))
-        t0 = time.time()
-        sts = []
-        for j in range(3):
-            x = torch.from_numpy(worker_bucket(rank, 200_000, j)).cuda()
-            job = C.allreduce_async(x)
-            C.wait_for_all_jobs()
-            sts.append(job.status())
-        took = time.time() - t0
-        C.stop()
-        q.put((rank, {"statuses": sts, "seconds": took}, ""))
-    except Exception:  # pragma: no cover
-        import traceback
-        q.put((rank, None, traceback.format_exc()[-2000:]))
+    import time
+    from switchml_amd import client as C
+    kw = dict(fail_worker_thread=0) if rank == fail_rank else {}
+    C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=2, packet_numel=256,
+                          max_outstanding_packets=128, mode="bulk", bandwidth=0, device=0, session=session,
+                          timeout_ms=30000, **kw))
+    t0 = time.time()
+    sts = []
+    for j in range(3):
+        x = torch.from_numpy(worker_bucket(rank, 200_000, j)).cuda()
+        job = C.allreduce_async(x)
+        C.wait_for_all_jobs()
+        sts.append(job.status())
+    took = time.time() - t0
+    C.stop()
+    return {"statuses": sts, "seconds": took}
 
 
 @pytest.mark.gpu
