@@ -121,7 +121,10 @@ def launch_ranks(n):
 
 def load_traffic(numel, P, key="quantize_pack"):
     """HBM bytes per launch from the PMC passes (profiles/pmc_traffic.json,
-    written by profiles/collect_pmc.py from separate rocprofv3 --pmc runs)."""
+    written by profiles/collect_pmc.py from separate rocprofv3 --pmc runs):
+    the entry `key` when its size matches, and for the cycling pattern also
+    the per-GPU FIFO slice sizes of configs[3] (`quantize_pack_cold_slices`,
+    the N > 1 lines)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
@@ -129,6 +132,10 @@ def load_traffic(numel, P, key="quantize_pack"):
         k = d.get(key, {})
         if k.get("numel") == numel and k.get("packet_numel") == P:
             return k.get("hbm_bytes_per_launch")
+        if key == "quantize_pack_cold":
+            for e in d.get("quantize_pack_cold_slices", []):
+                if e.get("numel") == numel and e.get("packet_numel") == P:
+                    return e.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
     return None

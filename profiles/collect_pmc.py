@@ -107,9 +107,46 @@ def main(tag="r02", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
                           "hbm_bytes_per_launch": round(fetch_b + write_b)}}
     if other_b is not None:
         traffic[other_key] = {"numel": numel, "packet_numel": packet_numel, "hbm_bytes_per_launch": round(other_b)}
+    slices = slice_traffic(src, packet_numel)
+    if slices:
+        traffic["quantize_pack_cold_slices"] = slices
+        summary["slice_traffic"] = slices
+        with open(os.path.join(dst, "summary.json"), "w") as f:
+            json.dump(summary, f, indent=1)
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(summary, indent=1))
+
+
+def slice_traffic(src, packet_numel):
+    """K1's HBM bytes per launch at configs[3]'s per-GPU FIFO slice sizes
+    (run_profiles.sh: slice_<numel>_{fetch,write}, 4 buckets cycled), for the
+    N > 1 lines' roofline.traffic."""
+    out = []
+    for d in sorted(os.listdir(src)) if os.path.isdir(src) else []:
+        if not (d.startswith("slice_") and d.endswith("_fetch")):
+            continue
+        numel = int(d.split("_")[1])
+        wdir = os.path.join(src, f"slice_{numel}_write")
+        if not os.path.isdir(wdir):
+            continue
+
+        def vals(sub, counter):
+            rr = rows(os.path.join(src, sub, "pmc_counter_collection.csv"))
+            q = [r for r in rr if "k_quantize_pack" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+            if not q:
+                return []
+            grid = max(int(r["Grid_Size"]) for r in q)
+            return [float(r["Counter_Value"]) for r in q if int(r["Grid_Size"]) == grid]
+
+        f, w = vals(d, "FETCH_SIZE"), vals(f"slice_{numel}_write", "WRITE_SIZE")
+        if not f or not w:
+            continue
+        B = -(-numel // packet_numel)
+        hbm = 2 * 1024 * statistics.mean(f) + 1024 * statistics.mean(w)
+        out.append({"numel": numel, "packet_numel": packet_numel, "buckets": 4,
+                    "hbm_bytes_per_launch": round(hbm), "traffic_over_algorithmic": hbm / (8 * numel + B)})
+    return out
 
 
 def frames_summary(src, dst, numel, packet_numel, batch_max=64):

@@ -27,6 +27,14 @@ step timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o pmc --o
 RARGS="$ARGS --buckets 1"
 step timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/res_fetch" -o pmc --output-format csv -- python3 $RARGS > "$OUT/res_fetch.log" 2>&1
 step timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/res_write" -o pmc --output-format csv -- python3 $RARGS > "$OUT/res_write.log" 2>&1
+# configs[3]'s per-GPU FIFO slices at N = 2 and 8 (512 and 128 MiB; N = 4's
+# slice is the 256 MiB headline bucket): HBM bytes per launch for the N > 1
+# lines' roofline.traffic, the steps cycling 4 buckets as the N > 1 runs do
+for SN in 134217728 33554432; do
+  SARGS="$ROOT/bench.py --numel $SN --steps 20 --warmup 5 --settle-ms 0 --no-cpu-baseline --no-side --no-rccl-collnet"
+  step timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/slice_${SN}_fetch" -o pmc --output-format csv -- python3 $SARGS > "$OUT/slice_${SN}_fetch.log" 2>&1
+  step timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/slice_${SN}_write" -o pmc --output-format csv -- python3 $SARGS > "$OUT/slice_${SN}_write.log" 2>&1
+done
 # F3 frames kernels (tx quantize-into-frames, rx claim/apply) on the same bucket
 FR="$ROOT/tools/prof_frames.py"
 step timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/fr_kt" -o kt --output-format csv -- python3 $FR > "$OUT/fr_kt.log" 2>&1

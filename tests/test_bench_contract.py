@@ -123,3 +123,17 @@ def test_n_gt1_line_names_both_readings():
     assert set(r["readings"]) == {"value", "weak_256MiB_value"}
     assert "strong" in r["readings"]["value"] and "weak" in r["readings"]["weak_256MiB_value"]
     assert bench.weak_readings(wk, 1) == {} and bench.weak_readings({"error": "x"}, 8) == {}
+
+
+def test_roofline_traffic_covers_the_n_gt1_slices():
+    """The N > 1 lines' roofline.traffic: profiles/pmc_traffic.json holds
+    K1's PMC bytes per launch at the headline bucket and at configs[3]'s
+    per-GPU FIFO slices for N = 2 / 8 (N = 4's slice is the headline
+    bucket), each within 0.1 % of the algorithmic bytes."""
+    for G in (1, 2, 4, 8):
+        n = 67_108_864 if G == 1 else 268_435_456 // G
+        t = bench.load_traffic(n, 256, "quantize_pack_cold")
+        assert t is not None, G
+        alg = 8 * n + n // 256
+        assert abs(t / alg - 1) < 1e-3, (G, t / alg)
+    assert bench.load_traffic(12345, 256, "quantize_pack_cold") is None
