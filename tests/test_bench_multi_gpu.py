@@ -78,3 +78,38 @@ def test_bench_n2_rehearsal_line(cuda, tmp_path):
     assert line["weak_256MiB_value"] > 0 and line["weak_256MiB"]["roofline"]["frac"] > 0
     assert set(line["config"]["readings"]) == {"value", "weak_256MiB_value"}
     assert line["scaling"] == "strong"
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_n1_line(cuda, tmp_path):
+    """The driver's N = 1 line keeps its contract: the metric and unit of
+    BASELINE.json, the headline's self-check against the committed digests,
+    `roofline` (hbm bound, 8 TB/s peak, frac = achieved / peak, PMC traffic
+    within 0.1 % of the algorithmic bytes) and `cpu_baseline` (the oracle's
+    port of the reference path on the host cores) — with a short CPU sample
+    (--cpu-seconds 2) to keep the test brief; `--graph-steps` exercised too."""
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    for extra in ([], ["--graph-steps", "2", "--no-cpu-baseline", "--no-side", "--no-rccl-collnet"]):
+        cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
+               "--cpu-seconds", "2"] + extra
+        rc, out, err, wall = run_child(cmd, env, str(tmp_path), 500, "bench.py --gpus 1")
+        lines = [l for l in out.splitlines() if l.startswith("{")]
+        assert rc == 0 and lines, (rc, err[-1500:])
+        line = json.loads(lines[-1])
+        assert line["metric"] == base["metric"] and line["unit"] == "GB/s" and line["n_gpus"] == 1
+        assert line["self_check"] is True and line["higher_is_better"] is True
+        assert line["ms_per_step"] * line["steps"] / 1e3 < wall
+        r = line["roofline"]
+        assert r["bound"] == "hbm" and r["peak"] == bench.HBM_PEAK_GBPS and r["unit"] == "GB/s"
+        assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3 and 0.3 < r["frac"] < 1.0
+        n, P = line["config"]["numel_per_gpu"], line["config"]["packet_numel"]
+        assert abs(r["traffic"] / (8 * n + -(-n // P)) - 1) < 1e-3
+        if not extra:
+            cb = line["cpu_baseline"]
+            assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["unit"].startswith("GB/s")
+        else:
+            assert "hipGraph" in line["config"]["launch"]
