@@ -393,15 +393,22 @@ def main():
     step, per_call = launch, 1
     if args.graph_steps > 1:
         # G consecutive steps captured into one hipGraph (G kernel nodes);
-        # each replay still runs exactly G full steps.
+        # each replay still runs exactly G full steps.  The captured steps
+        # cycle the buckets from bucket 0, so every replay covers every
+        # bucket only when G is a multiple of their number.
+        if args.graph_steps % nb:
+            sys.exit(f"bench.py: --graph-steps {args.graph_steps} must be a multiple of --buckets {nb} "
+                     "(each replay repeats the same captured steps)")
+        if args.steps % args.graph_steps or args.warmup % args.graph_steps:
+            sys.exit("bench.py: --steps and --warmup must be multiples of --graph-steps")
         launch()
         torch.cuda.synchronize()
+        cyc[0] = 0
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, stream=stream):
             for _ in range(args.graph_steps):
                 launch()
         step, per_call = graph.replay, args.graph_steps
-        assert args.steps % per_call == 0 and args.warmup % per_call == 0, "steps/warmup must be multiples of --graph-steps"
 
     settle(step, args.settle_ms)
     for _ in range(args.warmup // per_call):

@@ -88,18 +88,21 @@ def test_bench_n1_line(cuda, tmp_path):
     `roofline` (hbm bound, 8 TB/s peak, frac = achieved / peak, PMC traffic
     within 0.1 % of the algorithmic bytes) and `cpu_baseline` (the oracle's
     port of the reference path on the host cores) — with a short CPU sample
-    (--cpu-seconds 2) to keep the test brief; `--graph-steps` exercised too."""
+    (--cpu-seconds 2) to keep the test brief; `--graph-steps` exercised too
+    (a graph of 4 steps over the 4 cycled buckets: the self-check covers
+    every bucket the replays write)."""
     with open(os.path.join(ROOT, "BASELINE.json")) as f:
         base = json.load(f)
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
-    for extra in ([], ["--graph-steps", "2", "--no-cpu-baseline", "--no-side", "--no-rccl-collnet"]):
-        cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
+    for extra in ([], ["--graph-steps", "4", "--no-cpu-baseline", "--no-side", "--no-rccl-collnet"]):
+        cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "4",
                "--cpu-seconds", "2"] + extra
         rc, out, err, wall = run_child(cmd, env, str(tmp_path), 500, "bench.py --gpus 1")
         lines = [l for l in out.splitlines() if l.startswith("{")]
-        assert rc == 0 and lines, (rc, err[-1500:])
+        assert lines, (rc, err[-1500:])
         line = json.loads(lines[-1])
+        assert rc == 0, (rc, line.get("failures"), line.get("diagnostic_failures"), err[-800:])
         assert line["metric"] == base["metric"] and line["unit"] == "GB/s" and line["n_gpus"] == 1
         assert line["self_check"] is True and line["higher_is_better"] is True
         assert line["ms_per_step"] * line["steps"] / 1e3 < wall
