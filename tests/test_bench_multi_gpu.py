@@ -95,7 +95,8 @@ def test_bench_n1_line(cuda, tmp_path):
         base = json.load(f)
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
-    for extra in ([], ["--graph-steps", "4", "--no-cpu-baseline", "--no-side", "--no-rccl-collnet"]):
+    quick = ["--no-cpu-baseline", "--no-side", "--no-rccl-collnet"]
+    for extra in ([], ["--graph-steps", "4"] + quick, ["--buckets", "1"] + quick):
         cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "4",
                "--cpu-seconds", "2"] + extra
         rc, out, err, wall = run_child(cmd, env, str(tmp_path), 500, "bench.py --gpus 1")
@@ -105,6 +106,8 @@ def test_bench_n1_line(cuda, tmp_path):
         assert rc == 0, (rc, line.get("failures"), line.get("diagnostic_failures"), err[-800:])
         assert line["metric"] == base["metric"] and line["unit"] == "GB/s" and line["n_gpus"] == 1
         assert line["self_check"] is True and line["higher_is_better"] is True
+        nb = line["config"]["buckets_cycled"]
+        assert line["self_check_detail"]["buckets_checked_min_over_ranks"] == nb == (1 if "--buckets" in extra else 4)
         assert line["ms_per_step"] * line["steps"] / 1e3 < wall
         r = line["roofline"]
         assert r["bound"] == "hbm" and r["peak"] == bench.HBM_PEAK_GBPS and r["unit"] == "GB/s"
@@ -114,5 +117,5 @@ def test_bench_n1_line(cuda, tmp_path):
         if not extra:
             cb = line["cpu_baseline"]
             assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["unit"].startswith("GB/s")
-        else:
+        elif "--graph-steps" in extra:
             assert "hipGraph" in line["config"]["launch"]
