@@ -35,7 +35,7 @@ def _mode(mode):
 
 
 @pytest.mark.parametrize("mode", ["bulk", "fused", "fused-threads", "packet"])
-@pytest.mark.parametrize("T,W,P", [(1, 1, 256), (4, 2, 256), (3, 3, 64), (2, 8, 1024)])
+@pytest.mark.parametrize("T,W,P", [(1, 1, 256), (4, 2, 256), (3, 3, 64), (2, 8, 1024), (2, 5, 128), (3, 4, 512)])
 def test_allreduce_float_host_tensors(C, mode, T, W, P):
     n = 100_003 if mode != "packet" else 20_011
     C.start(C.make_config(num_workers=W, num_worker_threads=T, packet_numel=P, max_outstanding_packets=64 * T,
