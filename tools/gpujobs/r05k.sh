@@ -2,7 +2,7 @@
 # driver's N=1 command and the N=2 rehearsal at the driver's defaults.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-OUT=$GRAFT_REPO_ROOT/gpurun_out/r05k
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${JOB:-r05k}
 mkdir -p $OUT
 timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ > $OUT/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 $OUT/tests.log
