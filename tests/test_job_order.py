@@ -175,6 +175,49 @@ int main(int argc, char** argv) {
         delete b;
         return WIFEXITED(st) ? WEXITSTATUS(st) : 1;
     }
+    if (mode == "churn") {
+        // ADVICE r4 under load: K communicators in a row under one session.
+        // Worker 1 takes communicator k's key, says so, and closes at once;
+        // worker 0 closes comm k on that word and creates comm k + 1 — so
+        // worker 1's detach of k (possibly the last one, which removes the
+        // name) races worker 0's replacement of the name by k + 1.  Every
+        // communicator must deliver its own key; no segment in use may be lost.
+        const int K = atoi(argv[3]);
+        int up[2];
+        if (pipe(up)) return 9;
+        pid_t p = fork();
+        if (p == 0) {
+            for (int k = 0; k < K; k++) {
+                CallKey got{};
+                try {
+                    JobOrder b(session, 1, 2, 20000);
+                    while (!b.Peek(&got)) usleep(10);
+                    b.Consume();
+                    if (write(up[1], "c", 1) != 1) _exit(8);
+                } catch (const std::exception& e) {
+                    printf("follower %d: %s\n", k, e.what());
+                    fflush(stdout);
+                    _exit(4);
+                }
+                if (got.comm != (uint32_t)k) {
+                    printf("follower %d got comm %u\n", k, got.comm);
+                    fflush(stdout);
+                    _exit(5);
+                }
+            }
+            _exit(0);
+        }
+        char c;
+        for (int k = 0; k < K; k++) {
+            JobOrder a(session, 0, 2, 20000);
+            a.Append(CallKey{(uint32_t)k, 0, 0, 1, 7, 0});
+            if (read(up[0], &c, 1) != 1) return 7;
+        }
+        int st;
+        waitpid(p, &st, 0);
+        printf("churn done\n");
+        return WIFEXITED(st) ? WEXITSTATUS(st) : 1;
+    }
     try {                                            // "join": a second leader for the session
         JobOrder o(session, 0, 2, 2000);
         printf("joined\n");
@@ -258,6 +301,20 @@ def test_late_detach_keeps_the_new_segment(driver):
     session = f"late-{os.getpid()}"
     r = subprocess.run([driver, "late_detach", session], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "joined B" in r.stdout, r.stdout + r.stderr
+    assert not os.path.exists(f"/dev/shm/switchml-collnet-{session}")
+
+
+def test_churned_sessions_keep_every_communicator(driver):
+    """ADVICE r4 under load: 300 communicators in a row under one session,
+    each worker closing and reconnecting as fast as it can, the last
+    detach of one interleaving with worker 0's creation of the next: every
+    communicator delivers its own key, and the name is gone at the end.
+    (The check-then-unlink window itself is too narrow to hit on demand —
+    the round-4 code passes this too; the flock in unlink_if_named closes it
+    by construction.)"""
+    session = f"churn-{os.getpid()}"
+    r = subprocess.run([driver, "churn", session, "300"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "churn done" in r.stdout, r.stdout + r.stderr
     assert not os.path.exists(f"/dev/shm/switchml-collnet-{session}")
 
 
