@@ -1143,6 +1143,23 @@ def extra_measurements(sw, torch, x, P, stream, reps=20):
         t = timeit(rx_cycle)
     res["frames_rx_device_4sets_GBps"] = round((4 * N + fbytes) / t / 1e9, 1)
     del fsets, rxs
+    # INT32 job slices over the same wire format: B frames (no extra batch),
+    # payload = htonl of the words; and the receive side back to int32
+    xi = x.view(torch.int32)
+    fbytes_i = B * sw.frame_bytes(P)
+    iframes = torch.empty(fbytes_i, dtype=torch.uint8, device=x.device)
+    t = timeit(lambda: sw.pack_frames_int32(xi, fp, P, frames=iframes, stream=stream))
+    res["frames_int32_device_GBps"] = round((4 * N + fbytes_i) / t / 1e9, 1)
+    rxi = sw.RxSliceInt32(N, P, device=x.device)
+
+    def rxi_once():
+        rxi.reset(stream)
+        sw.unpack_frames_int32(iframes, B, rxi, stream=stream)
+    with torch.cuda.stream(stream):
+        t = timeit(rxi_once)
+    res["frames_int32_rx_device_GBps"] = round((4 * N + fbytes_i) / t / 1e9, 1)
+    res["frames_int32_round_trip_exact"] = bool(torch.equal(rxi.out, xi))
+    del iframes, rxi
     hframes = torch.empty(fbytes, dtype=torch.uint8).pin_memory()
     t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=hframes, stream=stream))
     res["frames_to_pinned_host_input_GBps"] = round(4 * N / t / 1e9, 2)

@@ -375,6 +375,27 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
                                    uint64_t* d_state, float* d_out, uint64_t* d_counts,
                                    void* stream);
 
+/* INT32 job slices (DataType::INT32, common.h:51-55) over the same frames.
+ * The INT32 pre/post-processor only reorders bytes and needs no extra batch
+ * (NeedsExtraBatch is false, ppp.cc:65-67), so a slice has B frames and frame
+ * p carries block p: BuildPacket's headers (as sml_quantize_pack_frames,
+ * extra-info bytes 0) and htonl of the block's words (ppp.cc:158-190; words
+ * past numel in the last frame are 0). */
+sml_status_t sml_pack_frames_int32(const int32_t* d_in, uint64_t numel, uint32_t packet_numel,
+                                   const sml_frame_params* params, void* frames, uint64_t frame_stride,
+                                   void* stream);
+
+/* The receive loop for an INT32 job slice: acceptance as for
+ * sml_dequantize_frames (this job, a pkt_id < B not received before, the
+ * first copy wins), and PostprocessSingle's INT32 branch (ppp.cc:262-298):
+ * ntohl of the accepted frame's words into d_out[pkt_id*P ..
+ * pkt_id*P + min(P, numel - pkt_id*P)).  d_state: uint64[B], zeroed per
+ * slice (sml_rx_reset), persists across calls; d_counts as for
+ * sml_dequantize_frames.  Two launches on `stream`. */
+sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, uint64_t frame_stride,
+                                     uint64_t numel, uint32_t packet_numel, uint64_t job_id,
+                                     uint64_t* d_state, int32_t* d_out, uint64_t* d_counts, void* stream);
+
 /* rte_bitmap_reset for one slice (dpdk_worker_thread.cc, per job slice):
  * zero d_state (uint64[B + b]) before the slice's first sml_dequantize_frames
  * call.  One async memset on `stream`. */

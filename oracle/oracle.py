@@ -69,6 +69,9 @@ def lib():
         L.orc_build_frames.restype = i32
         L.orc_build_frames.argtypes = [vp, u64, u64, u16, vp, u32, vp, vp, u64]
         L.orc_dequantize_frames.argtypes = [vp, u64, u64, u64, u64, u16, u32, u64, vp, vp, vp, vp]
+        L.orc_build_frames_i32.restype = i32
+        L.orc_build_frames_i32.argtypes = [vp, u64, u64, vp, vp, u64]
+        L.orc_unpack_frames_i32.argtypes = [vp, u64, u64, u64, u64, u64, vp, vp, vp]
         L.orc_pkt_id_to_pool_index.restype = ctypes.c_uint16
         L.orc_pkt_id_to_pool_index.argtypes = [u64, u32, u32, u32]
         L.orc_glibc_rand.argtypes = [u32, u64, vp]
@@ -232,6 +235,41 @@ def dequantize_frames(frames: np.ndarray, num_frames: int, stride: int, rx: RxSt
     counts = np.zeros(2, dtype=np.uint64)
     lib().orc_dequantize_frames(_p(frames), num_frames, stride, rx.numel, rx.P, num_workers, rx.batch_max,
                                 job_id, _p(rx.exps), _p(rx.seen), _p(rx.out), _p(counts))
+    rx.counts = [rx.counts[0] + int(counts[0]), rx.counts[1] + int(counts[1])]
+    return rx
+
+
+def build_frames_i32(x: np.ndarray, params, P: int = 256, stride: int | None = None) -> np.ndarray:
+    """DPDK frames of one INT32 slice: B frames (no extra batch), payload =
+    htonl of each block's words (ppp.cc:158-190)."""
+    x = np.ascontiguousarray(x, dtype=np.int32)
+    B = num_blocks(x.size, P)
+    stride = stride or 52 + 4 * P
+    out = np.zeros(B * stride, dtype=np.uint8)
+    rc = lib().orc_build_frames_i32(_p(x), x.size, P, ctypes.cast(ctypes.byref(params), ctypes.c_void_p),
+                                    _p(out), stride)
+    if rc != 0:
+        raise RuntimeError("orc_build_frames_i32 failed")
+    return out
+
+
+class RxStateI32:
+    """Receive-side state of one INT32 slice (rx bitmap over B pkt_ids, output)."""
+
+    def __init__(self, numel: int, P: int = 256):
+        self.numel, self.P = numel, P
+        self.seen = np.zeros(max(1, num_blocks(numel, P)), dtype=np.uint8)
+        self.out = np.zeros(numel, dtype=np.int32)
+        self.counts = [0, 0]
+
+
+def unpack_frames_i32(frames: np.ndarray, num_frames: int, stride: int, rx: RxStateI32, job_id: int = 0):
+    """The receive loop over INT32 frames in order (ntohl into rx.out)."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    assert frames.size >= num_frames * stride
+    counts = np.zeros(2, dtype=np.uint64)
+    lib().orc_unpack_frames_i32(_p(frames), num_frames, stride, rx.numel, rx.P, job_id, _p(rx.seen),
+                                _p(rx.out), _p(counts))
     rx.counts = [rx.counts[0] + int(counts[0]), rx.counts[1] + int(counts[1])]
     return rx
 

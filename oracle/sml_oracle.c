@@ -479,6 +479,96 @@ static uint16_t raw_cksum(const uint8_t* b, size_t len) {
 
 static void put16be(uint8_t* p, uint16_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
 
+/* Frame p's headers (BuildPacket, dpdk_worker_thread_utils.inc:73-126):
+ * Ethernet, IPv4, UDP (pseudo-header checksum), SwitchML header; returns the
+ * SwitchML header (extra info at +8, entries at +10).  The frame is zeroed
+ * first: bytes the reference leaves stale are written as 0. */
+static uint8_t* frame_header(uint8_t* f, uint64_t p, uint64_t P, uint64_t data_len, const orc_frame_params* prm) {
+    memset(f, 0, data_len);
+    /* 1. Ethernet */
+    memcpy(f + 0, prm->dst_mac, 6);
+    memcpy(f + 6, prm->src_mac, 6);
+    put16be(f + 12, 0x0800);
+    /* 2. IPv4 */
+    uint8_t* ip = f + 14;
+    ip[0] = 0x45;
+    put16be(ip + 2, (uint16_t)(data_len - 14));
+    ip[8] = 128;          /* ttl */
+    ip[9] = 17;           /* IPPROTO_UDP */
+    memcpy(ip + 12, &prm->src_ip_be, 4);
+    memcpy(ip + 16, &prm->dst_ip_be, 4);
+    /* 3. UDP */
+    uint8_t* udp = ip + 20;
+    memcpy(udp + 0, &prm->src_port_be, 2);
+    memcpy(udp + 2, &prm->dst_port_be, 2);
+    put16be(udp + 4, (uint16_t)(data_len - 34));
+    uint8_t psd[12];
+    memcpy(psd + 0, ip + 12, 4);
+    memcpy(psd + 4, ip + 16, 4);
+    psd[8] = 0;
+    psd[9] = ip[9];
+    put16be(psd + 10, (uint16_t)(data_len - 14 - 20)); /* l3 len - ihl*4 */
+    uint16_t ck = raw_cksum(psd, 12);
+    memcpy(udp + 6, &ck, 2);
+    /* 4. SwitchML header */
+    uint8_t* h = udp + 8;
+    uint8_t len_enum = P < 64 ? 0 : P < 128 ? 1 : P < 256 ? 2 : 3;
+    h[0] = (uint8_t)((1 << 4) + len_enum);
+    h[1] = (uint8_t)prm->job_id;
+    uint32_t pid = (uint32_t)p;
+    memcpy(h + 2, &pid, 4); /* host order */
+    put16be(h + 6, orc_pkt_id_to_pool_index(p, prm->pool_index_start, prm->pool_index_shift,
+                                            prm->max_outstanding_pkts));
+    return h;
+}
+
+/* INT32 jobs (DataType::INT32): no extra batch (NeedsExtraBatch is false for
+ * INT32, ppp.cc:65-67), so B frames; frame p = BuildPacket's headers + the
+ * INT32 PreprocessSingle of block p (ppp.cc:158-190: htonl of each word, only
+ * the n real words; the extra-info bytes are left as they were — 0 here). */
+int orc_build_frames_i32(const int32_t* in, uint64_t numel, uint64_t P, const orc_frame_params* prm,
+                         uint8_t* frames, uint64_t stride) {
+    const uint64_t B = orc_num_blocks(numel, P);
+    const uint64_t data_len = 14 + 20 + 8 + 8 + P * 4 + 2;
+    if (stride < data_len) return -1;
+    for (uint64_t p = 0; p < B; p++) {
+        uint8_t* entries = frame_header(frames + p * stride, p, P, data_len, prm) + 10;
+        const uint64_t off = p * P, n = numel - off < P ? numel - off : P;
+        for (uint64_t i = 0; i < n; i++) {
+            uint32_t w = bswap32((uint32_t)in[off + i]);
+            memcpy(entries + 4 * i, &w, 4);
+        }
+    }
+    return 0;
+}
+
+/* The receive loop for an INT32 job slice (dpdk_worker_thread.cc:300-345):
+ * discard a pkt_id already received or a frame of another job, otherwise
+ * PostprocessSingle's INT32 branch (ppp.cc:262-298): ntohl of the n real
+ * words of block pkt_id into out.  pkt_id >= B is counted as discarded.
+ * `seen` (one byte per pkt_id, B) carries over between calls of one slice. */
+void orc_unpack_frames_i32(const uint8_t* frames, uint64_t num_frames, uint64_t stride, uint64_t numel,
+                           uint64_t P, uint64_t job_id, uint8_t* seen, int32_t* out, uint64_t counts[2]) {
+    const uint64_t B = orc_num_blocks(numel, P);
+    for (uint64_t f = 0; f < num_frames; f++) {
+        const uint8_t* fr = frames + f * stride;
+        uint32_t pid;
+        memcpy(&pid, fr + 44, 4);
+        if (pid >= B || seen[pid] || fr[43] != (uint8_t)job_id) {
+            counts[1]++;
+            continue;
+        }
+        seen[pid] = 1;
+        counts[0]++;
+        const uint64_t off = (uint64_t)pid * P, n = numel - off < P ? numel - off : P;
+        for (uint64_t i = 0; i < n; i++) {
+            uint32_t w;
+            memcpy(&w, fr + 52 + 4 * i, 4);
+            out[off + i] = (int32_t)bswap32(w);
+        }
+    }
+}
+
 int orc_build_frames(const float* in, uint64_t numel, uint64_t P, uint16_t W, const int8_t* global_exps,
                      uint32_t batch_max, const orc_frame_params* prm, uint8_t* frames, uint64_t stride) {
     const uint64_t B = orc_num_blocks(numel, P);
@@ -488,42 +578,7 @@ int orc_build_frames(const float* in, uint64_t numel, uint64_t P, uint16_t W, co
     float lut[256];
     orc_scale_lut(W, lut);
     for (uint64_t p = 0; p < B + b; p++) {
-        uint8_t* f = frames + p * stride;
-        memset(f, 0, data_len);
-        /* 1. Ethernet */
-        memcpy(f + 0, prm->dst_mac, 6);
-        memcpy(f + 6, prm->src_mac, 6);
-        put16be(f + 12, 0x0800);
-        /* 2. IPv4 */
-        uint8_t* ip = f + 14;
-        ip[0] = 0x45;
-        put16be(ip + 2, (uint16_t)(data_len - 14));
-        ip[8] = 128;          /* ttl */
-        ip[9] = 17;           /* IPPROTO_UDP */
-        memcpy(ip + 12, &prm->src_ip_be, 4);
-        memcpy(ip + 16, &prm->dst_ip_be, 4);
-        /* 3. UDP */
-        uint8_t* udp = ip + 20;
-        memcpy(udp + 0, &prm->src_port_be, 2);
-        memcpy(udp + 2, &prm->dst_port_be, 2);
-        put16be(udp + 4, (uint16_t)(data_len - 34));
-        uint8_t psd[12];
-        memcpy(psd + 0, ip + 12, 4);
-        memcpy(psd + 4, ip + 16, 4);
-        psd[8] = 0;
-        psd[9] = ip[9];
-        put16be(psd + 10, (uint16_t)(data_len - 14 - 20)); /* l3 len - ihl*4 */
-        uint16_t ck = raw_cksum(psd, 12);
-        memcpy(udp + 6, &ck, 2);
-        /* 4. SwitchML header */
-        uint8_t* h = udp + 8;
-        uint8_t len_enum = P < 64 ? 0 : P < 128 ? 1 : P < 256 ? 2 : 3;
-        h[0] = (uint8_t)((1 << 4) + len_enum);
-        h[1] = (uint8_t)prm->job_id;
-        uint32_t pid = (uint32_t)p;
-        memcpy(h + 2, &pid, 4); /* host order */
-        put16be(h + 6, orc_pkt_id_to_pool_index(p, prm->pool_index_start, prm->pool_index_shift,
-                                                prm->max_outstanding_pkts));
+        uint8_t* h = frame_header(frames + p * stride, p, P, data_len, prm);
         /* PreprocessSingle(p, entries = h + 10, extra = h + 8) — ppp.cc:69-156 */
         uint8_t* extra = h + 8;
         uint8_t* entries = h + 10;

@@ -132,6 +132,13 @@ uint16_t orc_pkt_id_to_pool_index(uint64_t pkt_id, uint32_t start, uint32_t shif
 int orc_build_frames(const float* in, uint64_t numel, uint64_t P, uint16_t num_workers,
                      const int8_t* global_exps, uint32_t batch_max, const orc_frame_params* prm,
                      uint8_t* frames, uint64_t stride);
+/* INT32 job slices: B frames (no extra batch), payload = htonl of block p's
+ * words (ppp.cc:158-190), and the receive loop with the INT32 PostprocessSingle
+ * (ntohl into out, ppp.cc:262-298); `seen` (uint8[B]) carries over. */
+int orc_build_frames_i32(const int32_t* in, uint64_t numel, uint64_t P, const orc_frame_params* prm,
+                         uint8_t* frames, uint64_t stride);
+void orc_unpack_frames_i32(const uint8_t* frames, uint64_t num_frames, uint64_t stride, uint64_t numel,
+                           uint64_t P, uint64_t job_id, uint8_t* seen, int32_t* out, uint64_t counts[2]);
 /* Receive loop of DpdkWorkerThread + PostprocessSingle over received frames
  * (dpdk_worker_thread.cc:300-345, ppp.cc:197-260).  counts[0] += accepted,
  * counts[1] += discarded; exps (int8[B]) and seen (uint8[B + b], the rx

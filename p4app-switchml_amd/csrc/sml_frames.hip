@@ -76,7 +76,10 @@ __device__ __forceinline__ uint32_t pool_dword(const FrameArgs& a, uint32_t i, u
 // cycled, 256 MiB bucket, profiles/r04/ab_frames_nt.json): 98.1 -> 86.4 us;
 // non-temporal header dwords as well: 109.6 us (partial-line stores), so
 // headers keep the default policy.
-template <int P, bool ALIGNED, bool GLOBAL, bool NTS = false>
+// I32: an INT32 job slice (DataType::INT32): no extra batch (a.b = 0), so
+// frame f carries block f; its payload is htonl of the block's words
+// (ppp.cc:158-190) and its exponent byte 0 — the same tile walk, no scale.
+template <int P, bool ALIGNED, bool GLOBAL, bool NTS = false, bool I32 = false>
 __global__ __attribute__((amdgpu_waves_per_eu(8, 8))) __launch_bounds__(kBlockThreads)
 void k_quantize_frames(FrameArgs a) {
     __shared__ float lut[256];
@@ -98,13 +101,18 @@ void k_quantize_frames(FrameArgs a) {
     uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
     f4 v[kU];
     if (t < a.ntiles) load_tile<ALIGNED>(qa, t * kTileElems, lane, v);
-    build_lut(lut, a.W);
+    if constexpr (!I32) build_lut(lut, a.W);
     for (bool first = true; t < a.ntiles; t += nwaves, first = false) {
         const uint64_t base = t * kTileElems;
         const uint64_t pk0 = base / P;                     // first block of the tile
         if (!first) load_tile<ALIGNED>(qa, base, lane, v); // later tiles (grid-stride)
         int eloc[kU];
-        tile_exponents<P>(v, eloc);
+        if constexpr (I32) {
+#pragma unroll
+            for (int u = 0; u < kU; u++) eloc[u] = 0;
+        } else {
+            tile_exponents<P>(v, eloc);
+        }
         // exponent of packet j of the tile: slice j*P/256, lane (j*P/4) % 64
         uint32_t ej[kPk];
 #pragma unroll
@@ -164,9 +172,16 @@ void k_quantize_frames(FrameArgs a) {
             const uint64_t idx = base + (uint64_t)(u * kWave + lane) * 4;
             if (idx >= padded) continue;
             const uint64_t k = idx / P;
-            int e = eloc[u];
-            if constexpr (GLOBAL) e = a.gexp[k];
-            const u4 q = quantize4<false>(v[u], lut[(uint8_t)e], idx, 0);
+            u4 q;
+            if constexpr (I32) {
+                // the words as loaded (whole-vector bit cast: hipcc's bit cast of one
+                // vector component returned component x for every component)
+                q = __builtin_bit_cast(u4, v[u]);
+            } else {
+                int e = eloc[u];
+                if constexpr (GLOBAL) e = a.gexp[k];
+                q = quantize4<false>(v[u], lut[(uint8_t)e], idx, 0);
+            }
             uint32_t* dst = reinterpret_cast<uint32_t*>(a.frames + (k + a.b) * a.stride + 52) + (idx - k * P);
             const u4a wq{bswap(q.x), bswap(q.y), bswap(q.z), bswap(q.w)};
             if constexpr (NTS) SML_NT_STORE16_UNALIGNED(wq, reinterpret_cast<u4a*>(dst));
@@ -286,14 +301,19 @@ __device__ __forceinline__ bool rx_winner(unsigned long long sw, uint64_t nframe
     return hi != 0u && hi != kRxDone && f < nframes;
 }
 
-template <int P, bool NT = false>
+// I32: an INT32 job slice — no extra batch (a.b = 0: pkt_id k carries block
+// k), no exponents, and PostprocessSingle's INT32 branch (ppp.cc:262-298):
+// ntohl of the words into out, no scale.
+template <int P, bool NT = false, bool I32 = false>
 __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     __shared__ float lut[256];
     // power-of-two W: the table holds exact reciprocals and dequantize multiplies
     // (bit-equal to the IEEE division, rcp_scale_pow2); otherwise scales
     const bool pow2 = (a.W & (a.W - 1)) == 0;
-    if (pow2) build_rcp_lut(lut, a.W);
-    else build_lut(lut, a.W);
+    if constexpr (!I32) {
+        if (pow2) build_rcp_lut(lut, a.W);
+        else build_lut(lut, a.W);
+    }
     constexpr int kRxU = rx_slices(P);
     constexpr int kRxTileElems = kRxU * kWave * 4;
     constexpr int kChunksPerFrame = P / 4;     // 16-B chunks per payload
@@ -325,7 +345,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             for (int u = 0; u < kRxU; u++) {
                 const uint64_t k = t * kBlocksPerTile + (u * kWave) / kChunksPerFrame;
                 ok[u] = rx_winner(sw[u], a.nframes, f[u]) && k < a.nblocks;
-                s[u] = lut[(uint32_t)se[u] & 0xffu];
+                if constexpr (!I32) s[u] = lut[(uint32_t)se[u] & 0xffu];
             }
         } else {
 #pragma unroll
@@ -339,7 +359,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             for (int u = 0; u < kRxU; u++) {
                 const uint64_t k = t * kBlocksPerTile + (u * kWave + lane) / kChunksPerFrame;
                 ok[u] = rx_winner(sw[u], a.nframes, f[u]) && k < a.nblocks;
-                s[u] = lut[(uint32_t)se[u] & 0xffu];
+                if constexpr (!I32) s[u] = lut[(uint32_t)se[u] & 0xffu];
             }
         }
         // Non-temporal payload loads (25 % faster than default-policy loads for
@@ -361,7 +381,9 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
         f4 o[kRxU];
 #pragma unroll
         for (int u = 0; u < kRxU; u++) {
-            if (pow2)
+            if constexpr (I32)
+                o[u] = __builtin_bit_cast(f4, mku4(bswap(w[u].x), bswap(w[u].y), bswap(w[u].z), bswap(w[u].w)));
+            else if (pow2)
                 o[u] = mkf4((float)(int32_t)bswap(w[u].x) * s[u], (float)(int32_t)bswap(w[u].y) * s[u],
                             (float)(int32_t)bswap(w[u].z) * s[u], (float)(int32_t)bswap(w[u].w) * s[u]);
             else
@@ -393,7 +415,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             const uint32_t hw = (uint32_t)(sw[u] >> 32), he = (uint32_t)(se[u] >> 32);
             if (hw != 0u && hw != kRxDone)
                 a.state[k + a.b] = ((unsigned long long)kRxDone << 32) | (sw[u] & 0xffull);
-            if (he != 0u) a.exps[k] = (int8_t)(se[u] & 0xffull);
+            if constexpr (!I32)
+                if (he != 0u) a.exps[k] = (int8_t)(se[u] & 0xffull);
             if (k < a.b && he != 0u && he != kRxDone)
                 a.state[k] = ((unsigned long long)kRxDone << 32) | (se[u] & 0xffull);
         }
@@ -402,11 +425,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
 
 // ------------------------------------------------------------ host side
 
-template <bool ALIGNED, bool GLOBAL>
+template <bool ALIGNED, bool GLOBAL, bool I32 = false>
 static void launch_frames_p(uint32_t P, bool nts, dim3 grid, hipStream_t st, const FrameArgs& a) {
 #define SML_FR(PN)                                                                                   \
-    if (nts) k_quantize_frames<PN, ALIGNED, GLOBAL, true><<<grid, kBlockThreads, 0, st>>>(a);        \
-    else k_quantize_frames<PN, ALIGNED, GLOBAL, false><<<grid, kBlockThreads, 0, st>>>(a);
+    if (nts) k_quantize_frames<PN, ALIGNED, GLOBAL, true, I32><<<grid, kBlockThreads, 0, st>>>(a);   \
+    else k_quantize_frames<PN, ALIGNED, GLOBAL, false, I32><<<grid, kBlockThreads, 0, st>>>(a);
     switch (P) {
         case 64:   SML_FR(64) break;
         case 128:  SML_FR(128) break;
@@ -417,22 +440,23 @@ static void launch_frames_p(uint32_t P, bool nts, dim3 grid, hipStream_t st, con
 #undef SML_FR
 }
 
-template <bool NT>
+template <bool NT, bool I32>
 static void launch_rx_apply_nt(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
     switch (P) {
-        case 64:   k_rx_apply<64, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_rx_apply<128, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_rx_apply<256, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_rx_apply<512, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_rx_apply<1024, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   k_rx_apply<64, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_rx_apply<128, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_rx_apply<256, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_rx_apply<512, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_rx_apply<1024, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
     }
 }
 
-// The fp32 output of a slice from the non-temporal threshold on takes
+// The output of a slice from the non-temporal threshold on takes
 // non-temporal stores, as K4's does (sml_set_payload_nt_threshold).
+template <bool I32 = false>
 static void launch_rx_apply(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
-    if (4 * a.numel >= g_nt_threshold.load(std::memory_order_relaxed)) launch_rx_apply_nt<true>(P, grid, st, a);
-    else launch_rx_apply_nt<false>(P, grid, st, a);
+    if (4 * a.numel >= g_nt_threshold.load(std::memory_order_relaxed)) launch_rx_apply_nt<true, I32>(P, grid, st, a);
+    else launch_rx_apply_nt<false, I32>(P, grid, st, a);
 }
 
 }  // namespace sml
@@ -443,29 +467,26 @@ extern "C" {
 
 uint64_t sml_frame_bytes(uint32_t packet_numel) { return 52ull + 4ull * packet_numel; }
 
-sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_t P, uint16_t W,
-                                      const int8_t* d_global_exps, uint32_t batch_max,
-                                      const sml_frame_params* prm, void* frames, uint64_t stride, void* stream) {
-    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
-    if (W == 0 || !prm || batch_max == 0) return SML_ERR_INVALID_ARG;
-    if (numel == 0) return SML_OK;
-    if (!d_in || !aligned4(d_in) || !frames) return SML_ERR_INVALID_ARG;
-    if (!aligned4(frames) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
-    FrameArgs a;
+}  // extern "C"
+
+namespace sml {
+
+// FrameArgs of one slice's frames: geometry, pool indices and the constant
+// header bytes 0..43 (BuildPacket, dpdk_worker_thread_utils.inc:76-126).
+static void frame_args(const sml_frame_params* prm, uint64_t numel, uint32_t P, uint16_t W, uint64_t b,
+                       void* frames, uint64_t stride, FrameArgs& a) {
     a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
-    a.in = d_in;
     a.numel = numel;
     a.nblocks = sml_num_blocks(numel, P);
     a.ntiles = (a.nblocks * P + kTileElems - 1) / kTileElems;
-    a.b = a.nblocks < batch_max ? a.nblocks : batch_max;
-    a.gexp = d_global_exps;
+    a.b = b;
+    a.gexp = nullptr;
     a.frames = static_cast<uint8_t*>(frames);
     a.stride = stride;
     a.W = W;
     a.pool_start = prm->pool_index_start;
     a.pool_shift = prm->pool_index_shift;
     a.mop = prm->max_outstanding_pkts ? prm->max_outstanding_pkts : 1;
-    // Constant header bytes 0..43 (BuildPacket, dpdk_worker_thread_utils.inc:76-126).
     uint8_t h[44];
     memset(h, 0, sizeof(h));
     const uint32_t data_len = (uint32_t)sml_frame_bytes(P);
@@ -492,24 +513,62 @@ sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_
     h[42] = (uint8_t)((1 << 4) + (P < 64 ? 0 : P < 128 ? 1 : P < 256 ? 2 : 3));  // job_type_size
     h[43] = (uint8_t)prm->job_id;                                                // short_job_id
     memcpy(a.hdr, h, 44);
+}
+
+// Payload store policy: non-temporal for a frame set in device memory from
+// the threshold on (written once, handed on); host frames (a NIC's pinned
+// mbufs) keep the default policy.
+static bool frames_nt(const void* frames, uint64_t bytes) {
+    if (bytes < g_nt_threshold.load(std::memory_order_relaxed)) return false;
+    hipPointerAttribute_t pa;
+    if (hipPointerGetAttributes(&pa, frames) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return pa.type == hipMemoryTypeDevice;
+}
+
+}  // namespace sml
+
+extern "C" {
+
+sml_status_t sml_quantize_pack_frames(const float* d_in, uint64_t numel, uint32_t P, uint16_t W,
+                                      const int8_t* d_global_exps, uint32_t batch_max,
+                                      const sml_frame_params* prm, void* frames, uint64_t stride, void* stream) {
+    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
+    if (W == 0 || !prm || batch_max == 0) return SML_ERR_INVALID_ARG;
+    if (numel == 0) return SML_OK;
+    if (!d_in || !aligned4(d_in) || !frames) return SML_ERR_INVALID_ARG;
+    if (!aligned4(frames) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
+    FrameArgs a;
+    const uint64_t B = sml_num_blocks(numel, P);
+    frame_args(prm, numel, P, W, B < batch_max ? B : batch_max, frames, stride, a);
+    a.in = d_in;
+    a.gexp = d_global_exps;
     dim3 grid(grid_for_tiles(a.ntiles));
     hipStream_t st = (hipStream_t)stream;
     const bool al = aligned16(d_in);
-    // payload store policy: non-temporal for a frame set in device memory from
-    // the threshold on (written once, handed on); host frames (a NIC's pinned
-    // mbufs) keep the default policy
-    bool nts = (a.nblocks + a.b) * stride >= g_nt_threshold.load(std::memory_order_relaxed);
-    if (nts) {
-        hipPointerAttribute_t pa;
-        if (hipPointerGetAttributes(&pa, frames) != hipSuccess) {
-            (void)hipGetLastError();
-            nts = false;
-        } else {
-            nts = pa.type == hipMemoryTypeDevice;
-        }
-    }
+    const bool nts = frames_nt(frames, (a.nblocks + a.b) * stride);
     if (d_global_exps) { if (al) launch_frames_p<true, true>(P, nts, grid, st, a); else launch_frames_p<false, true>(P, nts, grid, st, a); }
     else               { if (al) launch_frames_p<true, false>(P, nts, grid, st, a); else launch_frames_p<false, false>(P, nts, grid, st, a); }
+    return launch_check();
+}
+
+sml_status_t sml_pack_frames_int32(const int32_t* d_in, uint64_t numel, uint32_t P, const sml_frame_params* prm,
+                                   void* frames, uint64_t stride, void* stream) {
+    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
+    if (!prm) return SML_ERR_INVALID_ARG;
+    if (numel == 0) return SML_OK;
+    if (!d_in || !aligned4(d_in) || !frames) return SML_ERR_INVALID_ARG;
+    if (!aligned4(frames) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
+    FrameArgs a;
+    frame_args(prm, numel, P, 1, 0, frames, stride, a);       // INT32: no extra batch
+    a.in = reinterpret_cast<const float*>(d_in);              // words moved as bits
+    dim3 grid(grid_for_tiles(a.ntiles));
+    hipStream_t st = (hipStream_t)stream;
+    const bool nts = frames_nt(frames, a.nblocks * stride);
+    if (aligned16(d_in)) launch_frames_p<true, false, true>(P, nts, grid, st, a);
+    else launch_frames_p<false, false, true>(P, nts, grid, st, a);
     return launch_check();
 }
 
@@ -545,6 +604,39 @@ sml_status_t sml_dequantize_frames(const void* frames, uint64_t num_frames, uint
     const uint64_t tile = (uint64_t)U * kWave * 4;
     const uint64_t ntiles = (a.nblocks * P + tile - 1) / tile;
     if (ntiles) launch_rx_apply(P, dim3(grid_for_tiles(ntiles)), st, a);
+    return launch_check();
+}
+
+sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, uint64_t stride, uint64_t numel,
+                                     uint32_t P, uint64_t job_id, uint64_t* d_state, int32_t* d_out,
+                                     uint64_t* d_counts, void* stream) {
+    if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
+    if (num_frames == 0) return SML_OK;
+    if (num_frames >= 0xFFFFFFFEull) return SML_ERR_UNSUPPORTED;
+    if (!frames || !d_state || (numel && !d_out)) return SML_ERR_INVALID_ARG;
+    if (!aligned4(frames) || !aligned4(d_out) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
+    if (((uintptr_t)d_state & 7u) || (d_counts && ((uintptr_t)d_counts & 7u))) return SML_ERR_ALIGNMENT;
+    RxArgs a;
+    const uint32_t U = (uint32_t)rx_slices((int)P);
+    a.xcd = U < 4 ? g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U)
+                  : g_xcd_chunk.load(std::memory_order_relaxed);
+    a.frames = static_cast<const uint8_t*>(frames);
+    a.nframes = num_frames;
+    a.stride = stride;
+    a.numel = numel;
+    a.nblocks = sml_num_blocks(numel, P);
+    a.b = 0;                                                  // INT32: no extra batch
+    a.state = reinterpret_cast<unsigned long long*>(d_state);
+    a.exps = nullptr;
+    a.out = reinterpret_cast<float*>(d_out);                  // words stored as bits
+    a.counts = reinterpret_cast<unsigned long long*>(d_counts);
+    a.W = 1;
+    a.job = (uint8_t)job_id;
+    hipStream_t st = (hipStream_t)stream;
+    k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
+    const uint64_t tile = (uint64_t)U * kWave * 4;
+    const uint64_t ntiles = (a.nblocks * P + tile - 1) / tile;
+    if (ntiles) launch_rx_apply<true>(P, dim3(grid_for_tiles(ntiles)), st, a);
     return launch_check();
 }
 

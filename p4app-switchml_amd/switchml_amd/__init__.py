@@ -139,6 +139,10 @@ def lib():
     L.sml_dequantize_frames.argtypes = [vp, u64, u64, u64, u32, u16, u32, u64, vp, vp, vp, vp, vp]
     L.sml_rx_reset.restype = i32
     L.sml_rx_reset.argtypes = [vp, u64, vp]
+    L.sml_pack_frames_int32.restype = i32
+    L.sml_pack_frames_int32.argtypes = [vp, u64, u32, ctypes.POINTER(FrameParams), vp, u64, vp]
+    L.sml_unpack_frames_int32.restype = i32
+    L.sml_unpack_frames_int32.argtypes = [vp, u64, u64, u64, u32, u64, vp, vp, vp, vp]
     L.sml_switch_aggregate.restype = i32
     L.sml_switch_aggregate.argtypes = [vp, vp, u16, u64, u32, vp, vp, vp, u32, vp]
     L.sml_copy_segments.restype = i32
@@ -628,6 +632,52 @@ def dequantize_frames(frames, num_frames: int, rx: RxSlice, num_workers: int = 1
         _dev(frames, torch.uint8, "frames"), num_frames, stride, rx.numel, rx.packet_numel, num_workers,
         rx.batch_max, job_id, _dev(rx.exps, torch.int8, "exps"), _dev(rx.state, torch.int64, "state"),
         _dev(rx.out, torch.float32, "out"), _dev(rx.counts, torch.int64, "counts"), _stream(stream, rx.out)))
+    return rx.out
+
+
+def pack_frames_int32(x, params: FrameParams, packet_numel: int = 256, frames=None, stride: int | None = None,
+                      stream=None):
+    """An INT32 job slice straight into DPDK frames: B frames (no extra
+    batch), frame p = BuildPacket's headers + htonl of block p's words."""
+    torch = _torch()
+    B = num_blocks(x.numel(), packet_numel)
+    stride = stride or frame_bytes(packet_numel)
+    if frames is None:
+        frames = torch.empty(B * stride, dtype=torch.uint8, device=x.device)
+    _check("sml_pack_frames_int32", lib().sml_pack_frames_int32(
+        _dev(x, torch.int32, "x"), x.numel(), packet_numel, ctypes.byref(params),
+        _dev(frames, torch.uint8, "frames"), stride, _stream(stream, x)))
+    return frames
+
+
+class RxSliceInt32:
+    """Receive-side state of one INT32 job slice for unpack_frames_int32: the
+    rx bitmap over its B pkt_ids, {accepted, discarded} counters, the output."""
+
+    def __init__(self, numel: int, packet_numel: int = 256, device="cuda", out=None):
+        torch = _torch()
+        self.numel, self.packet_numel = numel, packet_numel
+        self.state = torch.zeros(max(1, num_blocks(numel, packet_numel)), dtype=torch.int64, device=device)
+        self.counts = torch.zeros(2, dtype=torch.int64, device=device)
+        self.out = out if out is not None else torch.zeros(numel, dtype=torch.int32, device=device)
+
+    def reset(self, stream=None):
+        """rte_bitmap_reset for a new job slice (sml_rx_reset)."""
+        torch = _torch()
+        _check("sml_rx_reset", lib().sml_rx_reset(_dev(self.state, torch.int64, "state"), self.state.numel(),
+                                                  _stream(stream, self.state)))
+
+
+def unpack_frames_int32(frames, num_frames: int, rx: RxSliceInt32, job_id: int = 0, stride: int | None = None,
+                        stream=None):
+    """PostprocessSingle's INT32 branch over received DPDK frames (any order;
+    duplicates, other jobs' frames and pkt_id >= B discarded): ntohl into rx.out."""
+    torch = _torch()
+    stride = stride or frame_bytes(rx.packet_numel)
+    _check("sml_unpack_frames_int32", lib().sml_unpack_frames_int32(
+        _dev(frames, torch.uint8, "frames"), num_frames, stride, rx.numel, rx.packet_numel, job_id,
+        _dev(rx.state, torch.int64, "state"), _dev(rx.out, torch.int32, "out"),
+        _dev(rx.counts, torch.int64, "counts"), _stream(stream, rx.out)))
     return rx.out
 
 
