@@ -408,7 +408,9 @@ sml_status_t sml_rx_reset(uint64_t* d_state, uint64_t num_words, void* stream);
  * immediate: imm = (msg_id & 0xFFFF) | (exponent byte << 16), byte 3 = 0
  * (rdma_worker_thread.cc:341-356; PreprocessSingle writes byte 2).  Message
  * m in [0, B + b) carries exps[m] for m < B; the byte is 0 for m >= B.
- * d_imm: uint32[B + b] (host byte order, as ibv_send_wr.imm_data is filled). */
+ * d_imm: uint32[B + b] (host byte order, as ibv_send_wr.imm_data is filled).
+ * d_exps null: an INT32 slice — B messages (no extra batch, ppp.cc:65-67),
+ * imm = msg_id & 0xFFFF (the INT32 PreprocessSingle leaves byte 2 alone). */
 sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t num_blocks, uint32_t batch_max,
                           uint32_t* d_imm, void* stream);
 

@@ -391,7 +391,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rdma_imm(const int8_t* exps, 
                                                             uint32_t* imm) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
     for (uint64_t m = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; m < total; m += stride) {
-        const uint32_t e = m < B ? (uint32_t)(uint8_t)exps[m] : 0u;
+        const uint32_t e = exps && m < B ? (uint32_t)(uint8_t)exps[m] : 0u;
         imm[m] = (uint32_t)(m & 0xFFFFu) | (e << 16);
     }
 }
@@ -796,8 +796,9 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
 
 sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t B, uint32_t batch_max, uint32_t* d_imm, void* stream) {
     if (B == 0) return SML_OK;
-    if (!d_exps || !d_imm || batch_max == 0) return SML_ERR_INVALID_ARG;
-    const uint64_t total = B + (B < batch_max ? B : batch_max);
+    if (!d_imm || (d_exps && batch_max == 0)) return SML_ERR_INVALID_ARG;
+    // d_exps null: an INT32 slice — B messages (no extra batch), byte 2 untouched (0)
+    const uint64_t total = d_exps ? B + (B < batch_max ? B : batch_max) : B;
     k_rdma_imm<<<grid_for_vec(total), kBlockThreads, 0, (hipStream_t)stream>>>(d_exps, B, total, d_imm);
     return launch_check();
 }

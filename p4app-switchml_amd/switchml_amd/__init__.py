@@ -681,10 +681,17 @@ def unpack_frames_int32(frames, num_frames: int, rx: RxSliceInt32, job_id: int =
     return rx.out
 
 
-def rdma_imm(exps, batch_max: int = 64, stream=None):
+def rdma_imm(exps, batch_max: int = 64, stream=None, num_blocks_int32: int | None = None, device=None):
     """RDMA immediates of one slice's B + b messages (uint32 in host order, as
-    int32 tensor): (msg_id & 0xFFFF) | exponent << 16."""
+    int32 tensor): (msg_id & 0xFFFF) | exponent << 16.  exps=None with
+    num_blocks_int32=B: an INT32 slice's B messages, msg_id & 0xFFFF."""
     torch = _torch()
+    if exps is None:
+        B = int(num_blocks_int32)
+        out = torch.empty(B, dtype=torch.int32, device=device or "cuda")
+        _check("sml_rdma_imm", lib().sml_rdma_imm(None, B, batch_max, _dev(out, torch.int32, "imm"),
+                                                 _stream(stream, out)))
+        return out
     B = exps.numel()
     out = torch.empty(B + min(B, batch_max), dtype=torch.int32, device=exps.device)
     _check("sml_rdma_imm", lib().sml_rdma_imm(_dev(exps, torch.int8, "exps"), B, batch_max,

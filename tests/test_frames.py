@@ -161,3 +161,7 @@ def test_rdma_messages(cuda, n):
     assert np.array_equal(payload.cpu().numpy().view(np.uint32), O.quantize(x, P, W))
     imm = sw.rdma_imm(exps, bm).cpu().numpy().view(np.uint32)
     assert np.array_equal(imm, rdma_imm_reference(O.exponents(x, P), bm))
+    # an INT32 slice of the same size: B messages, the immediate is the msg id alone
+    B = exps.numel()
+    imm_i = sw.rdma_imm(None, num_blocks_int32=B, device=cuda).cpu().numpy().view(np.uint32)
+    assert np.array_equal(imm_i, (np.arange(B) & 0xFFFF).astype(np.uint32))
