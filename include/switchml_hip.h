@@ -401,6 +401,13 @@ sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, ui
  * call.  One async memset on `stream`. */
 sml_status_t sml_rx_reset(uint64_t* d_state, uint64_t num_words, void* stream);
 
+/* ncclUint8 buckets of the CollNet plugin (switchml_plugin.cc:318-337,
+ * 370-378: "SwitchML does not really support uint8"): each byte widened to an
+ * int32 for the INT32 all-reduce, and the summed words narrowed back (mod
+ * 256).  Device or device-mapped memory; one launch each on `stream`. */
+sml_status_t sml_widen_u8_i32(const uint8_t* d_in, int32_t* d_out, uint64_t n, void* stream);
+sml_status_t sml_narrow_i32_u8(const int32_t* d_in, uint8_t* d_out, uint64_t n, void* stream);
+
 /* ---- RDMA messages --------------------------------------
  * The RDMA backend's LTU is a message of msg_numel (1024) elements
  * (rdma_worker_thread.cc:86-88): its payload is block m of the planes built

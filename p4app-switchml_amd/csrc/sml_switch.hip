@@ -265,6 +265,19 @@ static void launch_switch_m(bool exps, bool rcp, uint32_t P, dim3 g, hipStream_t
     else launch_switch_p<ALIGNED, BE, false, true>(P, g, st, a);
 }
 
+// ncclUint8 buckets (the CollNet plugin, switchml_plugin.cc:318-337 and
+// 370-378): widened to int32 for the INT32 all-reduce, narrowed back (mod 256).
+__global__ __launch_bounds__(kBlockThreads) void k_widen_u8(const uint8_t* in, int32_t* out, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; i < n; i += stride) out[i] = in[i];
+}
+
+__global__ __launch_bounds__(kBlockThreads) void k_narrow_u8(const int32_t* in, uint8_t* out, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlockThreads;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlockThreads + threadIdx.x; i < n; i += stride)
+        out[i] = (uint8_t)in[i];
+}
+
 }  // namespace sml
 
 using namespace sml;
@@ -343,6 +356,21 @@ sml_status_t sml_copy_words(const void* d_src, void* d_dst, uint64_t num_words, 
     k_words<<<grid_for_tiles(ntiles), kBlockThreads, 0, (hipStream_t)stream>>>(
         static_cast<const uint32_t*>(d_src), static_cast<uint32_t*>(d_dst), num_words,
         g_xcd_chunk.load(std::memory_order_relaxed), CopyOp{});
+    return launch_check();
+}
+
+// ncclUint8 buckets of the CollNet plugin (kernels above).
+sml_status_t sml_widen_u8_i32(const uint8_t* d_in, int32_t* d_out, uint64_t n, void* stream) {
+    if (n == 0) return SML_OK;
+    if (!d_in || !d_out || !aligned4(d_out)) return SML_ERR_INVALID_ARG;
+    k_widen_u8<<<grid_for_vec(n), kBlockThreads, 0, (hipStream_t)stream>>>(d_in, d_out, n);
+    return launch_check();
+}
+
+sml_status_t sml_narrow_i32_u8(const int32_t* d_in, uint8_t* d_out, uint64_t n, void* stream) {
+    if (n == 0) return SML_OK;
+    if (!d_in || !d_out || !aligned4(d_in)) return SML_ERR_INVALID_ARG;
+    k_narrow_u8<<<grid_for_vec(n), kBlockThreads, 0, (hipStream_t)stream>>>(d_in, d_out, n);
     return launch_check();
 }
 

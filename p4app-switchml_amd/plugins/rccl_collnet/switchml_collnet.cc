@@ -13,8 +13,10 @@
 //    for data; the switch (here: the Context's backend) does the reduction;
 //  * a FAILED job makes test() return ncclInternalError (the reference kept
 //    reporting "not done");
-//  * ncclUint8 is widened to int32 on the host as in :318-337, for host
-//    buffers; device uint8 buffers are rejected (ncclInvalidArgument).
+//  * ncclUint8 is widened to int32 as in :318-337 and narrowed back in
+//    test() as in :370-378 — on the host for host buffers, by two small HIP
+//    kernels into / out of a device int32 scratch for device buffers (the
+//    reference, host-only, had no such case).
 //  * backend "xgmi" (the in-node switch, xgmi_switch.h) reduces across the
 //    ranks of one node; the loopback ("dummy") backend multiplies a rank's
 //    own buffer by num_workers instead, so with it init() refuses
@@ -49,8 +51,11 @@
 #include <mutex>
 #include <string>
 
+#include <hip/hip_runtime_api.h>
+
 #include "collnet_abi.h"
 #include "context.h"
+#include "switchml_hip.h"
 #include "loopback_backend.h"
 #include "job_order.h"
 #include "socket_net.h"
@@ -93,7 +98,8 @@ struct Request {
     void* send;
     void* recv;                           // what the job reduces into
     void* user_recv;                      // caller's recv buffer (uint8 case)
-    int32_t* widened;                     // temp int32 buffer (uint8 case)
+    int32_t* widened;                     // temp int32 buffer (uint8 case, host buffers)
+    int32_t* dwidened;                    // temp int32 buffer (uint8 case, device buffers)
     sml_collnet::CallKey key;
     bool failed;
 };
@@ -304,13 +310,31 @@ void pump() {
     }
 }
 
+// The plugin's own stream for the uint8 widen / narrow kernels (created on
+// the calling thread's device at first use; RCCL's proxy thread has it set).
+hipStream_t aux_stream() {
+    static hipStream_t st = nullptr;
+    if (!st && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        st = nullptr;
+    }
+    return st;
+}
+
+void release_widened(Request* r) {
+    delete[] r->widened;
+    r->widened = nullptr;
+    if (r->dwidened) (void)hipFree(r->dwidened);
+    r->dwidened = nullptr;
+}
+
 ncclResult_t sml_iallreduce(void* coll_comm, void* send, void* recv, int count, ncclDataType_t dtype,
                             ncclRedOp_t op, void* send_mh, void*, void** request) {
     if (op != ncclSum || type_size(dtype) == 0 || count < 0) return ncclInvalidArgument;
     switchml::Context& ctx = switchml::Context::GetInstance();
     if (ctx.GetContextState() != switchml::Context::RUNNING) return ncclInvalidUsage;
     auto* c = static_cast<CollComm*>(coll_comm);
-    auto* r = new Request{nullptr, dtype, count, send, recv, recv, nullptr, {}, false};
+    auto* r = new Request{nullptr, dtype, count, send, recv, recv, nullptr, nullptr, {}, false};
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_order && g_order->Poisoned()) {
         delete r;
@@ -318,14 +342,30 @@ ncclResult_t sml_iallreduce(void* coll_comm, void* send, void* recv, int count, 
     }
     try {
         if (dtype == ncclUint8) {
-            if (switchml::IsDevicePointer(send) || switchml::IsDevicePointer(recv)) {
+            const bool ds = switchml::IsDevicePointer(send), dr = switchml::IsDevicePointer(recv);
+            if (ds != dr) {                   // one device and one host buffer: not a CollNet call
                 delete r;
                 return ncclInvalidArgument;
             }
-            r->widened = new int32_t[count > 0 ? count : 1];
-            const uint8_t* s8 = static_cast<const uint8_t*>(send);
-            for (int i = 0; i < count; i++) r->widened[i] = s8[i];
-            r->send = r->recv = r->widened;
+            if (ds) {
+                // device buffers: widen on the GPU into a device int32 scratch;
+                // the job reads it only after this stream has finished
+                if (hipMalloc(&r->dwidened, 4ull * (count > 0 ? count : 1)) != hipSuccess) {
+                    (void)hipGetLastError();
+                    r->dwidened = nullptr;
+                    throw std::runtime_error("hipMalloc of the uint8 widening buffer failed");
+                }
+                hipStream_t st = aux_stream();
+                if (sml_widen_u8_i32(static_cast<const uint8_t*>(send), r->dwidened, (uint64_t)count, st) != SML_OK ||
+                    hipStreamSynchronize(st) != hipSuccess)
+                    throw std::runtime_error("uint8 widening kernel failed");
+                r->send = r->recv = r->dwidened;
+            } else {
+                r->widened = new int32_t[count > 0 ? count : 1];
+                const uint8_t* s8 = static_cast<const uint8_t*>(send);
+                for (int i = 0; i < count; i++) r->widened[i] = s8[i];
+                r->send = r->recv = r->widened;
+            }
         }
         const uint32_t buf = send_mh ? static_cast<MemHandle*>(send_mh)->id : 0xffffffffu;
         r->key = {c ? c->ordinal : 0u, buf, c ? c->calls[buf]++ : 0u, (int64_t)count, (int32_t)dtype, 0};
@@ -339,7 +379,7 @@ ncclResult_t sml_iallreduce(void* coll_comm, void* send, void* recv, int count, 
         }
     } catch (const std::exception& e) {
         if (g_logger) g_logger(NCCL_LOG_WARN, 0, __FILE__, __LINE__, "SwitchML CollNet: %s", e.what());
-        delete[] r->widened;
+        release_widened(r);
         delete r;
         return ncclInternalError;
     }
@@ -374,7 +414,7 @@ ncclResult_t sml_test(void* request, int* done, int* size) {
                     break;
                 }
         }
-        delete[] r->widened;
+        release_widened(r);
         delete r;
         return ncclInternalError;
     }
@@ -383,9 +423,21 @@ ncclResult_t sml_test(void* request, int* done, int* size) {
         return ncclSuccess;
     }
     if (r->dtype == ncclUint8) {   // switchml_plugin.cc:370-378
-        uint8_t* out = static_cast<uint8_t*>(r->user_recv);
-        for (int i = 0; i < r->count; i++) out[i] = (uint8_t)r->widened[i];
-        delete[] r->widened;
+        if (r->dwidened) {
+            hipStream_t st = aux_stream();
+            const bool ok = sml_narrow_i32_u8(r->dwidened, static_cast<uint8_t*>(r->user_recv), (uint64_t)r->count,
+                                              st) == SML_OK &&
+                            hipStreamSynchronize(st) == hipSuccess;
+            release_widened(r);
+            if (!ok) {
+                delete r;
+                return ncclInternalError;
+            }
+        } else {
+            uint8_t* out = static_cast<uint8_t*>(r->user_recv);
+            for (int i = 0; i < r->count; i++) out[i] = (uint8_t)r->widened[i];
+            release_widened(r);
+        }
     }
     *done = 1;
     g_calls.test_done++;

@@ -116,8 +116,13 @@ out["host_ok"] = bool(np.array_equal(h.view(np.uint32), ref.view(np.uint32)))
 i = np.arange(-5000, 5000, dtype=np.int32)
 run(ctypes.c_void_p(i.ctypes.data), ctypes.c_void_p(i.ctypes.data), i.size, 2)
 out["int_ok"] = bool((i == np.arange(-5000, 5000, dtype=np.int32) * 2).all())
-ud = torch.zeros(16, dtype=torch.uint8, device="cuda")
-out["dev_u8"] = run(ctypes.c_void_p(ud.data_ptr()), ctypes.c_void_p(ud.data_ptr()), 16, 1)
+uv = (np.arange(1000) * 37 % 256).astype(np.uint8)
+ud = torch.from_numpy(uv).cuda(); uo = torch.full((1000,), 7, dtype=torch.uint8, device="cuda")
+out["dev_u8"] = run(ctypes.c_void_p(ud.data_ptr()), ctypes.c_void_p(uo.data_ptr()), 1000, 1)
+out["dev_u8_ok"] = bool(np.array_equal(uo.cpu().numpy(), (uv.astype(np.int64) * 2 % 256).astype(np.uint8)))
+out["dev_u8_send_untouched"] = bool(np.array_equal(ud.cpu().numpy(), uv))
+uh = np.zeros(16, np.uint8)
+out["mixed_u8"] = run(ctypes.c_void_p(ud.data_ptr()), ctypes.c_void_p(uh.ctypes.data), 16, 1)
 '''
     ini = ("[general]\nnum_workers = 2\nnum_worker_threads = 4\npacket_numel = 256\n"
            "max_outstanding_packets = 256\n[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = bulk\n")
@@ -126,7 +131,10 @@ out["dev_u8"] = run(ctypes.c_void_p(ud.data_ptr()), ctypes.c_void_p(ud.data_ptr(
     assert out["dev_size"] == 4 * 100_003 and out["dev_ok"]
     assert out["host_size"] == 4 * 100_003 and out["host_ok"]
     assert out["int_ok"]
-    assert out["dev_u8"] == 4   # device uint8: ncclInvalidArgument
+    # device uint8 (RCCL hands device buffers, NCCL_PTR_CUDA): widened on the
+    # GPU, all-reduced as INT32 (loopback: x2), narrowed mod 256 — :318-337, 370-378
+    assert out["dev_u8"] == 1000 and out["dev_u8_ok"] and out["dev_u8_send_untouched"]
+    assert out["mixed_u8"] == 4   # one device and one host buffer: ncclInvalidArgument
 
 
 def test_loopback_collnet_needs_opt_in():
