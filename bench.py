@@ -1070,8 +1070,8 @@ def extra_measurements(sw, torch, x, P, stream, reps=20):
     out = torch.empty_like(x)
     res = {}
 
-    def timeit(fn):
-        return time_launches(torch, fn, stream, reps)
+    def timeit(fn, warm=3):
+        return time_launches(torch, fn, stream, reps, warm)
 
     t = timeit(lambda: sw.dequantize(payload, exps, N, P, 1, out=out, stream=stream))
     res["dequantize_GBps"] = round((8 * N + B) / t / 1e9, 1)
@@ -1137,10 +1137,13 @@ def extra_measurements(sw, torch, x, P, stream, reps=20):
         r.reset(stream)
         sw.dequantize_frames(fsets[k[0] % 4], fbytes // sw.frame_bytes(P), r, num_workers=1, stream=stream)
         k[0] += 1
-    t = timeit(tx_cycle)
+    # warm calls cover every set twice: a set's first use pays first-touch
+    # costs (~130 us once), which 3 warm calls over 4 sets left in the timed
+    # loop (+6 %, tools/debug/rx_bench_method_probe.py, profiles/r05)
+    t = timeit(tx_cycle, warm=8)
     res["frames_device_4sets_GBps"] = round((4 * N + fbytes) / t / 1e9, 1)
     with torch.cuda.stream(stream):
-        t = timeit(rx_cycle)
+        t = timeit(rx_cycle, warm=8)
     res["frames_rx_device_4sets_GBps"] = round((4 * N + fbytes) / t / 1e9, 1)
     del fsets, rxs
     # INT32 job slices over the same wire format: B frames (no extra batch),
