@@ -389,9 +389,13 @@ sml_status_t sml_pack_frames_int32(const int32_t* d_in, uint64_t numel, uint32_t
  * sml_dequantize_frames (this job, a pkt_id < B not received before, the
  * first copy wins), and PostprocessSingle's INT32 branch (ppp.cc:262-298):
  * ntohl of the accepted frame's words into d_out[pkt_id*P ..
- * pkt_id*P + min(P, numel - pkt_id*P)).  d_state: uint64[B], zeroed per
- * slice (sml_rx_reset), persists across calls; d_counts as for
- * sml_dequantize_frames.  Two launches on `stream`. */
+ * pkt_id*P + min(P, numel - pkt_id*P)).  d_state: uint64[B + 3] (the rx
+ * bitmap, the slice's call sequence, the running call's conflict count, the
+ * slice's count of copies that claimed ahead of an earlier copy),
+ * zeroed per slice (sml_rx_reset), persists across calls; d_counts as for
+ * sml_dequantize_frames.  One pass in stream order over the frames (an INT32
+ * frame needs no other frame) plus a one-workgroup fix-up, on `stream`;
+ * num_frames < 2^31 per call. */
 sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, uint64_t frame_stride,
                                      uint64_t numel, uint32_t packet_numel, uint64_t job_id,
                                      uint64_t* d_state, int32_t* d_out, uint64_t* d_counts, void* stream);

@@ -301,19 +301,14 @@ __device__ __forceinline__ bool rx_winner(unsigned long long sw, uint64_t nframe
     return hi != 0u && hi != kRxDone && f < nframes;
 }
 
-// I32: an INT32 job slice — no extra batch (a.b = 0: pkt_id k carries block
-// k), no exponents, and PostprocessSingle's INT32 branch (ppp.cc:262-298):
-// ntohl of the words into out, no scale.
-template <int P, bool NT = false, bool I32 = false>
+template <int P, bool NT = false>
 __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
     __shared__ float lut[256];
     // power-of-two W: the table holds exact reciprocals and dequantize multiplies
     // (bit-equal to the IEEE division, rcp_scale_pow2); otherwise scales
     const bool pow2 = (a.W & (a.W - 1)) == 0;
-    if constexpr (!I32) {
-        if (pow2) build_rcp_lut(lut, a.W);
-        else build_lut(lut, a.W);
-    }
+    if (pow2) build_rcp_lut(lut, a.W);
+    else build_lut(lut, a.W);
     constexpr int kRxU = rx_slices(P);
     constexpr int kRxTileElems = kRxU * kWave * 4;
     constexpr int kChunksPerFrame = P / 4;     // 16-B chunks per payload
@@ -345,7 +340,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             for (int u = 0; u < kRxU; u++) {
                 const uint64_t k = t * kBlocksPerTile + (u * kWave) / kChunksPerFrame;
                 ok[u] = rx_winner(sw[u], a.nframes, f[u]) && k < a.nblocks;
-                if constexpr (!I32) s[u] = lut[(uint32_t)se[u] & 0xffu];
+                s[u] = lut[(uint32_t)se[u] & 0xffu];
             }
         } else {
 #pragma unroll
@@ -359,7 +354,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             for (int u = 0; u < kRxU; u++) {
                 const uint64_t k = t * kBlocksPerTile + (u * kWave + lane) / kChunksPerFrame;
                 ok[u] = rx_winner(sw[u], a.nframes, f[u]) && k < a.nblocks;
-                if constexpr (!I32) s[u] = lut[(uint32_t)se[u] & 0xffu];
+                s[u] = lut[(uint32_t)se[u] & 0xffu];
             }
         }
         // Non-temporal payload loads (25 % faster than default-policy loads for
@@ -381,9 +376,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
         f4 o[kRxU];
 #pragma unroll
         for (int u = 0; u < kRxU; u++) {
-            if constexpr (I32)
-                o[u] = __builtin_bit_cast(f4, mku4(bswap(w[u].x), bswap(w[u].y), bswap(w[u].z), bswap(w[u].w)));
-            else if (pow2)
+            if (pow2)
                 o[u] = mkf4((float)(int32_t)bswap(w[u].x) * s[u], (float)(int32_t)bswap(w[u].y) * s[u],
                             (float)(int32_t)bswap(w[u].z) * s[u], (float)(int32_t)bswap(w[u].w) * s[u]);
             else
@@ -415,11 +408,191 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
             const uint32_t hw = (uint32_t)(sw[u] >> 32), he = (uint32_t)(se[u] >> 32);
             if (hw != 0u && hw != kRxDone)
                 a.state[k + a.b] = ((unsigned long long)kRxDone << 32) | (sw[u] & 0xffull);
-            if constexpr (!I32)
-                if (he != 0u) a.exps[k] = (int8_t)(se[u] & 0xffull);
+            if (he != 0u) a.exps[k] = (int8_t)(se[u] & 0xffull);
             if (k < a.b && he != 0u && he != kRxDone)
                 a.state[k] = ((unsigned long long)kRxDone << 32) | (se[u] & 0xffull);
         }
+    }
+}
+
+// --------------------------------------- INT32 job slices, receive side
+//
+// An INT32 frame is self-contained — pkt_id k carries block k's words and
+// there is no exponent to take from another frame (NeedsExtraBatch false,
+// ppp.cc:65-67; PostprocessSingle's INT32 branch, ppp.cc:262-298) — so one
+// pass in stream order decides and writes each frame: no claim pass over the
+// headers, no second walk in block order.  State: uint64[B + 3] per slice:
+// [0, B) the rx bitmap, [B] the call sequence c of this slice, [B + 1] the
+// conflict count of the running call, [B + 2] the conflicts resolved in the
+// slice so far (a statistic: copies that arrived ahead of an earlier one).  A frame's tag is
+//   (0xFFFFFFFF - c) << 32 | (0x7FFFFFFF - f) << 1      (bit 0: dirty),
+// larger for an earlier call and, within a call, for an earlier frame f, so
+// a 64-bit atomicMax on state[pkt_id] keeps the first copy of the stream,
+// and a pkt_id accepted by an earlier call (higher tag) discards every later
+// copy — the reference's "seen before" test (dpdk_worker_thread.cc:316-342)
+// without a retirement pass.  The atomic's old value decides:
+//   0                  first claim of the pkt_id: write, accepted;
+//   above the tag      an earlier copy (or call) holds it: discarded;
+//   below the tag      this frame is earlier than the copy that claimed first
+//                      and already wrote: write too, mark the pkt_id dirty,
+//                      count a conflict (the counts stay exact: the displaced
+//                      copy was counted accepted, this one is counted as the
+//                      discard).
+// Which of two racing writes lands last is not ordered, so the fix-up
+// (k_rx_int32_fixup, same stream) rewrites every dirty pkt_id from its final
+// winner — the highest tag, the first copy — and then advances c.  Copies
+// of one pkt_id are normally identical (retransmissions), but the rule holds
+// for any payloads.
+constexpr uint32_t kRxI32MaxFrames = 0x7FFFFFFFu;
+
+__host__ __device__ constexpr int rx_int32_slices(int P) { return P / 256 > 4 ? P / 256 : 4; }
+
+__device__ __forceinline__ unsigned long long rx_int32_tag(uint32_t call, uint64_t f) {
+    return ((unsigned long long)(0xFFFFFFFFu - call) << 32) | ((unsigned long long)(kRxI32MaxFrames - (uint32_t)f) << 1);
+}
+
+// A wave takes F = U * 256 / P consecutive frames per tile (4 frames at
+// P = 256): every lane loads one of the tile's F headers (lane l < F's is
+// the one used) and its 16-byte payload chunks; lane l < F then makes frame
+// l's claim, and the decision and the pkt_id are shuffled to the lanes
+// holding that frame's chunks.  Software-pipelined: the next tile's header
+// and payload loads are issued before this tile's claim, so a wave waits on
+// one round trip per tile (the claim's, with the next loads under it) rather
+// than two in series (loads, then the claim).
+template <int P>
+struct RxI32Tile {
+    static constexpr int kU = rx_int32_slices(P);
+    u3a hv;
+    u4a w[kU];
+};
+
+template <int P>
+__device__ __forceinline__ void rx_int32_load(const RxArgs& a, uint64_t t, int lane, RxI32Tile<P>& r) {
+    constexpr int kU = RxI32Tile<P>::kU;
+    constexpr int kChunksPerFrame = P / 4;
+    constexpr int kF = kU * kWave / kChunksPerFrame;
+    const uint64_t f0 = t * kF;
+    // header first (the claim needs it first); indices clamped into the call
+    // so every load is unconditional and in flight at once
+    uint64_t fh = f0 + (uint64_t)(lane % kF);
+    fh = fh < a.nframes ? fh : a.nframes - 1;
+    r.hv = *reinterpret_cast<const u3a*>(a.frames + fh * a.stride + 40);
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+        const int c = u * kWave + lane;
+        uint64_t f = f0 + c / kChunksPerFrame;
+        f = f < a.nframes ? f : a.nframes - 1;
+        r.w[u] = __builtin_nontemporal_load(reinterpret_cast<const u4a*>(
+            a.frames + f * a.stride + 52 + 16ull * (c % kChunksPerFrame)));
+    }
+}
+
+template <int P, bool NT>
+__global__ __launch_bounds__(kBlockThreads) void k_rx_int32(RxArgs a) {
+    constexpr int kU = RxI32Tile<P>::kU;
+    constexpr int kChunksPerFrame = P / 4;
+    constexpr int kF = kU * kWave / kChunksPerFrame;          // frames per tile
+    static_assert(kF >= 1 && kF <= kWave, "frames per tile");
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint64_t ntiles = (a.nframes + kF - 1) / kF;
+    const uint32_t call = (uint32_t)a.state[a.nblocks];
+    unsigned long long* const conflicts = a.state + a.nblocks + 1;
+    uint32_t disc = 0;
+    uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
+    RxI32Tile<P> cur, nxt;
+    if (t < ntiles) rx_int32_load<P>(a, t, lane, cur);
+    for (; t < ntiles; t += nwaves) {
+        const uint64_t tn = t + nwaves;
+        if (tn < ntiles) rx_int32_load<P>(a, tn, lane, nxt);
+        const uint64_t f0 = t * kF;
+        // lane l < kF: the claim of frame f0 + l
+        bool write = false;
+        uint32_t pid = cur.hv.y;
+        if (lane < kF && f0 + lane < a.nframes) {
+            const uint64_t f = f0 + lane;
+            const bool ok = (cur.hv.x >> 24) == a.job && (uint64_t)pid < a.nblocks;
+            bool keep = false;
+            if (ok) {
+                const unsigned long long tag = rx_int32_tag(call, f);
+                const unsigned long long old = atomicMax(a.state + pid, tag);
+                if (old == 0ull) {
+                    write = true;
+                    keep = true;
+                } else if ((old & ~1ull) < tag) {
+                    write = true;
+                    atomicOr(a.state + pid, 1ull);
+                    atomicAdd(conflicts, 1ull);
+                }
+            }
+            if (!keep) disc++;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int c = u * kWave + lane;
+            const int src = c / kChunksPerFrame;
+            const bool wr = __shfl(write ? 1 : 0, src) != 0;
+            const uint64_t k = (uint32_t)__shfl((int)pid, src);
+            if (!wr) continue;
+            const uint64_t off = k * P + 4ull * (c % kChunksPerFrame);
+            if (off >= a.numel) continue;
+            const u4a& w = cur.w[u];
+            const f4 o = __builtin_bit_cast(f4, mku4(bswap(w.x), bswap(w.y), bswap(w.z), bswap(w.w)));
+            float* p = a.out + off;
+            if (a.numel - off >= 4 && ((uintptr_t)p & 15u) == 0) {
+                // a wave's F frames land anywhere in the output (their pkt_ids),
+                // so not SML_NT_STORE16: its buffer resource spans +-1 GiB
+                // around the first lane's address
+                if constexpr (NT) SML_NT_STORE16_UNALIGNED(o, reinterpret_cast<f4*>(p));
+                else *reinterpret_cast<f4*>(p) = o;
+            }
+            else store4_guarded(p, o, 0, a.numel - off);
+        }
+        cur = nxt;
+    }
+    if (!a.counts) return;
+    // accepted = frames - discarded: block 0 adds the frame count once, and
+    // only workgroups that saw a discard touch the discard counter
+    __shared__ uint32_t bdisc;
+    if (threadIdx.x == 0) bdisc = 0;
+    __syncthreads();
+    if (disc) atomicAdd(&bdisc, disc);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long acc = blockIdx.x == 0 ? (unsigned long long)a.nframes : 0ull;
+        acc -= bdisc;                                                // mod 2^64
+        if (acc) atomicAdd(a.counts + 0, acc);
+        if (bdisc) atomicAdd(a.counts + 1, (unsigned long long)bdisc);
+    }
+}
+
+// One workgroup, after k_rx_int32 on the same stream: with conflicts in this
+// call, every dirty pkt_id is rewritten from the frame its tag names (the
+// first copy) and cleaned; then the conflict count is cleared and the call
+// sequence advanced (the slice's conflict total accumulates).  Without
+// conflicts (no copies claimed out of order) it only advances the sequence.
+__global__ __launch_bounds__(kBlockThreads) void k_rx_int32_fixup(RxArgs a, uint32_t P) {
+    const unsigned long long n = a.state[a.nblocks + 1];
+    const unsigned long long call = a.state[a.nblocks];
+    if (n) {
+        for (uint64_t k = threadIdx.x; k < a.nblocks; k += kBlockThreads) {
+            const unsigned long long s = a.state[k];
+            if (!(s & 1ull)) continue;
+            const uint64_t f = kRxI32MaxFrames - (uint32_t)((uint32_t)s >> 1);
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + f * a.stride + 52);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(a.out) + k * P;
+            const uint64_t valid = a.numel - k * P < P ? a.numel - k * P : P;
+            for (uint64_t i = 0; i < valid; i++) dst[i] = bswap(src[i]);
+            a.state[k] = s & ~1ull;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (n) {
+            a.state[a.nblocks + 2] += n;
+            a.state[a.nblocks + 1] = 0ull;
+        }
+        a.state[a.nblocks] = call + 1;
     }
 }
 
@@ -440,23 +613,33 @@ static void launch_frames_p(uint32_t P, bool nts, dim3 grid, hipStream_t st, con
 #undef SML_FR
 }
 
-template <bool NT, bool I32>
+template <bool NT>
 static void launch_rx_apply_nt(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
     switch (P) {
-        case 64:   k_rx_apply<64, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 128:  k_rx_apply<128, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 256:  k_rx_apply<256, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
-        case 512:  k_rx_apply<512, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
-        default:   k_rx_apply<1024, NT, I32><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 64:   k_rx_apply<64, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_rx_apply<128, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_rx_apply<256, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_rx_apply<512, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_rx_apply<1024, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
     }
 }
 
 // The output of a slice from the non-temporal threshold on takes
 // non-temporal stores, as K4's does (sml_set_payload_nt_threshold).
-template <bool I32 = false>
 static void launch_rx_apply(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
-    if (4 * a.numel >= g_nt_threshold.load(std::memory_order_relaxed)) launch_rx_apply_nt<true, I32>(P, grid, st, a);
-    else launch_rx_apply_nt<false, I32>(P, grid, st, a);
+    if (4 * a.numel >= g_nt_threshold.load(std::memory_order_relaxed)) launch_rx_apply_nt<true>(P, grid, st, a);
+    else launch_rx_apply_nt<false>(P, grid, st, a);
+}
+
+template <bool NT>
+static void launch_rx_int32_nt(uint32_t P, dim3 grid, hipStream_t st, const RxArgs& a) {
+    switch (P) {
+        case 64:   k_rx_int32<64, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 128:  k_rx_int32<128, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 256:  k_rx_int32<256, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        case 512:  k_rx_int32<512, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+        default:   k_rx_int32<1024, NT><<<grid, kBlockThreads, 0, st>>>(a); break;
+    }
 }
 
 }  // namespace sml
@@ -612,14 +795,12 @@ sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, ui
                                      uint64_t* d_counts, void* stream) {
     if (!valid_packet(P)) return SML_ERR_UNSUPPORTED;
     if (num_frames == 0) return SML_OK;
-    if (num_frames >= 0xFFFFFFFEull) return SML_ERR_UNSUPPORTED;
+    if (num_frames > kRxI32MaxFrames) return SML_ERR_UNSUPPORTED;
     if (!frames || !d_state || (numel && !d_out)) return SML_ERR_INVALID_ARG;
     if (!aligned4(frames) || !aligned4(d_out) || stride % 4 || stride < sml_frame_bytes(P)) return SML_ERR_ALIGNMENT;
     if (((uintptr_t)d_state & 7u) || (d_counts && ((uintptr_t)d_counts & 7u))) return SML_ERR_ALIGNMENT;
     RxArgs a;
-    const uint32_t U = (uint32_t)rx_slices((int)P);
-    a.xcd = U < 4 ? g_xcd_chunk.load(std::memory_order_relaxed) * (4 / U)
-                  : g_xcd_chunk.load(std::memory_order_relaxed);
+    a.xcd = g_xcd_chunk.load(std::memory_order_relaxed);
     a.frames = static_cast<const uint8_t*>(frames);
     a.nframes = num_frames;
     a.stride = stride;
@@ -633,10 +814,11 @@ sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, ui
     a.W = 1;
     a.job = (uint8_t)job_id;
     hipStream_t st = (hipStream_t)stream;
-    k_rx_claim<<<grid_for_vec(num_frames), kBlockThreads, 0, st>>>(a);
-    const uint64_t tile = (uint64_t)U * kWave * 4;
-    const uint64_t ntiles = (a.nblocks * P + tile - 1) / tile;
-    if (ntiles) launch_rx_apply<true>(P, dim3(grid_for_tiles(ntiles)), st, a);
+    const uint64_t frames_per_tile = (uint64_t)rx_int32_slices((int)P) * kWave * 4 / P;
+    const dim3 grid(grid_for_tiles((num_frames + frames_per_tile - 1) / frames_per_tile));
+    if (4 * numel >= g_nt_threshold.load(std::memory_order_relaxed)) launch_rx_int32_nt<true>(P, grid, st, a);
+    else launch_rx_int32_nt<false>(P, grid, st, a);
+    k_rx_int32_fixup<<<1, kBlockThreads, 0, st>>>(a, P);
     return launch_check();
 }
 

@@ -652,14 +652,22 @@ def pack_frames_int32(x, params: FrameParams, packet_numel: int = 256, frames=No
 
 class RxSliceInt32:
     """Receive-side state of one INT32 job slice for unpack_frames_int32: the
-    rx bitmap over its B pkt_ids, {accepted, discarded} counters, the output."""
+    rx bitmap over its B pkt_ids plus the slice's call sequence, the running
+    call's conflict count and the slice's conflict total (uint64[B + 3]),
+    {accepted, discarded} counters, the output."""
 
     def __init__(self, numel: int, packet_numel: int = 256, device="cuda", out=None):
         torch = _torch()
         self.numel, self.packet_numel = numel, packet_numel
-        self.state = torch.zeros(max(1, num_blocks(numel, packet_numel)), dtype=torch.int64, device=device)
+        self.state = torch.zeros(num_blocks(numel, packet_numel) + 3, dtype=torch.int64, device=device)
         self.counts = torch.zeros(2, dtype=torch.int64, device=device)
         self.out = out if out is not None else torch.zeros(numel, dtype=torch.int32, device=device)
+
+    @property
+    def conflicts(self) -> int:
+        """Copies of a pkt_id that claimed it ahead of an earlier copy and were
+        resolved by the fix-up, over the slice so far (reads the device)."""
+        return int(self.state[-1].item())
 
     def reset(self, stream=None):
         """rte_bitmap_reset for a new job slice (sml_rx_reset)."""

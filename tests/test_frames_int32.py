@@ -209,3 +209,237 @@ def test_int32_frames_round_trip_16M(cuda):
     torch.cuda.synchronize()
     assert torch.equal(rx.out, x)
     assert rx.counts.cpu().tolist() == [B, 0]
+
+
+def altered_copies_stream(frames, B, fb, seed, pairs, max_gap=4096):
+    """The slice's frames in order, plus for `pairs` pkt_ids a copy whose
+    payload differs (words XOR 0x5A5A5A5A), inserted a random 1..max_gap
+    frames before or after the original: the first copy in stream order must
+    win whichever copy the GPU claims first."""
+    rng = np.random.default_rng(seed)
+    fr = [f.copy() for f in frames.reshape(B, fb)]
+    pos = {p: float(p) for p in range(B)}
+    extra = []
+    for p in rng.choice(B, min(pairs, B), replace=False):
+        alt = fr[p].copy()
+        alt[52:] ^= 0x5A
+        gap = int(rng.integers(1, max_gap + 1)) * (1 if rng.random() < 0.5 else -1)
+        extra.append((pos[p] + gap + 0.5 * np.sign(gap), alt))
+    items = [(pos[p], fr[p]) for p in range(B)] + extra
+    items.sort(key=lambda it: it[0])
+    return np.concatenate([f for _, f in items])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,n,pairs", [(64, 4 * 1024 * 1024, 20_000), (256, 8 * 1024 * 1024 + 3, 8_000),
+                                       (1024, 2 * 1024 * 1024, 1_000)])
+def test_int32_rx_first_copy_wins_over_racing_copies(cuda, P, n, pairs):
+    """Copies of a pkt_id with DIFFERENT payloads, one before or after the
+    original at random distances, in one rx call: the one-pass kernel claims
+    in whatever order the waves run; the output must be the first copy's
+    words (the reference loop's rule) and the counts exact."""
+    import torch
+    import switchml_amd as sw
+    fp = params(job_id=5)
+    x = int32_data(P + 17, n)
+    fb = 52 + 4 * P
+    B = O.num_blocks(n, P)
+    s = altered_copies_stream(O.build_frames_i32(x, fp, P=P), B, fb, seed=P, pairs=pairs)
+    nfr = s.size // fb
+    seen = np.zeros(B, dtype=np.uint8)
+    ref = np.zeros(n, dtype=np.int32)
+    acc, dis = python_rx(s, fb, n, P, 5, seen, ref)
+    rx = sw.RxSliceInt32(n, P, device=cuda)
+    rx.reset()
+    sw.unpack_frames_int32(torch.from_numpy(s).to(cuda), nfr, rx, job_id=5)
+    torch.cuda.synchronize()
+    got = rx.out.cpu().numpy()
+    bad = np.flatnonzero(got != ref)
+    assert bad.size == 0, (bad.size, bad[:8].tolist())
+    assert rx.counts.cpu().tolist() == [acc, dis] and acc == B and dis == pairs
+    st = rx.state.cpu().numpy()
+    assert st[B] == 1 and st[B + 1] == 0                      # call sequence advanced, conflicts cleared
+    assert not (st[:B] & 1).any()                              # no dirty pkt_id left
+    print(f"P={P}: {rx.conflicts} of {pairs} copies claimed ahead of an earlier copy")
+
+
+def lead_stream(x, fp, P, K, pairs_iters, other_job):
+    """A stream shaped for ONE workgroup of 4 waves (grid limit 1: wave w
+    takes tiles w, w + 4, ... of F = 1024 / P frames, P >= 256 here): for K
+    iterations wave 0's tiles hold distinct valid frames (claim + store) and
+    waves 1-3's tiles another job's frames (no claim), so wave 1 runs ahead;
+    then for `pairs_iters` iterations wave 0's tile holds the first copies of
+    F pkt_ids and wave 1's tile later, altered copies of the same pkt_ids —
+    which wave 1 reaches first.  Returns the stream bytes."""
+    F = 1024 // P
+    fb = 52 + 4 * P
+    B = O.num_blocks(x.size, P)
+    fr = O.build_frames_i32(x, fp, P=P).reshape(B, fb)
+    other = fr[0].copy()
+    other[43] = other_job
+    tiles = []
+    pid = 0
+    for _ in range(K):
+        tiles.append([fr[pid + j] for j in range(F)])
+        pid += F
+        tiles += [[other] * F] * 3
+    for _ in range(pairs_iters):
+        first = [fr[pid + j] for j in range(F)]
+        alt = [f.copy() for f in first]
+        for a in alt:
+            a[52:] ^= 0x5A
+        tiles += [first, alt, [other] * F, [other] * F]
+        pid += F
+    assert pid <= B
+    return np.concatenate([f for t in tiles for f in t])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [256, 1024])
+def test_int32_rx_later_copy_claiming_first_is_fixed_up(cuda, P):
+    """Deterministic cover of the fix-up: later copies that claim their
+    pkt_ids BEFORE the earlier copies (their wave runs ahead), with different
+    payloads.  The output must be the first copies' words, the counts exact,
+    and the slice's conflict total shows the later copies did claim first."""
+    import torch
+    import switchml_amd as sw
+    K, pairs_iters = 3000, 64
+    F = 1024 // P
+    n = (K + pairs_iters) * F * P
+    fp = params(job_id=5)
+    x = int32_data(P, n)
+    fb = 52 + 4 * P
+    B = O.num_blocks(n, P)
+    s = lead_stream(x, fp, P, K, pairs_iters, other_job=6)
+    nfr = s.size // fb
+    seen = np.zeros(B, dtype=np.uint8)
+    ref = np.zeros(n, dtype=np.int32)
+    acc, dis = python_rx(s, fb, n, P, 5, seen, ref)
+    assert np.array_equal(ref, x)                               # every first copy is the original
+    old_lim, old_xcd = sw.set_grid_limit(1), sw.set_xcd_chunk(0)
+    try:
+        rx = sw.RxSliceInt32(n, P, device=cuda)
+        rx.reset()
+        sw.unpack_frames_int32(torch.from_numpy(s).to(cuda), nfr, rx, job_id=5)
+        torch.cuda.synchronize()
+    finally:
+        sw.set_grid_limit(old_lim)
+        sw.set_xcd_chunk(old_xcd)
+    got = rx.out.cpu().numpy()
+    bad = np.flatnonzero(got != ref)
+    assert bad.size == 0, (bad.size, bad[:8].tolist())
+    assert rx.counts.cpu().tolist() == [acc, dis]
+    print(f"P={P}: {rx.conflicts} of {pairs_iters * F} later copies claimed first")
+    assert rx.conflicts > 0                                     # 256 of 256 / 64 of 64 on MI355X
+
+
+def claim_tag(call, f):
+    """k_rx_int32's claim tag (sml_frames.hip rx_int32_tag) as a signed int64."""
+    t = ((0xFFFFFFFF - call) << 32) | ((0x7FFFFFFF - f) << 1)
+    return int(np.array(t, dtype=np.uint64).view(np.int64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P", [64, 256, 1024])
+def test_int32_rx_fixup_rewrites_displaced_claims(cuda, P):
+    """The fix-up path, white box: before the call, some pkt_ids hold the
+    claim tag of a LATER frame of this call (as when a later copy wins the
+    race to the atomic) and their output words hold that copy's garbage.  The
+    real (earlier) frames must displace those claims, mark them dirty, and
+    the fix-up must leave the earlier frames' words, clean state words, the
+    conflict count in the slice total, and the call sequence advanced."""
+    import torch
+    import switchml_amd as sw
+    n = 40_000 + 7
+    fp = params(job_id=4)
+    x = int32_data(P + 3, n)
+    fb = 52 + 4 * P
+    B = O.num_blocks(n, P)
+    frames = O.build_frames_i32(x, fp, P=P)
+    rng = np.random.default_rng(P)
+    stolen = np.sort(rng.choice(B, max(1, B // 5), replace=False))
+    rx = sw.RxSliceInt32(n, P, device=cuda)
+    rx.reset()
+    st = rx.state.cpu().numpy()
+    for k in stolen:                                    # frame k's later twin (index B + k) claimed k first
+        st[k] = claim_tag(0, B + int(k))
+    rx.state.copy_(torch.from_numpy(st))
+    rx.out.fill_(-1)
+    sw.unpack_frames_int32(torch.from_numpy(frames).to(cuda), B, rx, job_id=4)
+    torch.cuda.synchronize()
+    assert np.array_equal(rx.out.cpu().numpy(), x)
+    st = rx.state.cpu().numpy()
+    assert not (st[:B] & 1).any()
+    assert [int(v) for v in st[B:]] == [1, 0, len(stolen)]
+    assert rx.conflicts == len(stolen)
+    # displaced claims count as the discards (their twins were counted accepted)
+    assert rx.counts.cpu().tolist() == [B - len(stolen), len(stolen)]
+    # a second call: every pkt_id is now held by call 0, so all copies are discarded
+    rx.out.fill_(0)
+    sw.unpack_frames_int32(torch.from_numpy(frames).to(cuda), B, rx, job_id=4)
+    torch.cuda.synchronize()
+    assert not rx.out.cpu().numpy().any()
+    assert rx.counts.cpu().tolist() == [B - len(stolen), B + len(stolen)]
+    assert int(rx.state[B].item()) == 2
+
+
+@pytest.mark.gpu
+def test_int32_rx_many_calls_keep_earlier_winners(cuda):
+    """Seven rx calls of one slice, each a shuffled part of a stream with
+    altered copies: a pkt_id accepted by an earlier call discards every later
+    copy (no retirement pass: the call sequence orders the tags)."""
+    import torch
+    import switchml_amd as sw
+    P, n = 256, 300_001
+    fp = params(job_id=9)
+    x = int32_data(99, n)
+    fb = 52 + 4 * P
+    B = O.num_blocks(n, P)
+    s = altered_copies_stream(O.build_frames_i32(x, fp, P=P), B, fb, seed=3, pairs=600, max_gap=B)
+    nfr = s.size // fb
+    cuts = np.sort(np.random.default_rng(4).choice(np.arange(1, nfr), 6, replace=False))
+    bounds = [0, *cuts.tolist(), nfr]
+    seen = np.zeros(B, dtype=np.uint8)
+    ref = np.zeros(n, dtype=np.int32)
+    acc = dis = 0
+    rx = sw.RxSliceInt32(n, P, device=cuda)
+    rx.reset()
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        part = s[lo * fb:hi * fb]
+        a, d = python_rx(part, fb, n, P, 9, seen, ref)
+        acc, dis = acc + a, dis + d
+        sw.unpack_frames_int32(torch.from_numpy(part.copy()).to(cuda), hi - lo, rx, job_id=9)
+    torch.cuda.synchronize()
+    assert np.array_equal(rx.out.cpu().numpy(), ref)
+    assert rx.counts.cpu().tolist() == [acc, dis]
+    assert int(rx.state[B].item()) == len(bounds) - 1
+
+
+@pytest.mark.gpu
+def test_int32_rx_scattered_pids_over_1GiB_output(cuda):
+    """An INT32 slice whose output passes 1 GiB, received with every wave's
+    frames interleaving pkt_ids from the two halves (half a GiB apart and
+    more): the non-temporal output stores must reach every address (a buffer
+    store spanning +-1 GiB around a wave's first lane would drop them)."""
+    import torch
+    import switchml_amd as sw
+    P = 256
+    n = (1 << 28) + 1000
+    fp = params(job_id=2)
+    g = torch.Generator(device=cuda)
+    g.manual_seed(5)
+    x = torch.randint(-2 ** 31, 2 ** 31 - 1, (n,), dtype=torch.int32, device=cuda, generator=g)
+    B = sw.num_blocks(n, P)
+    fb = sw.frame_bytes(P)
+    frames = sw.pack_frames_int32(x, fp, P).view(B, fb)
+    h = B // 2
+    order = torch.stack([torch.arange(h, device=cuda), torch.arange(h, 2 * h, device=cuda)], 1).flatten()
+    order = torch.cat([order, torch.arange(2 * h, B, device=cuda)])
+    shuffled = frames.index_select(0, order).flatten()
+    del frames
+    rx = sw.RxSliceInt32(n, P, device=cuda)
+    rx.reset()
+    sw.unpack_frames_int32(shuffled, B, rx, job_id=2)
+    torch.cuda.synchronize()
+    assert rx.counts.cpu().tolist() == [B, 0]
+    assert torch.equal(rx.out, x)
