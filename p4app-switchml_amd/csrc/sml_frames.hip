@@ -575,15 +575,25 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_int32_fixup(RxArgs a, uint
     const unsigned long long n = a.state[a.nblocks + 1];
     const unsigned long long call = a.state[a.nblocks];
     if (n) {
-        for (uint64_t k = threadIdx.x; k < a.nblocks; k += kBlockThreads) {
-            const unsigned long long s = a.state[k];
-            if (!(s & 1ull)) continue;
-            const uint64_t f = kRxI32MaxFrames - (uint32_t)((uint32_t)s >> 1);
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + f * a.stride + 52);
-            uint32_t* dst = reinterpret_cast<uint32_t*>(a.out) + k * P;
-            const uint64_t valid = a.numel - k * P < P ? a.numel - k * P : P;
-            for (uint64_t i = 0; i < valid; i++) dst[i] = bswap(src[i]);
-            a.state[k] = s & ~1ull;
+        // each wave scans 64 state words at a time; the dirty ones (a ballot)
+        // are rewritten one after another by the whole wave, lane-strided
+        const int lane = threadIdx.x & (kWave - 1);
+        for (uint64_t k0 = (uint64_t)wave_index() * kWave; k0 < a.nblocks; k0 += kBlockThreads) {
+            const uint64_t k = k0 + lane;
+            const unsigned long long s = k < a.nblocks ? a.state[k] : 0ull;
+            unsigned long long dirty = __ballot((s & 1ull) != 0);
+            while (dirty) {
+                const int j = __builtin_ctzll(dirty);
+                dirty &= dirty - 1;
+                const uint64_t kd = k0 + j;
+                const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)s, j);
+                const uint64_t f = kRxI32MaxFrames - (lo >> 1);
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + f * a.stride + 52);
+                uint32_t* dst = reinterpret_cast<uint32_t*>(a.out) + kd * P;
+                const uint64_t valid = a.numel - kd * P < P ? a.numel - kd * P : P;
+                for (uint64_t i = lane; i < valid; i += kWave) dst[i] = bswap(src[i]);
+            }
+            if (s & 1ull) a.state[k] = s & ~1ull;
         }
     }
     __syncthreads();
