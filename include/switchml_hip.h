@@ -401,7 +401,8 @@ sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, ui
                                      uint64_t* d_state, int32_t* d_out, uint64_t* d_counts, void* stream);
 
 /* rte_bitmap_reset for one slice (dpdk_worker_thread.cc, per job slice):
- * zero d_state (uint64[B + b]) before the slice's first sml_dequantize_frames
+ * zero d_state (uint64[B + b]; for INT32 slices uint64[B + 3]) before the
+ * slice's first sml_dequantize_frames / sml_unpack_frames_int32
  * call.  One async memset on `stream`. */
 sml_status_t sml_rx_reset(uint64_t* d_state, uint64_t num_words, void* stream);
 
