@@ -333,6 +333,11 @@ typedef struct sml_frame_params {
 /* Bytes of one frame: 52 + 4 * packet_numel. */
 uint64_t sml_frame_bytes(uint32_t packet_numel);
 
+/* Words of the per-slice rx state (d_state) a receive call needs: FLOAT32
+ * (sml_dequantize_frames) max(1, B + b) with b = min(batch_max, B); INT32
+ * (sml_unpack_frames_int32, int32 != 0) B + 3.  B = ceil(numel / P). */
+uint64_t sml_rx_state_words(uint64_t numel, uint32_t packet_numel, uint32_t batch_max, int int32);
+
 /* Fused K1 -> frames: quantize + pack one job slice straight into B + b
  * frames at `frame_stride` bytes apart (>= sml_frame_bytes, multiple of 4).
  * `frames` may be device memory or pinned, device-mapped host memory (the

@@ -660,6 +660,14 @@ extern "C" {
 
 uint64_t sml_frame_bytes(uint32_t packet_numel) { return 52ull + 4ull * packet_numel; }
 
+uint64_t sml_rx_state_words(uint64_t numel, uint32_t packet_numel, uint32_t batch_max, int int32) {
+    if (!valid_packet(packet_numel)) return 0;
+    const uint64_t B = sml_num_blocks(numel, packet_numel);
+    if (int32) return B + 3;
+    const uint64_t w = B + (B < batch_max ? B : batch_max);
+    return w ? w : 1;
+}
+
 }  // extern "C"
 
 namespace sml {

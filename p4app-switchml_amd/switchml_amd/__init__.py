@@ -125,6 +125,8 @@ def lib():
     L.sml_rdma_imm.argtypes = [vp, u64, u32, vp, vp]
     L.sml_frame_bytes.restype = u64
     L.sml_frame_bytes.argtypes = [u32]
+    L.sml_rx_state_words.restype = u64
+    L.sml_rx_state_words.argtypes = [u64, u32, u32, i32]
     L.sml_quantize_pack_frames.restype = i32
     L.sml_quantize_pack_frames.argtypes = [vp, u64, u32, u16, vp, u32, ctypes.POINTER(FrameParams), vp, u64, vp]
     L.sml_set_quantize_tile_slices.restype = u32
@@ -610,7 +612,8 @@ class RxSlice:
         self.numel, self.packet_numel, self.batch_max = numel, packet_numel, batch_max
         B = num_blocks(numel, packet_numel)
         self.exps = torch.zeros(B, dtype=torch.int8, device=device)
-        self.state = torch.zeros(max(1, B + min(B, batch_max)), dtype=torch.int64, device=device)
+        self.state = torch.zeros(int(lib().sml_rx_state_words(numel, packet_numel, batch_max, 0)),
+                                 dtype=torch.int64, device=device)
         self.counts = torch.zeros(2, dtype=torch.int64, device=device)
         self.out = out if out is not None else torch.zeros(numel, dtype=torch.float32, device=device)
 
@@ -659,7 +662,8 @@ class RxSliceInt32:
     def __init__(self, numel: int, packet_numel: int = 256, device="cuda", out=None):
         torch = _torch()
         self.numel, self.packet_numel = numel, packet_numel
-        self.state = torch.zeros(num_blocks(numel, packet_numel) + 3, dtype=torch.int64, device=device)
+        self.state = torch.zeros(int(lib().sml_rx_state_words(numel, packet_numel, 1, 1)), dtype=torch.int64,
+                                 device=device)
         self.counts = torch.zeros(2, dtype=torch.int64, device=device)
         self.out = out if out is not None else torch.zeros(numel, dtype=torch.int32, device=device)
 

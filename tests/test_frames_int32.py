@@ -111,6 +111,18 @@ def test_oracle_int32_rx_loop(P, n):
     assert rx.counts == [acc, dis] and acc == B
 
 
+def test_rx_state_words():
+    """sml_rx_state_words: the rx state a receive call needs (host-only)."""
+    import switchml_amd as sw
+    L = sw.lib()
+    for n, P, bm in [(0, 256, 64), (1, 64, 64), (20_011, 256, 64), (3 * 1024, 1024, 2), (10 ** 9 + 7, 128, 512)]:
+        B = O.num_blocks(n, P)
+        assert L.sml_rx_state_words(n, P, bm, 1) == B + 3
+        assert L.sml_rx_state_words(n, P, bm, 0) == max(1, B + min(B, bm))
+    assert L.sml_rx_state_words(1000, 100, 64, 0) == 0          # unsupported packet size
+    assert sw.RxSliceInt32(20_011, 256, device="cpu").state.numel() == O.num_blocks(20_011, 256) + 3
+
+
 # ---------------------------------------------------------------- GPU --
 
 @pytest.mark.gpu
