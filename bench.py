@@ -1163,6 +1163,27 @@ def extra_measurements(sw, torch, x, P, stream, reps=20):
     res["frames_int32_rx_device_GBps"] = round((4 * N + fbytes_i) / t / 1e9, 1)
     res["frames_int32_round_trip_exact"] = bool(torch.equal(rxi.out, xi))
     del iframes, rxi
+    # the same two on 4 cycled frame sets and outputs (cold, as the FLOAT32 4-set rates)
+    ifsets = [torch.empty(fbytes_i, dtype=torch.uint8, device=x.device) for _ in range(4)]
+    rxis = [sw.RxSliceInt32(N, P, device=x.device) for _ in range(4)]
+    k[0] = 0
+
+    def itx_cycle():
+        sw.pack_frames_int32(xi, fp, P, frames=ifsets[k[0] % 4], stream=stream)
+        k[0] += 1
+
+    def irx_cycle():
+        r = rxis[k[0] % 4]
+        r.reset(stream)
+        sw.unpack_frames_int32(ifsets[k[0] % 4], B, r, stream=stream)
+        k[0] += 1
+    t = timeit(itx_cycle, warm=8)
+    res["frames_int32_device_4sets_GBps"] = round((4 * N + fbytes_i) / t / 1e9, 1)
+    with torch.cuda.stream(stream):
+        t = timeit(irx_cycle, warm=8)
+    res["frames_int32_rx_device_4sets_GBps"] = round((4 * N + fbytes_i) / t / 1e9, 1)
+    res["frames_int32_4sets_exact"] = all(bool(torch.equal(r.out, xi)) for r in rxis)
+    del ifsets, rxis
     hframes = torch.empty(fbytes, dtype=torch.uint8).pin_memory()
     t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=hframes, stream=stream))
     res["frames_to_pinned_host_input_GBps"] = round(4 * N / t / 1e9, 2)
