@@ -309,10 +309,11 @@ def lead_stream(x, fp, P, K, pairs_iters, other_job):
 @pytest.mark.gpu
 @pytest.mark.parametrize("P", [256, 1024])
 def test_int32_rx_later_copy_claiming_first_is_fixed_up(cuda, P):
-    """Deterministic cover of the fix-up: later copies that claim their
+    """Cover of the fix-up by real races: later copies that claim their
     pkt_ids BEFORE the earlier copies (their wave runs ahead), with different
-    payloads.  The output must be the first copies' words, the counts exact,
-    and the slice's conflict total shows the later copies did claim first."""
+    payloads.  The output must be the first copies' words and the counts
+    exact; the slice's conflict total (printed) shows how many later copies
+    did claim first."""
     import torch
     import switchml_amd as sw
     K, pairs_iters = 3000, 64
@@ -341,8 +342,10 @@ def test_int32_rx_later_copy_claiming_first_is_fixed_up(cuda, P):
     bad = np.flatnonzero(got != ref)
     assert bad.size == 0, (bad.size, bad[:8].tolist())
     assert rx.counts.cpu().tolist() == [acc, dis]
+    # 256 of 256 (P = 256) and 64 of 64 (P = 1024) on MI355X in every run so
+    # far; a scheduling fact, not a correctness one, so reported rather than
+    # asserted (the fix-up itself is pinned by the white-box test below)
     print(f"P={P}: {rx.conflicts} of {pairs_iters * F} later copies claimed first")
-    assert rx.conflicts > 0                                     # 256 of 256 / 64 of 64 on MI355X
 
 
 def claim_tag(call, f):
