@@ -321,10 +321,14 @@ hipStream_t aux_stream() {
     return st;
 }
 
+// The device scratch is stream-ordered (hipMallocAsync / hipFreeAsync on the
+// plugin's stream): hipMalloc / hipFree may synchronise the whole device, and
+// RCCL calls iallreduce / test from its proxy thread while its own kernels
+// can be waiting on that proxy — a device-wide wait there could deadlock.
 void release_widened(Request* r) {
     delete[] r->widened;
     r->widened = nullptr;
-    if (r->dwidened) (void)hipFree(r->dwidened);
+    if (r->dwidened) (void)hipFreeAsync(r->dwidened, aux_stream());
     r->dwidened = nullptr;
 }
 
@@ -350,12 +354,13 @@ ncclResult_t sml_iallreduce(void* coll_comm, void* send, void* recv, int count, 
             if (ds) {
                 // device buffers: widen on the GPU into a device int32 scratch;
                 // the job reads it only after this stream has finished
-                if (hipMalloc(&r->dwidened, 4ull * (count > 0 ? count : 1)) != hipSuccess) {
+                hipStream_t st = aux_stream();
+                if (!st || hipMallocAsync(reinterpret_cast<void**>(&r->dwidened), 4ull * (count > 0 ? count : 1), st) !=
+                               hipSuccess) {
                     (void)hipGetLastError();
                     r->dwidened = nullptr;
-                    throw std::runtime_error("hipMalloc of the uint8 widening buffer failed");
+                    throw std::runtime_error("allocation of the uint8 widening buffer failed");
                 }
-                hipStream_t st = aux_stream();
                 if (sml_widen_u8_i32(static_cast<const uint8_t*>(send), r->dwidened, (uint64_t)count, st) != SML_OK ||
                     hipStreamSynchronize(st) != hipSuccess)
                     throw std::runtime_error("uint8 widening kernel failed");
