@@ -29,7 +29,7 @@ HipExponentQuantizerPPP::HipExponentQuantizerPPP(Config& config, WorkerTid worke
 HipExponentQuantizerPPP::~HipExponentQuantizerPPP() {
     job_slice_ = nullptr;
     if (server_) (void)sml_burst_server_destroy(server_);   // no throwing from a destructor
-    if (d_recv_exps_) (void)hipFree(d_recv_exps_);
+    if (d_recv_exps_) (void)hipFreeAsync(d_recv_exps_, stream_);   // stream-ordered allocation
     if (d_stage_) (void)hipFree(d_stage_);
     if (d_stage_exp_) (void)hipFree(d_stage_exp_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -86,9 +86,12 @@ void HipExponentQuantizerPPP::ensure_single_buffers() {
         hip_ok(hipMalloc(&d_stage_exp_, 16), "hipMalloc");
     }
     if (d_recv_exps_cap_ < total_main_num_ltus_) {
-        if (d_recv_exps_) hip_ok(hipFree(d_recv_exps_), "hipFree");
+        // stream-ordered: no device-wide sync on a worker thread (see
+        // loopback_backend.cc DeviceBuffer)
+        if (d_recv_exps_) hip_ok(hipFreeAsync(d_recv_exps_, stream_), "hipFreeAsync");
+        d_recv_exps_ = nullptr;
         d_recv_exps_cap_ = std::max<uint64_t>(total_main_num_ltus_, 1);
-        hip_ok(hipMalloc(&d_recv_exps_, d_recv_exps_cap_), "hipMalloc");
+        hip_ok(hipMallocAsync(reinterpret_cast<void**>(&d_recv_exps_), d_recv_exps_cap_, stream_), "hipMallocAsync");
     }
 }
 

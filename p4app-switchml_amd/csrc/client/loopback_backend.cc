@@ -45,20 +45,28 @@ void stream_wait(hipStream_t st) {
     hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
 }
 
-// Grow-only device buffer owned by one worker thread.
+// Grow-only device buffer owned by one worker thread, used only on that
+// worker's stream.  Stream-ordered (hipFreeAsync / hipMallocAsync on the
+// stream): the old buffer is released after the work already queued on it,
+// and no device-wide synchronisation happens on the worker thread — hipFree
+// waits for every stream of the device, which a worker serving RCCL's
+// CollNet proxy must not do while RCCL's kernels wait on that proxy.
 struct DeviceBuffer {
     void* p = nullptr;
     size_t cap = 0;
-    void* get(size_t bytes) {
+    hipStream_t owner = nullptr;
+    void* get(size_t bytes, hipStream_t st) {
         if (bytes > cap) {
-            if (p) hip_ok(hipFree(p), "hipFree");
+            if (p) hip_ok(hipFreeAsync(p, owner), "hipFreeAsync");
+            p = nullptr;
             cap = std::max<size_t>(bytes, 4096);
-            hip_ok(hipMalloc(&p, cap), "hipMalloc");
+            hip_ok(hipMallocAsync(&p, cap, st), "hipMallocAsync");
+            owner = st;
         }
         return p;
     }
     ~DeviceBuffer() {
-        if (p) (void)hipFree(p);
+        if (p) (void)hipFreeAsync(p, owner);
     }
 };
 
@@ -103,8 +111,8 @@ void run_packet_loop(HipExponentQuantizerPPP& ppp, const Config& cfg, WorkerStat
     int32_t* ring;
     uint8_t* extra;
     if (where == "device") {
-        ring = static_cast<int32_t*>(ws.ring.get(b * P * 4));
-        extra = static_cast<uint8_t*>(ws.ring_extra.get(b * 2));
+        ring = static_cast<int32_t*>(ws.ring.get(b * P * 4, ppp.stream()));
+        extra = static_cast<uint8_t*>(ws.ring_extra.get(b * 2, ppp.stream()));
         hip_ok(hipMemsetAsync(ring, 0, b * P * 4, ppp.stream()), "hipMemsetAsync");
     } else {
         const bool pin = where == "pinned";
@@ -178,11 +186,11 @@ uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, J
     if (in_d) {
         staged.slice.in_ptr = in_d;
     } else {
-        staged.slice.in_ptr = ws.in.get(bytes);
+        staged.slice.in_ptr = ws.in.get(bytes, st);
         hip_ok(hipMemcpyAsync(staged.slice.in_ptr, t.in_ptr, bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync H2D");
     }
     if (out_d) staged.slice.out_ptr = out_d;
-    else staged.slice.out_ptr = (t.out_ptr == t.in_ptr) ? staged.slice.in_ptr : ws.out.get(bytes);
+    else staged.slice.out_ptr = (t.out_ptr == t.in_ptr) ? staged.slice.in_ptr : ws.out.get(bytes, st);
 
     const uint64_t B = ppp->SetupJobSlice(&staged);
     const uint64_t P = ppp->ltu_numel();
@@ -202,8 +210,8 @@ uint64_t run_slice(PrePostProcessor& base, const Config& cfg, WorkerState& ws, J
                                       nullptr, cfg.backend_.hip.vcl ? SML_FLAG_ROUND_RNE : 0u, st),
                "sml_roundtrip_loopback");
     } else {  // bulk
-        void* payload = ws.payload.get(B * P * 4);
-        void* exps = ws.exps.get(B);
+        void* payload = ws.payload.get(B * P * 4, st);
+        void* exps = ws.exps.get(B, st);
         ppp->PreprocessBulk(payload, exps, nullptr, false);
         if (cfg.backend_.dummy.process_packets)
             sml_ok(sml_loopback_aggregate(static_cast<int32_t*>(payload), B * P, W, 0, st), "sml_loopback_aggregate");
