@@ -458,3 +458,69 @@ def test_int32_rx_scattered_pids_over_1GiB_output(cuda):
     torch.cuda.synchronize()
     assert rx.counts.cpu().tolist() == [B, 0]
     assert torch.equal(rx.out, x)
+
+
+@pytest.mark.gpu
+def test_int32_rx_random_streams(cuda):
+    """Randomized INT32 receive streams (Hypothesis, derandomized): any P,
+    slice length, 1-5 rx calls, copies with altered payloads before or after
+    the original, other jobs' frames, pkt_ids past the slice, frames missing
+    — output words and counts equal the sequential first-copy-wins loop after
+    every call."""
+    pytest.importorskip("hypothesis")
+    import torch
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+    import switchml_amd as sw
+
+    @settings(max_examples=60, deadline=None, derandomize=True, suppress_health_check=list(HealthCheck))
+    @given(n=st.integers(0, 30_000), P=st.sampled_from([64, 128, 256, 512, 1024]), job=st.integers(0, 255),
+           pairs=st.integers(0, 40), wrong=st.integers(0, 4), bad=st.integers(0, 3), drop=st.integers(0, 5),
+           calls=st.integers(1, 5), seed=st.integers(0, 2 ** 31))
+    def check(n, P, job, pairs, wrong, bad, drop, calls, seed):
+        rng = np.random.default_rng(seed)
+        fp = params(job_id=job)
+        fb = 52 + 4 * P
+        B = O.num_blocks(n, P)
+        x = int32_data(seed, n)
+        if B:
+            frames = O.build_frames_i32(x, fp, P=P)
+            s = altered_copies_stream(frames, B, fb, seed, pairs=min(pairs, B), max_gap=max(1, B))
+            rows = list(s.reshape(-1, fb))
+            for _ in range(min(drop, len(rows) - 1)):                  # frames that never arrive
+                rows.pop(int(rng.integers(len(rows))))
+            other = frames[:fb].copy()
+        else:
+            rows = []
+            other = np.zeros(fb, dtype=np.uint8)
+            other[43] = job
+        for _ in range(wrong):
+            f = other.copy()
+            f[43] = (job + 1) & 0xFF
+            rows.insert(int(rng.integers(len(rows) + 1)), f)
+        for _ in range(bad):
+            f = other.copy()
+            f[43] = job & 0xFF
+            f[44:48] = np.frombuffer(struct.pack("<I", B + int(rng.integers(0, 5))), dtype=np.uint8)
+            rows.insert(int(rng.integers(len(rows) + 1)), f)
+        if not rows:
+            return
+        s = np.concatenate(rows)
+        nfr = len(rows)
+        cuts = sorted(set(int(c) for c in rng.integers(1, nfr, calls - 1))) if nfr > 1 and calls > 1 else []
+        bounds = [0, *cuts, nfr]
+        seen = np.zeros(max(B, 1), dtype=np.uint8)
+        ref = np.zeros(n, dtype=np.int32)
+        acc = dis = 0
+        rx = sw.RxSliceInt32(n, P, device=cuda)
+        rx.reset()
+        for lo, hi in zip(bounds[:-1], bounds[1:]):
+            part = s[lo * fb:hi * fb]
+            a, d = python_rx(part, fb, n, P, job, seen, ref)
+            acc, dis = acc + a, dis + d
+            sw.unpack_frames_int32(torch.from_numpy(part.copy()).to(cuda), hi - lo, rx, job_id=job)
+            torch.cuda.synchronize()
+            assert np.array_equal(rx.out.cpu().numpy(), ref), (n, P, lo, hi)
+            assert rx.counts.cpu().tolist() == [acc, dis], (n, P, lo, hi)
+        assert int(rx.state[-3].item()) == len(bounds) - 1          # call sequence
+    check()
