@@ -400,7 +400,7 @@ sml_status_t sml_pack_frames_int32(const int32_t* d_in, uint64_t numel, uint32_t
  * zeroed per slice (sml_rx_reset), persists across calls; d_counts as for
  * sml_dequantize_frames.  One pass in stream order over the frames (an INT32
  * frame needs no other frame) plus a one-workgroup fix-up, on `stream`;
- * num_frames < 2^31 per call. */
+ * num_frames < 2^31 per call, fewer than 2^32 - 1 calls per slice. */
 sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, uint64_t frame_stride,
                                      uint64_t numel, uint32_t packet_numel, uint64_t job_id,
                                      uint64_t* d_state, int32_t* d_out, uint64_t* d_counts, void* stream);
