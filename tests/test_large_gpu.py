@@ -88,6 +88,28 @@ def test_frames_round_trip_past_4GiB(cuda):
     assert rx.counts.tolist() == [F, 0]
 
 
+def test_int32_frames_round_trip_past_4GiB(cuda):
+    """An INT32 slice of 5 GiB (≈ 5.3 GB of frames, pkt_ids past 2^20 and byte
+    offsets past 2^32 on both sides): tx, then the one-pass rx over the frames
+    in REVERSED order (every wave's stores far from the last one's), gives
+    the words back; every frame accepted."""
+    import torch
+    import switchml_amd as sw
+    dev = torch.device("cuda:0")
+    xi = _x(torch, dev).view(torch.int32)
+    fr = sw.pack_frames_int32(xi, sw.frame_params(job_id=5), packet_numel=P)
+    fb = sw.frame_bytes(P)
+    F = fr.numel() // fb
+    fr = fr.view(F, fb).flip(0).contiguous().view(-1)
+    rx = sw.RxSliceInt32(N, P, device=dev)
+    rx.reset()
+    sw.unpack_frames_int32(fr, F, rx, job_id=5)
+    del fr
+    torch.cuda.synchronize()
+    assert rx.counts.tolist() == [F, 0]
+    assert torch.equal(rx.out, xi)
+
+
 def test_batch_kernel_past_4GiB(cuda):
     """The batched round trip with a slice table spanning > 4 GiB (FIFO
     slices of one 5 GiB job, T = 3): equal to the single-slice launches."""
