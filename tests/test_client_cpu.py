@@ -108,6 +108,50 @@ def test_config_validation(ctx):
             C.stop()
 
 
+def test_reference_style_config_starts_unchanged(ctx):
+    """A user's switchml.cfg as the reference's Makefile assembles it (the
+    [general] keys of client_lib/src/configs/general.cfg, a backend section as
+    dummy.cfg's, the [timeouts] of timeouts.cfg — key names from those files,
+    values chosen here) starts the Context as it is: every [general] key is
+    read, controller_* are kept (no controller in this build), keys of
+    subsystems out of scope are ignored with a note, never fatal."""
+    C = ctx
+    ini = """
+# switchml.cfg
+[general]
+rank = 0
+num_workers = 2
+num_worker_threads = 4
+max_outstanding_packets = 256
+packet_numel = 256
+backend = dummy
+scheduler = fifo
+prepostprocessor = bypass
+instant_job_completion = false
+controller_ip = 10.0.0.7
+controller_port = 50099
+
+[backend.dummy]
+bandwidth = 0
+process_packets = true
+
+[timeouts]
+timeout = 10
+timeout_threshold = 100
+timeout_threshold_increment = 100
+"""
+    C.start(ini)
+    txt = C.config_text()
+    for want in ("num_workers = 2", "num_worker_threads = 4", "max_outstanding_packets = 256", "packet_numel = 256",
+                 "backend = dummy", "scheduler = fifo", "prepostprocessor = bypass", "controller_ip = 10.0.0.7",
+                 "controller_port = 50099"):
+        assert want in txt, want
+    j = C.allreduce_async(np.ones(10_000, dtype=np.float32))
+    j.wait()
+    assert j.status() == C.JOB_FINISHED
+    C.stop()
+
+
 def test_bad_ppp_name_fails_jobs_not_process(ctx):
     C = ctx
     try:
