@@ -152,6 +152,71 @@ def test_burst_int32_and_argument_checks(cuda):
         s.postprocess_burst(bt)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,Q,ring", [(1, 16, "pinned"), (3, 16, "device"), (2, 5, "pinned")])
+def test_rdma_message_loop_with_immediate_words(cuda, W, Q, ring):
+    """The RDMA worker's loop (rdma_worker_thread.cc:205-262, 330-356) through
+    the burst calls: 1024-element messages in Q queue-pair slots; message m
+    posts from slot m % Q with imm_data = m & 0xFFFF and PreprocessSingle's
+    extra info at imm byte 2 (:345-351); on receipt the short id is checked
+    and PostprocessSingle reads the exponent from the received imm byte 2
+    (:223-244), then slot m % Q is refilled with message m + Q.  The kernels
+    must write ONLY imm byte 2 (the message id in bytes 0-1 survives, byte 3
+    stays 0), and every message and the output must equal the oracle's packet
+    loop with b = Q."""
+    import torch
+    s = sw()
+    P, n = 1024, 70_001
+    x = O.splitmix_normal(W + Q, n) * np.float32(3.0)
+    pe, pp, ref_out, b = O.dummy_packet_stream(x, P=P, batch_max=Q, num_workers=W)
+    B = O.num_blocks(n, P)
+    assert b == min(B, Q)
+    total = B + b
+    xd = torch.from_numpy(x).to(cuda)
+    out = torch.full((n,), float("nan"), device=cuda)
+    recv = torch.zeros(B, dtype=torch.int8, device=cuda)
+    msgs = torch.zeros(b * P, dtype=torch.int32)
+    imm = torch.zeros(b, dtype=torch.int32).pin_memory()          # one imm word per queue pair
+    msgs = msgs.to(cuda) if ring == "device" else msgs.pin_memory()
+    stream = torch.cuda.current_stream(cuda)
+    cap_e = np.zeros(total, dtype=np.int8)
+    cap_p = np.zeros((total, P), dtype=np.uint32)
+
+    def burst(ids, pre):
+        bt = s.packet_burst(xd, out, P, W, b, recv, ids, [msgs.data_ptr() + (m % b) * P * 4 for m in ids],
+                            [imm.data_ptr() + 4 * (m % b) + 2 for m in ids])
+        (s.preprocess_burst if pre else s.postprocess_burst)(bt, stream)
+        torch.cuda.synchronize()
+
+    def post_sends(ids):                                          # PostSendWr for each message
+        iv = imm.numpy().view(np.uint32)
+        for m in ids:
+            iv[m % b] = m & 0xFFFF
+        burst(ids, True)
+        iv = imm.numpy().view(np.uint32)
+        mh = msgs.cpu().numpy().view(np.uint32).reshape(b, P)
+        for m in ids:
+            assert iv[m % b] & 0xFFFF == m & 0xFFFF and iv[m % b] >> 24 == 0, (m, hex(int(iv[m % b])))
+            cap_e[m] = np.int8(np.uint8((iv[m % b] >> 16) & 0xFF)) if m < B else 0
+            if m >= b:
+                k = m - b
+                cap_p[m, :min(P, n - k * P)] = mh[m % b, :min(P, n - k * P)]
+
+    post_sends(list(range(b)))
+    for p0 in range(0, total, b):
+        ids = list(range(p0, min(p0 + b, total)))
+        if W != 1:                                                 # the switch: x W on the payload words
+            s.loopback_aggregate(msgs.view(torch.int32)[: len(ids) * P], W)
+            torch.cuda.synchronize()
+        iv = imm.numpy().view(np.uint32)
+        assert all(iv[m % b] & 0xFFFF == m & 0xFFFF for m in ids)   # the expected short message ids
+        burst(ids, False)                                          # PostprocessSingle(imm byte 2)
+        post_sends([m + b for m in ids if m + b < total])
+    assert np.array_equal(cap_e, pe)
+    assert np.array_equal(cap_p, pp.view(np.uint32))
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref_out.view(np.uint32))
+
+
 def run_exchange(x, P, W, b_max, ring_place, cuda, rng, burst_cap=64, proc_in_kernel=True):
     """The same packet loop with one sml_exchange_burst per pass (post of p
     and pre of p + b into the slot, in one launch — DPDK's receive loop +
