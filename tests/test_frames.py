@@ -165,3 +165,55 @@ def test_rdma_messages(cuda, n):
     B = exps.numel()
     imm_i = sw.rdma_imm(None, num_blocks_int32=B, device=cuda).cpu().numpy().view(np.uint32)
     assert np.array_equal(imm_i, (np.arange(B) & 0xFFFF).astype(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", ["pinned", "device"])
+def test_per_packet_bursts_into_mbufs_equal_bulk_frames(cuda, where):
+    """A DPDK worker that keeps the per-packet PPP calls (BuildPacket by the
+    host, then PreprocessSingle into the mbuf: payload at offset 52, extra
+    info at offset 50 — dpdk_worker_thread_utils.inc:132-134) and runs them in
+    bursts, interleaved with PostprocessSingle of the returned packets as the
+    receive loop does (dpdk_worker_thread.cc:300-345), leaves exactly the
+    frames the fused frames kernel writes in bulk: the two entry points agree
+    byte for byte on the wire."""
+    import torch
+    import switchml_amd as sw
+    P, n, bm = 256, 50_003, 64
+    fp = params(job_id=3, max_outstanding_pkts=bm)
+    x = O.splitmix_normal(77, n)
+    want = O.build_frames(x, fp, P=P, batch_max=bm)
+    fb = 52 + 4 * P
+    B = O.num_blocks(n, P)
+    b = min(B, bm)
+    total = B + b
+    # BuildPacket's part: the headers; the PPP's part (exponent byte, payload) blank
+    pre = want.reshape(total, fb).copy()
+    pre[:, 50] = 0
+    pre[:, 52:] = 0
+    frames = torch.from_numpy(pre.reshape(-1).copy())
+    frames = frames.to(cuda) if where == "device" else frames.pin_memory()
+    base = frames.data_ptr()
+    xd = torch.from_numpy(x).to(cuda)
+    out = torch.full((n,), float("nan"), device=cuda)
+    recv = torch.zeros(B, dtype=torch.int8, device=cuda)
+    stream = torch.cuda.current_stream(cuda)
+
+    def burst(ids, pre_call):
+        if not ids:
+            return
+        bt = sw.packet_burst(xd, out, P, 1, b, recv, ids, [base + p * fb + 52 for p in ids],
+                             [base + p * fb + 50 for p in ids])
+        (sw.preprocess_burst if pre_call else sw.postprocess_burst)(bt, stream)
+
+    burst(list(range(b)), True)
+    for p0 in range(0, total, b):
+        ids = list(range(p0, min(p0 + b, total)))
+        burst(ids, False)                                            # the switch returned them unchanged (W = 1)
+        burst([q + b for q in ids if q + b < total], True)           # ReusePacket -> the next packet
+    torch.cuda.synchronize()
+    got = frames.cpu().numpy()
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, (bad.size, [(int(i) // fb, int(i) % fb) for i in bad[:8]])
+    _, _, ref_out, _ = O.dummy_packet_stream(x, P=P, batch_max=bm, num_workers=1)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref_out.view(np.uint32))
