@@ -217,3 +217,33 @@ def test_per_packet_bursts_into_mbufs_equal_bulk_frames(cuda, where):
     assert bad.size == 0, (bad.size, [(int(i) // fb, int(i) % fb) for i in bad[:8]])
     _, _, ref_out, _ = O.dummy_packet_stream(x, P=P, batch_max=bm, num_workers=1)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), ref_out.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_per_packet_int32_bursts_into_mbufs_equal_bulk_frames(cuda):
+    """The same for an INT32 slice (no extra batch, no exponent): per-packet
+    bursts into mbuf-layout frames == sml_pack_frames_int32, and the receive
+    side's bursts give the words back."""
+    import torch
+    import switchml_amd as sw
+    P, n = 256, 30_011
+    fp = params(job_id=6)
+    xi = np.random.default_rng(8).integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+    want = O.build_frames_i32(xi, fp, P=P)
+    fb = 52 + 4 * P
+    B = O.num_blocks(n, P)
+    pre = want.reshape(B, fb).copy()
+    pre[:, 52:] = 0
+    frames = torch.from_numpy(pre.reshape(-1).copy()).pin_memory()
+    base = frames.data_ptr()
+    xd = torch.from_numpy(xi).to(cuda)
+    out = torch.zeros(n, dtype=torch.int32, device=cuda)
+    for p0 in range(0, B, sw.MAX_BURST):
+        ids = list(range(p0, min(p0 + sw.MAX_BURST, B)))
+        bt = sw.packet_burst(xd, out, P, 1, 0, None, ids, [base + p * fb + 52 for p in ids],
+                             [base + p * fb + 50 for p in ids])
+        sw.preprocess_burst(bt)
+        sw.postprocess_burst(bt)
+    torch.cuda.synchronize()
+    assert np.array_equal(frames.numpy(), want)
+    assert np.array_equal(out.cpu().numpy(), xi)
