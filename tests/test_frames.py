@@ -132,6 +132,47 @@ def test_frames_global_exponents_and_misaligned_slice(cuda):
     assert np.array_equal(got.cpu().numpy(), ref)
 
 
+@pytest.mark.gpu
+def test_frames_random_parameters(cuda):
+    """Randomized frame builds (Hypothesis, derandomized): any P, slice
+    length, W, batch, job id, pool start / shift / max outstanding, frame
+    padding, misalignment of the slice, global exponents or not, device or
+    pinned frames — every byte equal to the oracle's BuildPacket +
+    PreprocessSingle, padding untouched."""
+    pytest.importorskip("hypothesis")
+    import torch
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+    import switchml_amd as sw
+
+    @settings(max_examples=60, deadline=None, derandomize=True, suppress_health_check=list(HealthCheck))
+    @given(n=st.integers(1, 20_000), P=st.sampled_from([64, 128, 256, 512, 1024]), W=st.integers(1, 9),
+           bm=st.integers(1, 300), job=st.integers(0, 2 ** 16 - 1), start=st.integers(0, 2 ** 15 - 1),
+           shift=st.integers(0, 4000), mop=st.integers(1, 512), pad=st.sampled_from([0, 4, 12, 60]),
+           off=st.integers(0, 3), glob=st.booleans(), pinned=st.booleans(), seed=st.integers(0, 2 ** 31))
+    def check(n, P, W, bm, job, start, shift, mop, pad, off, glob, pinned, seed):
+        fp = params(job_id=job, pool_index_start=start, pool_index_shift=shift, max_outstanding_pkts=mop)
+        xfull = O.splitmix_normal(seed, n + off) * np.float32(2.0 ** ((seed % 40) - 20))
+        x = xfull[off:]
+        B = O.num_blocks(n, P)
+        b = min(B, bm)
+        ge = None
+        if glob:
+            ge = np.clip(O.exponents(x, P).astype(np.int32) + (seed % 3), -128, 127).astype(np.int8)
+        ref = O.build_frames(x, fp, P=P, num_workers=W, batch_max=bm, global_exps=ge)
+        stride = 52 + 4 * P + pad
+        frames = torch.full(((B + b) * stride,), 0xAB, dtype=torch.uint8)
+        frames = frames.pin_memory() if pinned else frames.to(cuda)
+        xd = torch.from_numpy(xfull).to(cuda)[off:]
+        sw.quantize_pack_frames(xd, fp, P, W, batch_max=bm, frames=frames, stride=stride,
+                                global_exps=None if ge is None else torch.from_numpy(ge).to(cuda))
+        torch.cuda.synchronize()
+        got = frames.cpu().numpy().reshape(B + b, stride)
+        assert np.array_equal(got[:, :52 + 4 * P], ref.reshape(B + b, 52 + 4 * P)), (n, P, W, bm, off)
+        assert np.all(got[:, 52 + 4 * P:] == 0xAB)
+    check()
+
+
 # ------------------------------------------------------- RDMA (F4) -----
 
 def rdma_imm_reference(exps, batch_max):
