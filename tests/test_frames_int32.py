@@ -524,3 +524,35 @@ def test_int32_rx_random_streams(cuda):
             assert rx.counts.cpu().tolist() == [acc, dis], (n, P, lo, hi)
         assert int(rx.state[-3].item()) == len(bounds) - 1          # call sequence
     check()
+
+
+@pytest.mark.gpu
+def test_int32_frames_random_parameters(cuda):
+    """Randomized INT32 frame builds (Hypothesis, derandomized): any P,
+    length, job id, pool start / shift / max outstanding, padding,
+    misalignment, device or pinned frames — every byte equal to the oracle."""
+    pytest.importorskip("hypothesis")
+    import torch
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+    import switchml_amd as sw
+
+    @settings(max_examples=50, deadline=None, derandomize=True, suppress_health_check=list(HealthCheck))
+    @given(n=st.integers(1, 20_000), P=st.sampled_from([64, 128, 256, 512, 1024]),
+           job=st.integers(0, 2 ** 16 - 1), start=st.integers(0, 2 ** 15 - 1), shift=st.integers(0, 4000),
+           mop=st.integers(1, 512), pad=st.sampled_from([0, 4, 12, 60]), off=st.integers(0, 3),
+           pinned=st.booleans(), seed=st.integers(0, 2 ** 31))
+    def check(n, P, job, start, shift, mop, pad, off, pinned, seed):
+        fp = params(job_id=job, pool_index_start=start, pool_index_shift=shift, max_outstanding_pkts=mop)
+        full = int32_data(seed, n + off)
+        ref = O.build_frames_i32(full[off:], fp, P=P)
+        B = O.num_blocks(n, P)
+        stride = 52 + 4 * P + pad
+        frames = torch.full((B * stride,), 0xAB, dtype=torch.uint8)
+        frames = frames.pin_memory() if pinned else frames.to(cuda)
+        sw.pack_frames_int32(torch.from_numpy(full).to(cuda)[off:], fp, P, frames=frames, stride=stride)
+        torch.cuda.synchronize()
+        got = frames.cpu().numpy().reshape(B, stride)
+        assert np.array_equal(got[:, :52 + 4 * P], ref.reshape(B, 52 + 4 * P)), (n, P, off)
+        assert np.all(got[:, 52 + 4 * P:] == 0xAB)
+    check()
