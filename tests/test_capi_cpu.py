@@ -192,3 +192,23 @@ def test_rx_frames_validation_without_gpu(sw):
     assert f(frames, 2 ** 32, 1076, 16, 256, 1, 64, 0, ex, st, out, None, None) == sw.SML_ERR_UNSUPPORTED
     cnt = (ctypes.c_uint64 * 3)()
     assert f(frames, 1, 1076, 16, 256, 1, 64, 0, ex, st, out, ctypes.addressof(cnt) + 4, None) == sw.SML_ERR_ALIGNMENT
+
+
+@pytest.mark.parametrize("header", ["switchml_hip.h", "switchml_client.h"])
+def test_public_header_is_plain_c(header, tmp_path):
+    """The drop-in boundary is a C ABI: each public header compiles on its own
+    as strict C99 (what a cgo / JNI / N-API stub includes) and as C++11, with
+    every warning an error."""
+    import os
+    import shutil
+    import subprocess
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    src = tmp_path / "inc.c"
+    src.write_text(f'#include "{header}"\nint main(void) {{ return 0; }}\n')
+    for cc, std in (("gcc", "-std=c99"), ("g++", "-std=c++11")):
+        if not shutil.which(cc):
+            pytest.skip(f"{cc} not found")
+        lang = ["-x", "c++"] if cc == "g++" else []
+        r = subprocess.run([cc, std, "-Wall", "-Wextra", "-pedantic", "-Werror", "-fsyntax-only", *lang, f"-I{inc}",
+                            str(src)], capture_output=True, text=True)
+        assert r.returncode == 0, (cc, r.stderr[-2000:])
