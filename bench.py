@@ -1187,7 +1187,31 @@ def extra_measurements(sw, torch, x, P, stream, reps=20):
     hframes = torch.empty(fbytes, dtype=torch.uint8).pin_memory()
     t = timeit(lambda: sw.quantize_pack_frames(x, fp, P, 1, batch_max=64, frames=hframes, stream=stream))
     res["frames_to_pinned_host_input_GBps"] = round(4 * N / t / 1e9, 2)
-    del hframes
+    # the receive side from a NIC's rx ring: returned frames in pinned host
+    # memory, read by the rx kernels over PCIe, fp32 out in HBM (output bytes / s)
+    hrx = sw.RxSlice(N, P, 64, device=x.device)
+
+    def hrx_once():
+        hrx.reset(stream)
+        sw.dequantize_frames(hframes, fbytes // sw.frame_bytes(P), hrx, num_workers=1, stream=stream)
+    with torch.cuda.stream(stream):
+        t = timeit(hrx_once)
+    res["frames_rx_from_pinned_host_output_GBps"] = round(4 * N / t / 1e9, 2)
+    res["frames_rx_from_pinned_host_exact"] = bool(torch.equal(hrx.out.view(torch.int32),
+                                                               sw.roundtrip_loopback(x, P, 1).view(torch.int32)))
+    del hframes, hrx
+    hi = torch.empty(fbytes_i, dtype=torch.uint8).pin_memory()
+    sw.pack_frames_int32(xi, fp, P, frames=hi, stream=stream)
+    hrxi = sw.RxSliceInt32(N, P, device=x.device)
+
+    def hrxi_once():
+        hrxi.reset(stream)
+        sw.unpack_frames_int32(hi, B, hrxi, stream=stream)
+    with torch.cuda.stream(stream):
+        t = timeit(hrxi_once)
+    res["frames_int32_rx_from_pinned_host_output_GBps"] = round(4 * N / t / 1e9, 2)
+    res["frames_int32_rx_from_pinned_host_exact"] = bool(torch.equal(hrxi.out, xi))
+    del hi, hrxi
     # K6: the switch's aggregation over W worker planes fused with the
     # dequantize (the peer-to-peer switch's compute; planes local here)
     sw.quantize_pack(x, P, 1, payload=payload, exps_out=exps, stream=stream)
