@@ -137,3 +137,28 @@ def test_roofline_traffic_covers_the_n_gt1_slices():
         alg = 8 * n + n // 256
         assert abs(t / alg - 1) < 1e-3, (G, t / alg)
     assert bench.load_traffic(12345, 256, "quantize_pack_cold") is None
+
+
+def test_scale_report_tabulates_bench_lines(tmp_path):
+    """tools/scale_report.py finds bench lines in JSON files and text logs and
+    tabulates them (used on the driver's scaling run)."""
+    import importlib.util
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("scale_report", os.path.join(root, "tools", "scale_report.py"))
+    sr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sr)
+    one = {"metric": "m", "n_gpus": 1, "value": 6500.0, "roofline": {"frac": 0.82}, "ms_per_step": 0.082,
+           "self_check": True}
+    two = {"metric": "m", "n_gpus": 2, "value": 12000.0, "roofline": {"frac": 0.8}, "ms_per_step": 0.09,
+           "self_check": True, "weak_256MiB_value": 13000.0, "weak_256MiB": {"roofline": {"frac": 0.81}},
+           "switchsim": {"ms_per_allreduce": 5.0, "busbw_GBps": 200.0, "frac_of_xgmi_bound": 0.4, "verified": True,
+                         "phases_ms": {"k2": 0.1, "payload_sum": 4.0}}}
+    (tmp_path / "scale.json").write_text(json.dumps({"runs": [two, one]}))
+    (tmp_path / "log.txt").write_text("banner\nrank0 " + json.dumps(two) + "\n")
+    got = list(sr.load(str(tmp_path / "scale.json"))) + list(sr.load(str(tmp_path / "log.txt")))
+    assert [b["n_gpus"] for b in got] == [2, 1, 2]
+    rep = sr.report(got[:2])
+    assert "| 2 | switchsim | 5.000 |" in rep and "payload_sum 4.00" in rep
+    assert "| 2 | 0.923 |" in rep                     # 12000 / (2 x 6500)
