@@ -162,8 +162,13 @@ def frames_summary(src, dst, numel, packet_numel, batch_max=64):
                 w.writerow(r)
     B = -(-numel // packet_numel)
     fbytes = (B + min(B, batch_max)) * (52 + 4 * packet_numel)
-    alg = {"k_quantize_frames": (4 * numel, fbytes), "k_rx_apply": (fbytes, 4 * numel),
-           "k_rx_claim": (None, None)}   # k_rx_apply also retires the winners (the old commit pass)
+    fbytes_i = B * (52 + 4 * packet_numel)   # INT32 slices: B frames, no extra batch
+    alg = {"k_quantize_frames<%d, true, false, true, false>" % packet_numel: (4 * numel, fbytes),
+           "k_quantize_frames<%d, true, false, true, true>" % packet_numel: (4 * numel, fbytes_i),
+           "k_rx_apply": (fbytes, 4 * numel),
+           "k_rx_claim": (None, None),   # k_rx_apply also retires the winners (the old commit pass)
+           "k_rx_int32<": (fbytes_i, 4 * numel),
+           "k_rx_int32_fixup": (None, None)}
 
     def pmc(sub, counter, key):
         rr = rows(os.path.join(src, sub, "pmc_counter_collection.csv"))

@@ -55,6 +55,35 @@ def main(N=64 * 2 ** 20, P=256, bm=64, reps=20, sets=int(os.environ.get("FRAME_S
     ref = sw.roundtrip_loopback(x, P, 1)
     torch.cuda.synchronize()
     res["rx_equals_roundtrip"] = all(bool(torch.equal(ref.view(torch.int32), r.out.view(torch.int32))) for r in rxs)
+    del frames, rxs, ref
+    # INT32 slices: B frames, tx = k_quantize_frames<.., I32>, rx = k_rx_int32 + fix-up
+    xi = x.view(torch.int32)
+    fbi = B * sw.frame_bytes(P)
+    iframes = [torch.empty(fbi, dtype=torch.uint8, device=dev) for _ in range(sets)]
+    irxs = [sw.RxSliceInt32(N, P, device=dev) for _ in range(sets)]
+
+    def itx():
+        sw.pack_frames_int32(xi, fp, P, frames=iframes[k[0] % sets])
+        k[0] += 1
+
+    def irx():
+        r = irxs[k[0] % sets]
+        r.reset()
+        sw.unpack_frames_int32(iframes[k[0] % sets], B, r)
+        k[0] += 1
+
+    for name, fn in (("int32_tx", itx), ("int32_rx", irx)):
+        k[0] = 0
+        for _ in range(sets):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / reps
+        res[name] = {"us": round(t * 1e6, 1), "GBps": round((4 * N + fbi) / t / 1e9, 1)}
+    res["int32_rx_exact"] = all(bool(torch.equal(r.out, xi)) for r in irxs)
     print(json.dumps(res))
 
 
