@@ -52,15 +52,32 @@ def run_child(cmd, env, out_dir, timeout, what):
     return p.returncode, out, err, wall
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-def test_bench_n2_rehearsal_line(cuda, tmp_path):
+@pytest.mark.parametrize("launcher", ["bench", "driver"])
+def test_bench_n2_rehearsal_line(cuda, tmp_path, launcher):
+    """launcher "bench": `bench.py --gpus 2` starts its ranks itself;
+    "driver": the driver's own form, `python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P
+    bench.py --gpus 2 ...` (RANK / LOCAL_RANK / MASTER_* from torchrun)."""
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
            and not k.startswith("TORCHELASTIC_")}
     env["SML_BENCH_REHEARSE"] = "1"
-    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2"]
-    rc, out, err, wall = run_child(cmd, env, str(tmp_path), 800, "bench.py --gpus 2 (rehearsal)")
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2"]
+    if launcher == "bench":
+        cmd = [sys.executable, "-u", *args]
+    else:
+        cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
+    rc, out, err, wall = run_child(cmd, env, str(tmp_path), 800, f"bench.py --gpus 2 (rehearsal, {launcher})")
     lines = [l for l in out.splitlines() if l.startswith("{")]
     assert lines, f"no JSON line (rc {rc}); stderr tail:\n{err}"
     line = json.loads(lines[-1])
