@@ -61,8 +61,8 @@ def _free_port():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("launcher", ["bench", "driver"])
-def test_bench_n2_rehearsal_line(cuda, tmp_path, launcher):
+@pytest.mark.parametrize("launcher,n", [("bench", 2), ("driver", 2), ("driver", 4)])
+def test_bench_n2_rehearsal_line(cuda, tmp_path, launcher, n):
     """launcher "bench": `bench.py --gpus 2` starts its ranks itself;
     "driver": the driver's own form, `python -m torch.distributed.run
     --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P
@@ -71,24 +71,24 @@ def test_bench_n2_rehearsal_line(cuda, tmp_path, launcher):
            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
            and not k.startswith("TORCHELASTIC_")}
     env["SML_BENCH_REHEARSE"] = "1"
-    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2"]
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "4", "--warmup", "2"]
     if launcher == "bench":
         cmd = [sys.executable, "-u", *args]
     else:
-        cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+        cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
-    rc, out, err, wall = run_child(cmd, env, str(tmp_path), 800, f"bench.py --gpus 2 (rehearsal, {launcher})")
+    rc, out, err, wall = run_child(cmd, env, str(tmp_path), 800, f"bench.py --gpus {n} (rehearsal, {launcher})")
     lines = [l for l in out.splitlines() if l.startswith("{")]
     assert lines, f"no JSON line (rc {rc}); stderr tail:\n{err}"
     line = json.loads(lines[-1])
     assert rc == 0, (rc, line.get("failures"), line.get("diagnostic_failures"), err[-1500:])
-    assert line["n_gpus"] == 2 and line["steps"] == 4 and line["warmup"] == 2
+    assert line["n_gpus"] == n and line["steps"] == 4 and line["warmup"] == 2
     assert line["config"]["process_group"]["backend"] == "nccl"
     assert line["config"]["process_group"]["rehearsal"]
     assert line["self_check"] is True and line["self_check_detail"]["buckets_checked_min_over_ranks"] == 4
     for k in bench.SWITCH_PATHS:
         assert line[k].get("verified") is True, (k, line[k])
-        assert line[k]["workers"] == 2
+        assert line[k]["workers"] == n
     assert line["p2p_switch"]["bit_equal_to_switchsim"] and line["xgmi_switch"]["bit_equal_to_switchsim"]
     assert line["ms_per_step"] * line["steps"] / 1e3 < wall
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
