@@ -9,13 +9,18 @@ in HBM, as one launch of the fused HIP kernel sml_quantize_pack (K1) per GPU.
 Exponents are the loopback's (the dummy backend returns them unchanged, so
 the local exponent is the global one: W = 1).
 
-N = 1 (default): the step is K1 over one 256 MiB bucket (configs[2]'s bucket).
-N > 1 (`--gpus N`; the N ranks are started here when WORLD_SIZE is unset, or
-by torch.distributed.run): the step is configs[3] — ONE 1 GiB job split over
-the N GPUs by the FIFO rule (fifo_scheduler.cc:93-109, slice g -> GPU g); the
-path has no exchange step at W = 1, so no collective runs in the timed region
-(strong scaling: total work fixed).  Beside it, first-class fields time the
-switch simulation with W = N real workers (each holding its own 1 GiB bucket):
+Every N (1 by default; `--gpus N` starts the N ranks itself when WORLD_SIZE
+is unset, or they come from torch.distributed.run) reports the SAME two
+readings, each with its own timed region, self-check and roofline, so a
+1/2/4/8 curve compares each reading with itself:
+  value = weak_256MiB_value   the step is K1 over a 256 MiB bucket (configs[2]'s
+              bucket) on EVERY GPU, 4 buckets cycled; `scaling` "weak" at every N
+  strong_1GiB_value   the step is configs[3] — ONE 1 GiB job split over the N
+              GPUs by the FIFO rule (fifo_scheduler.cc:93-109, slice g -> GPU
+              g; the whole job on one GPU at N = 1); strong scaling
+The path has no exchange step at W = 1, so no collective runs in either timed
+region.  At N > 1, first-class fields beside them time the switch simulation
+with W = N real workers (each holding its own 1 GiB bucket):
   switchsim   K2 -> RCCL int8 MAX -> K3 -> RCCL int32 SUM -> K4 (ring, xGMI)
   p2p_switch  K2 -> RCCL int8 MAX -> K3 -> K6 over the peers' HBM (hipIpc,
               xGMI) on this rank's block shard -> RCCL all_gather (fp32)
@@ -73,10 +78,14 @@ def parse(argv=None):
                          "(HBM/fabric clocks ramp under load: profiles/r01/bench_warmup_sweep.jsonl)")
     ap.add_argument("--numel", type=int, default=64 * 1024 * 1024, help="fp32 elements per GPU at N=1 (256 MiB)")
     ap.add_argument("--packet-numel", type=int, default=256)
-    ap.add_argument("--job-numel", type=int, default=-1,
-                    help="strong scaling: one job of this many fp32 elements split over the ranks by the FIFO "
-                         "rule; -1 = configs[3]'s 268435456 (1 GiB) when N > 1, --numel per GPU when N = 1; "
-                         "0 = --numel per GPU (weak scaling) at any N")
+    ap.add_argument("--job-numel", type=int, default=CFG3_JOB_NUMEL,
+                    help="the strong_1GiB reading (at every N, beside the weak headline): one job of this many "
+                         "fp32 elements split over the ranks by the FIFO rule (default configs[3]'s 268435456 = "
+                         "1 GiB; 0 = skip the reading)")
+    ap.add_argument("--strong-steps", type=int, default=200,
+                    help="timed steps of the strong_1GiB reading (fixed, so its value does not carry the first "
+                         "launch's latency at N = 8's 128 MiB slices the way 20 steps would)")
+    ap.add_argument("--strong-warmup", type=int, default=100)
     ap.add_argument("--switch-numel", type=int, default=CFG3_JOB_NUMEL,
                     help="N > 1: fp32 elements per worker for the switchsim / p2p_switch fields (0 = skip them)")
     ap.add_argument("--exchange-timeout", type=float, default=300.0,
@@ -353,18 +362,6 @@ def main():
     sw.set_xcd_chunk(args.xcd_chunk)
 
     P = args.packet_numel
-    job_numel = args.job_numel if args.job_numel >= 0 else (CFG3_JOB_NUMEL if world > 1 else 0)
-    off = 0
-    if job_numel:
-        # configs[3]: one job sharded over the ranks, slice g -> GPU g (fifo_scheduler.cc:93-109)
-        off, N = sw.fifo_slice(job_numel, world, rank)
-        total_alg = sum(8 * n + sw.num_blocks(n, P)
-                        for n in (sw.fifo_slice(job_numel, world, r)[1] for r in range(world)))
-    else:
-        N = args.numel
-        total_alg = world * (8 * N + sw.num_blocks(N, P))
-    B = sw.num_blocks(N, P)
-    alg_bytes = 8 * N + B
     if args.graph_steps > 1:
         # hipGraph capture needs a non-default stream: the whole run (launchers,
         # capture, replays, the timing events) moves to one
@@ -373,107 +370,25 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
     nb = max(1, args.buckets)
-    # bucket b = elements [off, off + N) of the job bench_bucket(4242 + b, .):
-    # integer-exact, so the timed planes can be checked against committed digests
-    xs = [bench_bucket(torch, BENCH_SEED0 + b, off, N, dev) for b in range(nb)]
-    pls = [torch.empty(B * P, dtype=torch.int32, device=dev) for _ in range(nb)]
-    exs = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nb)]
-    x, payload, exps = xs[0], pls[0], exs[0]
-    cyc = [0]
 
-    # one prepared C call per step (arguments checked once: the first step's
-    # launch is not delayed by the Python wrapper)
-    launchers = [sw.quantize_pack_launcher(xs[i], P, 1, pls[i], exps_out=exs[i], stream=stream) for i in range(nb)]
+    # The headline, `value` = weak_256MiB_value at every N: every GPU runs K1
+    # over its own 256 MiB buckets (the metric's bucket; N = 1 is configs[2]'s).
+    hl = k1_reading(sw, torch, dist, world, rank, dev, stream, 0, args.numel, P, nb, args.steps, args.warmup,
+                    args.settle_ms, args.graph_steps)
+    # The second named reading at every N, strong_1GiB_value: configs[3]'s one
+    # 1 GiB job split over the N GPUs by the FIFO rule (at N = 1 the whole job
+    # on one GPU), its own timed region, self-check and roofline.
+    st = None
+    if args.job_numel:
+        st = k1_reading(sw, torch, dist, world, rank, dev, stream, args.job_numel, 0, P, nb, args.strong_steps,
+                        args.strong_warmup, args.settle_ms, 1)
+    N, B, alg_bytes = hl["numel_per_gpu"], hl["num_blocks_per_gpu"], hl["alg_bytes_per_gpu"]
+    elapsed, kern_ms_max = hl["elapsed_s"], hl["kernel_ms"]
 
-    def launch():
-        i = cyc[0]
-        cyc[0] = (i + 1) % nb
-        launchers[i]()
-
-    step, per_call = launch, 1
-    if args.graph_steps > 1:
-        # G consecutive steps captured into one hipGraph (G kernel nodes);
-        # each replay still runs exactly G full steps.  The captured steps
-        # cycle the buckets from bucket 0, so every replay covers every
-        # bucket only when G is a multiple of their number.
-        if args.graph_steps % nb:
-            sys.exit(f"bench.py: --graph-steps {args.graph_steps} must be a multiple of --buckets {nb} "
-                     "(each replay repeats the same captured steps)")
-        if args.steps % args.graph_steps or args.warmup % args.graph_steps:
-            sys.exit("bench.py: --steps and --warmup must be multiples of --graph-steps")
-        launch()
-        torch.cuda.synchronize()
-        cyc[0] = 0
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=stream):
-            for _ in range(args.graph_steps):
-                launch()
-        step, per_call = graph.replay, args.graph_steps
-
-    settle(step, args.settle_ms)
-    for _ in range(args.warmup // per_call):
-        step()
-    torch.cuda.synchronize()
-
-    # Timed region: K back-to-back launches on `stream`, bracketed by a barrier
-    # and a device sync on both sides (wall clock -> value), and by two HIP
-    # events recorded on the launch stream itself (-> average launch duration
-    # for the roofline; includes the inter-launch gaps, so it is conservative
-    # against rocprofv3's per-dispatch durations).
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # one untimed pass through the timing code itself (events, syncs,
-    # barriers), so lazy first-use costs of those calls stay out of the region
-    for _ in range(2):
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        ev0.record(stream)
-        step()
-        ev1.record(stream)
-        torch.cuda.synchronize()
-        _ = ev0.elapsed_time(ev1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps // per_call):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    # The closing barrier brackets the region but its own latency (a
-    # collective, tens of us at N = 8 against ~0.4 ms of K1 at 20 steps of
-    # 128 MiB) is not a step: each rank stops its clock at its device sync
-    # and the MAX over ranks below is the job's time.
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms_max = float(t[0]), float(t[1])
-
-    # self-check: the planes the TIMED launches left (the last launch on each
-    # bucket, the kernel instance and knobs of this run) hashed and compared
-    # with the oracle's digests of the same inputs (tests/golden/digests_bench.json)
-    want = expected_digests(job_numel, world, rank, N, P, nb)
-    if want is None:
-        ok, check_note = True, "no committed digest for this shape: not checked"
-        checked = 0
-    else:
-        got = [planes_sha256(torch, exs[b], pls[b], N, P) for b in range(nb)]
-        bad = [b for b in range(nb) if got[b] != want[b]]
-        ok, checked = not bad, nb
-        check_note = ("timed exponent + BE payload planes of every bucket == tests/golden/digests_bench.json"
-                      if ok else f"buckets {bad} differ from tests/golden/digests_bench.json")
-    ok_t = torch.tensor([int(ok), checked], dtype=torch.int32, device=dev)
-    if world > 1:
-        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
-    ok, checked = bool(ok_t[0].item()), int(ok_t[1].item())
-    del xs, pls, exs, x, payload, exps
-
-    failures = [] if ok else ["self_check: " + check_note]
+    failures = []
+    for r in (hl, st):
+        if r is not None and not r["ok"]:
+            failures.append(f"self_check ({r['name']}): " + r["check_note"])
     diag_failures = []          # diagnostic fields: reported, not fatal (module docstring)
     side, fields, extra = {}, {}, {}
 
@@ -482,18 +397,11 @@ def main():
         if rank != 0:
             return
         ms_per_step = elapsed * 1e3 / args.steps
-        value = total_alg / (elapsed / args.steps) / 1e9
+        value = hl["total_alg"] / (elapsed / args.steps) / 1e9
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
-        if job_numel:
-            workload = (f"configs[3]: one {job_numel * 4 >> 20} MiB fp32 job sharded over {world} GPU(s) by the FIFO "
-                        f"rule ({N} elements on rank 0), fused exponent+quantize+BE pack (sml_quantize_pack, K1), "
-                        "loopback exponents (W=1); `value` is this job's STRONG-scaling rate (total work fixed, "
-                        "each GPU's slice shrinks as N grows)" +
-                        ("; `weak_256MiB_value` is the WEAK-scaling rate (256 MiB per GPU at every N)"
-                         if world > 1 else ""))
-        else:
-            workload = (f"configs[2]-sized bucket: {N * 4 >> 20} MiB fp32 per GPU, fused exponent+quantize+BE pack "
-                        "(sml_quantize_pack, K1), loopback exponents (W=1)")
+        workload = (f"configs[2]-sized bucket: {N * 4 >> 20} MiB fp32 on EVERY GPU ({world} GPU(s), weak scaling), "
+                    "fused exponent+quantize+BE pack (sml_quantize_pack, K1), loopback exponents (W=1); `value` "
+                    "= weak_256MiB_value at every N; strong_1GiB_value = configs[3]'s 1 GiB job split over the N GPUs")
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -504,25 +412,26 @@ def main():
             "settle_ms": args.settle_ms,
             "ms_per_step": round(ms_per_step, 5),
             "higher_is_better": True,
-            "scaling": "strong" if job_numel else "weak",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32->i32",
             "data": ("synthetic gradient-like fp32 generated on device from integers only (bench_bucket: "
-                     "splitmix64 24-bit mantissas x 2^-(24..39), seed 4242 + bucket, global element index)"),
+                     "splitmix64 24-bit mantissas x 2^-(24..39), seed 4242 + bucket, global element index); "
+                     "every GPU holds its own copy of the same 4 buckets"),
             "config": {
                 "workload": workload,
-                "job_numel": job_numel or world * N,
+                "job_numel": world * N,
                 "numel_per_gpu": N,
                 "packet_numel": P,
                 "num_blocks_per_gpu": B,
-                "parallelism": f"shard{world} (FIFO slices, no data-path collective)",
+                "parallelism": f"shard{world} (every GPU its own buckets, no data-path collective)",
                 "bytes_per_step_per_gpu": alg_bytes,
                 "buckets_cycled": nb,
                 "xcd_chunk": args.xcd_chunk,
                 "launch": "eager" if args.graph_steps <= 1 else f"hipGraph replay, {args.graph_steps} steps per graph",
                 "process_group": pg,
             },
-            "input_GBps": round(4 * (job_numel or world * N) / (elapsed / args.steps) / 1e9, 2),
+            "input_GBps": round(4 * world * N / (elapsed / args.steps) / 1e9, 2),
             "kernel_ms": round(kern_ms_max, 5),
             "roofline": {
                 "bound": "hbm",
@@ -533,8 +442,8 @@ def main():
                 "traffic": load_traffic(N, P, "quantize_pack" if nb == 1 else "quantize_pack_cold"),
                 "kernel": f"sml::k_quantize_pack<{P},aligned,fused,BE,half-away> (K1: 2-slice wave tiles, sc1 nt payload stores at >= 64 MiB)",
             },
-            "self_check": ok,
-            "self_check_detail": {"what": check_note, "buckets_checked_min_over_ranks": checked},
+            "self_check": hl["ok"],
+            "self_check_detail": {"what": hl["check_note"], "buckets_checked_min_over_ranks": hl["checked"]},
         }
         if nb > 1:
             line["roofline"]["note"] = (f"steps cycle {nb} distinct buckets + planes ({nb * (8 * N + B) >> 20} MiB "
@@ -542,10 +451,14 @@ def main():
         if "frac" in side.get("resident", {}):
             line["roofline"]["frac_resident"] = side["resident"]["frac"]
             line["roofline"]["traffic_resident"] = load_traffic(args.numel, P, "quantize_pack")
-        readings = weak_readings(side.get("weak_256MiB_per_gpu", {}), world)
-        if readings:
-            line["config"]["readings"] = readings.pop("readings")
-            line.update(readings)
+        rd = readings(hl, st, world, nb, P)
+        line["config"]["readings"] = rd.pop("readings")
+        line.update(rd)
+        line["value"] = rd["weak_256MiB_value"]     # the same number, by construction
+        if st is not None and rehearse:
+            line["strong_1GiB"]["rehearsal_note"] = REHEARSAL_NOTE
+        if rehearse:
+            line["rehearsal_note"] = ("value / weak_256MiB_value / strong_1GiB_value: " + REHEARSAL_NOTE)
         line.update(fields)
         if side:
             line["side"] = side
@@ -590,9 +503,7 @@ def main():
         else:
             guarded("cold_hbm", lambda: bucket_measure(sw, torch, args.numel, P, stream, nbuf=4))
         guarded("copy_ceiling", lambda: copy_ceiling(sw, torch, args.numel, stream, nbuf=nb, k1_ms=kern_ms_max))
-        guarded("configs3_1gpu", lambda: job_measure(sw, torch, CFG3_JOB_NUMEL, P, stream, dev))
     if world > 1 and not args.no_side:
-        guarded("weak_256MiB_per_gpu", lambda: weak_measure(sw, torch, dist, args.numel, P, stream, dev, world))
         if rank == 0:
             # what the peer-to-peer paths rely on: every pair of the node's GPUs can map each other
             guarded("topology", lambda: {
@@ -601,7 +512,8 @@ def main():
                                 for i in range(ndev)]})
     if world > 1 and args.switch_numel:
         try:
-            fields.update(exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev))
+            fields.update(exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev,
+                                           rehearsal=pg["rehearsal"]))
         except Exception as e:  # noqa: BLE001 - recorded as a diagnostic failure below
             fields["switchsim"] = {"error": repr(e)[:400]}
         fatal, diag = switch_verdicts(fields, lenient=args.lenient_switch)
@@ -613,6 +525,10 @@ def main():
         # is the in-node switch (a real cross-rank SwitchML all-reduce)
         try:
             fields["configs4_plugin"] = plugin_measure_ranks(torch, dist, dev, world)
+            if rehearse:
+                fields["configs4_plugin"]["rehearsal_note"] = (
+                    "rehearsal: the N ranks' plugins share one GPU (peer planes in the same HBM, no xGMI); "
+                    "times are not an N-GPU measurement")
             if not fields["configs4_plugin"]["placements_agree_all_ranks"]:
                 diag_failures.append("configs4_plugin: device and pinned-host results differ")
         except Exception as e:  # noqa: BLE001
@@ -642,26 +558,167 @@ def main():
         sys.exit(1)
 
 
-def weak_readings(wk, world):
-    """The N > 1 line's two readings, both named: `value` is
-    configs[3]'s 1 GiB job strong-scaled over the N GPUs; `weak_256MiB_value`
-    (with its own roofline) the metric's 256 MiB bucket on EVERY GPU.  `wk` is
-    weak_measure's result; {} at N = 1 or when it did not run."""
-    if world <= 1 or "value_GBps" not in wk:
-        return {}
+REHEARSAL_NOTE = ("rehearsal: the ranks share ONE GPU (SML_BENCH_REHEARSE), so these rates are one device's "
+                  "throughput split between the ranks, not N GPUs'; never a measurement of the N-GPU node")
+
+
+def k1_reading(sw, torch, dist, world, rank, dev, stream, job_numel, numel, P, nb, steps, warmup, settle_ms,
+               graph_steps=1):
+    """One timed K1 reading on every rank.
+
+    job_numel = 0: every rank quantizes its own `numel`-element buckets (the
+    weak reading: the same per-GPU work at every N).  job_numel > 0: ONE job
+    of that many elements split over the ranks by the FIFO rule
+    (fifo_scheduler.cc:93-109, slice g -> GPU g: the strong reading).  Either
+    way `nb` distinct buckets + planes are cycled step after step (past the
+    256 MiB Infinity Cache: HBM proper), bucket b = elements [off, off + N) of
+    bench_bucket(4242 + b, .) — integer-exact, so the planes the TIMED
+    launches leave are hashed afterwards and compared with the oracle's
+    digests (tests/golden/digests_bench.json).
+
+    Timed region: `steps` back-to-back launches on `stream`, bracketed by a
+    barrier and a device sync on both sides (wall clock -> value; MAX over
+    ranks) and by two HIP events on the launch stream itself (-> average
+    launch duration for the roofline; includes the inter-launch gaps, so it
+    is conservative against rocprofv3's per-dispatch durations)."""
+    off = 0
+    if job_numel:
+        off, N = sw.fifo_slice(job_numel, world, rank)
+        total_alg = sum(8 * n + sw.num_blocks(n, P)
+                        for n in (sw.fifo_slice(job_numel, world, r)[1] for r in range(world)))
+    else:
+        N = numel
+        total_alg = world * (8 * N + sw.num_blocks(N, P))
+    B = sw.num_blocks(N, P)
+    xs = [bench_bucket(torch, BENCH_SEED0 + b, off, N, dev) for b in range(nb)]
+    pls = [torch.empty(B * P, dtype=torch.int32, device=dev) for _ in range(nb)]
+    exs = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nb)]
+    cyc = [0]
+    # one prepared C call per step (arguments checked once: the first step's
+    # launch is not delayed by the Python wrapper)
+    launchers = [sw.quantize_pack_launcher(xs[i], P, 1, pls[i], exps_out=exs[i], stream=stream) for i in range(nb)]
+
+    def launch():
+        i = cyc[0]
+        cyc[0] = (i + 1) % nb
+        launchers[i]()
+
+    step, per_call = launch, 1
+    if graph_steps > 1:
+        # G consecutive steps captured into one hipGraph (G kernel nodes);
+        # each replay still runs exactly G full steps.  The captured steps
+        # cycle the buckets from bucket 0, so every replay covers every
+        # bucket only when G is a multiple of their number.
+        if graph_steps % nb:
+            sys.exit(f"bench.py: --graph-steps {graph_steps} must be a multiple of --buckets {nb} "
+                     "(each replay repeats the same captured steps)")
+        if steps % graph_steps or warmup % graph_steps:
+            sys.exit("bench.py: --steps and --warmup must be multiples of --graph-steps")
+        launch()
+        torch.cuda.synchronize()
+        cyc[0] = 0
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            for _ in range(graph_steps):
+                launch()
+        step, per_call = graph.replay, graph_steps
+
+    settle(step, settle_ms)
+    for _ in range(warmup // per_call):
+        step()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # one untimed pass through the timing code itself (events, syncs,
+    # barriers), so lazy first-use costs of those calls stay out of the region
+    for _ in range(2):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        step()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        _ = ev0.elapsed_time(ev1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps // per_call):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    # The closing barrier brackets the region but its own latency (a
+    # collective, tens of us at N = 8) is not a step: each rank stops its
+    # clock at its device sync and the MAX over ranks below is the job's time.
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    kern_ms = ev0.elapsed_time(ev1) / steps
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms_max = float(t[0]), float(t[1])
+
+    # self-check: the planes the TIMED launches left (the last launch on each
+    # bucket, the kernel instance and knobs of this run) against the oracle's digests
+    want = expected_digests(job_numel, world, rank, N, P, nb)
+    if want is None:
+        ok, check_note, checked = True, "no committed digest for this shape: not checked", 0
+    else:
+        got = [planes_sha256(torch, exs[b], pls[b], N, P) for b in range(nb)]
+        bad = [b for b in range(nb) if got[b] != want[b]]
+        ok, checked = not bad, nb
+        check_note = ("timed exponent + BE payload planes of every bucket == tests/golden/digests_bench.json"
+                      if ok else f"buckets {bad} differ from tests/golden/digests_bench.json")
+    ok_t = torch.tensor([int(ok), checked], dtype=torch.int32, device=dev)
+    if world > 1:
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+    del xs, pls, exs, launchers
+    return {"name": "strong_1GiB" if job_numel else "weak_256MiB", "job_numel": job_numel or world * N,
+            "numel_per_gpu": N, "num_blocks_per_gpu": B, "alg_bytes_per_gpu": 8 * N + B, "total_alg": total_alg,
+            "steps": steps, "warmup": warmup, "elapsed_s": elapsed, "kernel_ms": kern_ms_max,
+            "ok": bool(ok_t[0].item()), "checked": int(ok_t[1].item()), "check_note": check_note}
+
+
+def reading_block(r, world, nb, P, scaling):
+    """A reading's own sub-object: rate, scaling, timing, self-check and its
+    roofline (algorithmic bytes of rank 0's slice / HIP-event kernel time, max
+    over ranks; PMC traffic from profiles/pmc_traffic.json at that size)."""
+    ms = r["elapsed_s"] * 1e3 / r["steps"]
+    ach = r["alg_bytes_per_gpu"] / (r["kernel_ms"] * 1e-3) / 1e9
     return {
-        "weak_256MiB_value": wk["value_GBps"],
-        "weak_256MiB": {
-            "value": wk["value_GBps"], "unit": "GB/s", "scaling": "weak", "n_gpus": world,
-            "ms_per_step": wk["ms_per_step"], "numel_per_gpu": wk["numel_per_gpu"],
-            "buckets_cycled": wk["buckets"],
-            "roofline": {"bound": "hbm", "achieved": wk["kernel_GBps_per_gpu"], "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": wk["frac_per_gpu"],
-                         "note": "per GPU: algorithmic bytes / HIP-event kernel time, max over ranks"}},
-        "readings": {
-            "value": "strong scaling: configs[3]'s one 1 GiB job split over the N GPUs",
-            "weak_256MiB_value": "weak scaling: every GPU quantizes its own 256 MiB buckets (4 cycled)"},
+        "value": round(r["total_alg"] / (ms * 1e-3) / 1e9, 2), "unit": "GB/s", "scaling": scaling,
+        "n_gpus": world, "job_numel": r["job_numel"], "numel_per_gpu": r["numel_per_gpu"],
+        "buckets_cycled": nb, "steps": r["steps"], "warmup": r["warmup"], "ms_per_step": round(ms, 5),
+        "kernel_ms": round(r["kernel_ms"], 5),
+        "self_check": r["ok"], "buckets_checked_min_over_ranks": r["checked"],
+        "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBPS, 4),
+                     "traffic": load_traffic(r["numel_per_gpu"], P, "quantize_pack" if nb == 1 else "quantize_pack_cold"),
+                     "note": "per GPU: algorithmic bytes of rank 0's slice / HIP-event kernel time, max over ranks"},
     }
+
+
+def readings(hl, st, world, nb, P=256):
+    """The two named readings every line carries at every N,
+    so a 1/2/4/8 curve compares each reading with ITSELF at N = 1:
+      weak_256MiB_value   256 MiB buckets on EVERY GPU (4 cycled) — `value`
+      strong_1GiB_value   configs[3]'s 1 GiB job split over the N GPUs (at
+                          N = 1 the whole job on one GPU)
+    `hl` / `st` are k1_reading results (st None: the strong reading skipped)."""
+    out = {"weak_256MiB_value": None, "weak_256MiB": reading_block(hl, world, nb, P, "weak"),
+           "readings": {
+               "value": "= weak_256MiB_value (the same reading at every N; scaling weak)",
+               "weak_256MiB_value": "weak scaling: every GPU quantizes its own 256 MiB buckets (4 cycled)",
+               "strong_1GiB_value": "strong scaling: configs[3]'s one 1 GiB job split over the N GPUs "
+                                    "(FIFO rule; the whole job on one GPU at N = 1)"}}
+    out["weak_256MiB_value"] = out["weak_256MiB"]["value"]
+    out["strong_1GiB_value"] = None
+    if st is not None:
+        out["strong_1GiB"] = reading_block(st, world, nb, P, "strong")
+        out["strong_1GiB_value"] = out["strong_1GiB"]["value"]
+    return out
 
 
 SWITCH_PATHS = ("switchsim", "p2p_switch", "xgmi_switch", "xgmi_switch_push")
@@ -808,71 +865,7 @@ def copy_ceiling(sw, torch, N, stream, nbuf=4, reps=200, k1_ms=None):
     return out
 
 
-def job_measure(sw, torch, job_numel, P, stream, dev, reps=50):
-    """configs[3] on ONE GPU: the whole 1 GiB job (T = 1 slice) through K1 —
-    the single-GPU point of the strong-scaling curve the N > 1 runs report."""
-    B = sw.num_blocks(job_numel, P)
-    g = torch.Generator(device=dev)
-    g.manual_seed(42)
-    x = torch.randn(job_numel, device=dev, generator=g)
-    pl = torch.empty(B * P, dtype=torch.int32, device=dev)
-    ex = torch.empty(B, dtype=torch.int8, device=dev)
-    fn = lambda: sw.quantize_pack(x, P, 1, payload=pl, exps_out=ex, stream=stream)  # noqa: E731
-    settle(fn, 20.0)
-    t = time_launches(torch, fn, stream, reps)
-    alg = 8 * job_numel + B
-    return {"job_numel": job_numel, "kernel_ms": round(t * 1e3, 4), "value_GBps": round(alg / t / 1e9, 1),
-            "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4)}
-
-
-def weak_measure(sw, torch, dist, N, P, stream, dev, world, reps=200, nbuf=4):
-    """Weak scaling beside the strong-scaling headline at N > 1: every rank
-    runs K1 over its own N-element buckets (the metric's 256 MiB per GPU, as
-    at N = 1), the steps cycling `nbuf` distinct buckets + planes like the
-    headline (HBM proper), launches bracketed by a barrier and a device sync;
-    aggregate = world x (8N + B) / max-over-ranks time per step.  The kernel
-    time (HIP events on the launch stream, max over ranks) gives the per-GPU
-    roofline fraction."""
-    B = sw.num_blocks(N, P)
-    g = torch.Generator(device=dev)
-    g.manual_seed(4343 + dist.get_rank())
-    xs = [torch.randn(N, device=dev, generator=g) for _ in range(nbuf)]
-    pls = [torch.empty(B * P, dtype=torch.int32, device=dev) for _ in range(nbuf)]
-    exs = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nbuf)]
-    i = [0]
-
-    def fn():
-        k = i[0]
-        i[0] = (k + 1) % nbuf
-        sw.quantize_pack(xs[k], P, 1, payload=pls[k], exps_out=exs[k], stream=stream)
-
-    settle(fn, 30.0)
-    for _ in range(20):
-        fn()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(reps):
-        fn()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0          # the closing barrier is not a step (see main)
-    dist.barrier()
-    t = torch.tensor([el / reps, ev0.elapsed_time(ev1) * 1e-3 / reps], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    t, tk = float(t[0]), float(t[1])
-    alg = 8 * N + B
-    return {"numel_per_gpu": N, "buckets": nbuf, "ms_per_step": round(t * 1e3, 5),
-            "value_GBps": round(world * alg / t / 1e9, 1), "per_gpu_GBps": round(alg / t / 1e9, 1),
-            "kernel_ms": round(tk * 1e3, 5), "kernel_GBps_per_gpu": round(alg / tk / 1e9, 1),
-            "frac_per_gpu": round(alg / tk / 1e9 / HBM_PEAK_GBPS, 4),
-            "note": "every GPU quantizes its own 256 MiB buckets, 4 cycled (weak scaling); the headline "
-                    "shards one 1 GiB job (strong scaling, configs[3])"}
-
-
-def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
+def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5, rehearsal=None):
     """The switch simulation with W = world real workers, each holding its
     own n-element fp32 bucket (distinct per rank).  Two exchange paths:
       switchsim   ring all-reduces (RCCL) of the int8 exponents (MAX) and the
@@ -1056,6 +1049,27 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5):
                                  and (name == "switchsim" or same))
         r["xgmi_link_GBps_assumed"] = XGMI_LINK_GBPS
     res["p2p_switch"]["status"] = "experimental (first cross-GPU run is the driver's multi-GPU bench)"
+    label_rehearsal(res, rehearsal)
+    return res
+
+
+def label_rehearsal(res, rehearsal):
+    """Fields a rehearsal (ranks sharing one GPU) cannot measure, marked so
+    (VERDICT r5 #3): no xGMI link is crossed, so `frac_of_xgmi_bound` is
+    null; the collectives ran over the SwitchML library's TCP net (or gloo),
+    so rates and `phases_ms` time that net, not xGMI.  No-op on a node."""
+    if not rehearsal:
+        return res
+    for k, r in res.items():
+        if not isinstance(r, dict) or "error" in r:
+            continue
+        if "frac_of_xgmi_bound" in r:
+            r["frac_of_xgmi_bound"] = None
+        r["rehearsal_note"] = ("rehearsal (" + rehearsal + "): no xGMI link was crossed, so frac_of_xgmi_bound is "
+                               "null; ms / GB/s time one shared GPU and, for the collectives, the TCP net")
+        if "phases_ms" in r:
+            r["phases_note"] = ("rehearsal: the all_reduce / all_gather phases ran over the SwitchML TCP net "
+                                "between ranks on one GPU, not xGMI")
     return res
 
 

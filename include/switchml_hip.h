@@ -426,10 +426,15 @@ sml_status_t sml_narrow_i32_u8(const int32_t* d_in, uint8_t* d_out, uint64_t n, 
  * (rdma_worker_thread.cc:341-356; PreprocessSingle writes byte 2).  Message
  * m in [0, B + b) carries exps[m] for m < B; the byte is 0 for m >= B.
  * d_imm: uint32[B + b] (host byte order, as ibv_send_wr.imm_data is filled).
- * d_exps null: an INT32 slice — B messages (no extra batch, ppp.cc:65-67),
- * imm = msg_id & 0xFFFF (the INT32 PreprocessSingle leaves byte 2 alone). */
+ * d_exps must not be null (SML_ERR_INVALID_ARG): an INT32 slice has its own
+ * entry point below. */
 sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t num_blocks, uint32_t batch_max,
                           uint32_t* d_imm, void* stream);
+
+/* An INT32 slice's immediates: B messages (no extra batch, ppp.cc:65-67),
+ * imm = msg_id & 0xFFFF (the INT32 PreprocessSingle leaves byte 2 alone).
+ * d_imm: uint32[B]. */
+sml_status_t sml_rdma_imm_int32(uint64_t num_blocks, uint32_t* d_imm, void* stream);
 
 /* Measurement probe (not part of the PPP): copy `bytes` (a multiple of 4 KiB,
  * 16-B aligned buffers) with the quantize kernel's tile shape (K1's slices
@@ -438,6 +443,13 @@ sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t num_blocks, uint32_t ba
  * policy sml_quantize_pack uses for an output plane of `bytes`) — the
  * practical HBM ceiling bench.py reports. */
 sml_status_t sml_stream_copy(const void* d_in, void* d_out, uint64_t bytes, void* stream);
+
+/* Fault injection for tests (not part of the PPP): one small kernel that
+ * keeps `stream` busy for `microseconds` of the device's wall clock (at most
+ * 60 s; SML_ERR_INVALID_ARG above) and then ends on its own — a device that
+ * does not finish within a caller's timeout (backend.dummy.stall_worker_thread
+ * uses it to exercise the in-node switch's bounded waits), never a hang. */
+sml_status_t sml_debug_stall(uint32_t microseconds, void* stream);
 
 /* Launch-geometry knob for experiments: workgroups per launch for the
  * streaming kernels (0 = one 256-thread workgroup per 4 tiles of 1024

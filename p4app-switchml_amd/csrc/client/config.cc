@@ -72,6 +72,8 @@ bool Config::LoadFromString(const std::string& ini) {
         else if (full == "backend.dummy.bandwidth") backend_.dummy.bandwidth = std::stof(val);
         else if (full == "backend.dummy.process_packets") backend_.dummy.process_packets = parse_bool(val);
         else if (full == "backend.dummy.fail_worker_thread") backend_.dummy.fail_worker_thread = std::stoi(val);
+        else if (full == "backend.dummy.stall_worker_thread") backend_.dummy.stall_worker_thread = std::stoi(val);
+        else if (full == "backend.dummy.stall_ms") backend_.dummy.stall_ms = parse_uint<uint32_t>(full, val, 60000ull);
         else if (full == "backend.hip.device") backend_.hip.device = std::stoi(val);
         else if (full == "backend.xgmi.session") backend_.xgmi.session = val;
         else if (full == "backend.xgmi.max_slice_numel") backend_.xgmi.max_slice_numel = parse_uint<uint64_t>(full, val, ~0ull);
@@ -157,6 +159,8 @@ std::string Config::ToString() const {
       << "\n\n[backend.dummy]\nbandwidth = " << backend_.dummy.bandwidth
       << "\nprocess_packets = " << (backend_.dummy.process_packets ? "true" : "false")
       << "\nfail_worker_thread = " << backend_.dummy.fail_worker_thread
+      << "\nstall_worker_thread = " << backend_.dummy.stall_worker_thread
+      << "\nstall_ms = " << backend_.dummy.stall_ms
       << "\n\n[backend.hip]\ndevice = " << backend_.hip.device << "\nmode = " << backend_.hip.mode
       << "\npacket_ring = " << backend_.hip.packet_ring
       << "\nburst_server = " << (backend_.hip.burst_server ? "true" : "false")

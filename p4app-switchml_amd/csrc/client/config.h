@@ -33,6 +33,12 @@ struct DummyBackendConfig {
     // P4 drop simulator, controller/drop_simulator.py): the worker thread with
     // this id fails every slice it is handed without touching the buffers.
     int fail_worker_thread = -1;
+    // Fault injection for tests: before each slice it is handed, the worker
+    // thread with id stall_worker_thread queues a kernel that keeps its stream
+    // busy for stall_ms (sml_debug_stall; at most 60000) — a device that does
+    // not finish within backend.xgmi.timeout_ms, which ends on its own.
+    int stall_worker_thread = -1;
+    uint32_t stall_ms = 0;
 };
 
 // MI355X-specific knobs of the loopback backend.

@@ -28,6 +28,7 @@ HipExponentQuantizerPPP::HipExponentQuantizerPPP(Config& config, WorkerTid worke
 
 HipExponentQuantizerPPP::~HipExponentQuantizerPPP() {
     job_slice_ = nullptr;
+    if (abandoned_) return;   // Abandon(): nothing here may wait on the stream's unfinished work
     if (server_) (void)sml_burst_server_destroy(server_);   // no throwing from a destructor
     if (d_recv_exps_) (void)hipFreeAsync(d_recv_exps_, stream_);   // stream-ordered allocation
     if (d_stage_) (void)hipFree(d_stage_);

@@ -65,6 +65,11 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     void PostprocessBulk(const void* payload_plane, const void* global_exps, bool payload_le) override;
 
     hipStream_t stream() const { return stream_; }
+    // Work on stream() did not finish within a bounded wait (the in-node
+    // switch's timeout) and may never: the destructor then leaks the stream
+    // and the device buffers instead of freeing them (hipFree /
+    // hipStreamDestroy would wait on that work).
+    void Abandon() { abandoned_ = true; }
     uint64_t total_main_num_ltus() const { return total_main_num_ltus_; }
     uint64_t batch_num_ltus() const { return batch_num_ltus_; }
     Numel ltu_numel() const { return ltu_numel_; }
@@ -90,6 +95,7 @@ class HipExponentQuantizerPPP : public PrePostProcessor {
     int32_t* d_stage_ = nullptr;
     int8_t* d_stage_exp_ = nullptr;
     bool stream_ordered_ = false;
+    bool abandoned_ = false;
     bool per_ltu_calls_ = true;
     // SML_FLAG_ROUND_RNE when backend.hip.vcl (the reference's VCL=1 build's
     // rounding), else 0: or'ed into every quantizing launch

@@ -55,6 +55,7 @@ struct DeviceBuffer {
     void* p = nullptr;
     size_t cap = 0;
     hipStream_t owner = nullptr;
+    void Abandon() { p = nullptr; cap = 0; }   // the owner stream is wedged: leak, never free
     void* get(size_t bytes, hipStream_t st) {
         if (bytes > cap) {
             if (p) hip_ok(hipFreeAsync(p, owner), "hipFreeAsync");
@@ -98,6 +99,13 @@ struct HostBuffer {
 struct WorkerState {
     DeviceBuffer in, out, payload, exps, ring, ring_extra;
     HostBuffer hring, hring_extra;
+    // the worker's stream is wedged (XgmiSwitch::Wedged): its unfinished work
+    // may still use these buffers, so they are leaked, not freed
+    void Abandon() {
+        for (DeviceBuffer* b : {&in, &out, &payload, &exps, &ring, &ring_extra}) b->Abandon();
+        hring.p = hring_extra.p = nullptr;
+        hring.cap = hring_extra.cap = 0;
+    }
 };
 
 // DummyWorkerThread's per-packet loop (dummy_worker_thread.cc:86-177) with
@@ -566,6 +574,10 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
     WorkerState ws;
     JobSlice js;
     uint64_t last_seq = 0;  // sched_seq of the last job this thread took a slice of
+    // this worker's stream did not finish within the in-node switch's bounded
+    // wait: every later slice fails at once, nothing waits on the stream again
+    bool wedged = false;
+    const DummyBackendConfig& dummy = config_.backend_.dummy;
     while (context_.GetContextState() == Context::RUNNING) {
         while (!inflight.empty() && hipEventQuery(inflight.front().ev) != hipErrorNotReady) retire(true);
         if (!inflight.empty() && (inflight.size() >= kMaxInFlight || !context_.HasJobAfter(last_seq))) {
@@ -587,9 +599,12 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
             // worker (as a real mid-exchange failure does), not a barrier wait
             if (xgmi_) xgmi_->Poison();
         }
+        if (work && wedged) ok = false;
         uint64_t packets = 0;
         if (ok && work) {
             try {
+                if (hip_ppp && tid == dummy.stall_worker_thread && dummy.stall_ms > 0)   // injected stall
+                    sml_ok(sml_debug_stall(dummy.stall_ms * 1000u, hip_ppp->stream()), "sml_debug_stall");
                 packets = run_slice(*ppp, config_, ws, js, xgmi_.get(), tid);
                 if (hip_ppp && bw <= 0) {
                     if (events.empty()) {
@@ -608,7 +623,21 @@ void LoopbackBackend::WorkerMain(WorkerTid tid) {
             } catch (const std::exception& e) {
                 fprintf(stderr, "[switchml] worker thread %d: job %llu failed: %s\n", tid,
                         (unsigned long long)js.job->id_, e.what());
-                if (hip_ppp) (void)hipStreamSynchronize(hip_ppp->stream());  // nothing may still touch the buffers
+                // nothing may still touch the buffers when the slice is
+                // published FAILED.  With the in-node switch the wait is
+                // bounded (backend.xgmi.timeout_ms): a device that does not
+                // finish fails the slice now, and the worker, its stream and
+                // buffers are abandoned rather than blocking here forever.
+                if (hip_ppp && xgmi_) {
+                    if (xgmi_->Wedged() || !xgmi_->WaitBounded(hip_ppp->stream())) {
+                        wedged = true;
+                        hip_ppp->Abandon();   // its stream stays alive: the switch's reaper waits on it
+                        ws.Abandon();
+                        xgmi_->NoteStuckStream(tid, hip_ppp->stream());
+                    }
+                } else if (hip_ppp) {
+                    (void)hipStreamSynchronize(hip_ppp->stream());
+                }
                 ok = false;
             }
             if (ok && bw > 0) {  // the dummy backend's simulated wire time (dummy_backend.cc:124-133)

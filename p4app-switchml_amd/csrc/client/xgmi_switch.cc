@@ -10,6 +10,9 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <cstdio>
 #include <cstring>
 #include <thread>
 
@@ -33,6 +36,12 @@ void sml_ok(int s, const char* what) {
         throw SwitchMLFatal(std::string("xgmi switch: ") + what + ": " + sml_status_string((sml_status_t)s) + " " +
                             sml_last_error());
 }
+
+// Reapers of wedged switches (XgmiSwitch::Wedged): how many are still
+// waiting for their streams to drain before they free what they hold.
+std::mutex g_reap_mu;
+std::condition_variable g_reap_cv;
+int g_reaping = 0;
 
 }  // namespace
 
@@ -169,6 +178,15 @@ XgmiSwitch::XgmiSwitch(const Config& config, int device) {
 
 void XgmiSwitch::Setup(int device) {
     hip_ok(hipSetDevice(device), "hipSetDevice");
+    device_ = device;
+    {
+        // an earlier switch of this process that wedged still holds peer
+        // mappings until its streams drain: wait for its reaper (bounded)
+        std::unique_lock<std::mutex> lk(g_reap_mu);
+        if (!g_reap_cv.wait_for(lk, std::chrono::milliseconds(timeout_ms_), [] { return g_reaping == 0; }))
+            throw SwitchMLFatal("xgmi switch: an earlier session's device work has not finished (its planes and "
+                                "peer mappings are still held); restart the process");
+    }
     OpenSegment();
     if (shm_->attached.fetch_add(1) >= (uint32_t)W_)
         throw SwitchMLFatal("xgmi switch: session " + name_ + " already has num_workers workers");
@@ -235,6 +253,44 @@ void XgmiSwitch::Setup(int device) {
 // Everything this worker holds, in reverse order of Setup; safe on a
 // partially built instance.
 void XgmiSwitch::Release() {
+    if (Wedged() && (!planes_.empty() || !opened_.empty())) {
+        // device work that has not finished may still use the planes, the
+        // peer mappings and the streams: a detached reaper frees them once
+        // every stream involved has drained (never, if the device is hung)
+        fprintf(stderr, "[switchml] xgmi switch: device work did not finish; %zu planes and %zu peer mappings "
+                        "are freed once it does\n", planes_.size() * 4, opened_.size());
+        struct Remains {
+            std::vector<ThreadPlanes> planes;
+            std::vector<void*> opened;
+            int device;
+        };
+        auto* rem = new Remains{std::move(planes_), std::move(opened_), device_};
+        planes_.clear();
+        opened_.clear();
+        {
+            std::lock_guard<std::mutex> lk(g_reap_mu);
+            g_reaping++;
+        }
+        std::thread([rem] {
+            (void)hipSetDevice(rem->device);
+            for (ThreadPlanes& tp : rem->planes) {
+                if (tp.stuck) (void)hipStreamSynchronize(tp.stuck);
+                if (tp.xst) (void)hipStreamSynchronize(tp.xst);
+            }
+            for (void* p : rem->opened) (void)hipIpcCloseMemHandle(p);
+            for (ThreadPlanes& tp : rem->planes) {
+                (void)hipFree(tp.exps);
+                (void)hipFree(tp.payload);
+                (void)hipFree(tp.out);
+                (void)hipFree(tp.gexp);
+                if (tp.xst) (void)hipStreamDestroy(tp.xst);
+            }
+            delete rem;
+            std::lock_guard<std::mutex> lk(g_reap_mu);
+            g_reaping--;
+            g_reap_cv.notify_all();
+        }).detach();
+    }
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
     opened_.clear();
     for (ThreadPlanes& tp : planes_) {
@@ -258,6 +314,7 @@ void XgmiSwitch::Release() {
 
 XgmiSwitch::~XgmiSwitch() {
     if (!shm_) return;
+    if (Wedged()) Poison();   // the peers must not wait for this worker's teardown barriers
     if (!shm_->poisoned.load()) {
         try {
             Barrier(kMaxT);   // nobody reads a peer's planes any more
@@ -271,6 +328,10 @@ XgmiSwitch::~XgmiSwitch() {
         }
     }
     Release();
+}
+
+void XgmiSwitch::NoteStuckStream(int tid, hipStream_t st) {
+    if (tid >= 0 && tid < (int)planes_.size()) planes_[tid].stuck = st;
 }
 
 void XgmiSwitch::Poison() {
@@ -316,12 +377,14 @@ bool XgmiSwitch::StreamSync(hipStream_t st, bool bounded_only) {
         const hipError_t q = hipStreamQuery(st);
         if (q == hipSuccess) return true;
         if (q != hipErrorNotReady) {
+            wedged_.store(true, std::memory_order_release);   // a failed stream: its work's state is unknown
             if (bounded_only) return false;
             hip_ok(q, "hipStreamQuery");
         }
         if (spins > 256) {
             std::this_thread::yield();
             if ((spins & 1023) == 0 && std::chrono::steady_clock::now() > deadline) {
+                wedged_.store(true, std::memory_order_release);
                 if (bounded_only) return false;
                 throw SwitchMLFatal("xgmi switch: device work did not finish within backend.xgmi.timeout_ms");
             }
@@ -509,6 +572,7 @@ void XgmiSwitch::IntChunk(int tid, const int32_t* in, int32_t* out, uint64_t n, 
 void XgmiSwitch::AllReduceSlice(int tid, const void* in, void* out, uint64_t numel, DataType type, hipStream_t st) {
     if (tid < 0 || tid >= T_) throw SwitchMLFatal("xgmi switch: bad worker thread id");
     if (numel == 0) return;
+    if (Wedged()) throw SwitchMLFatal("xgmi switch: an earlier slice's device work did not finish");
     if (shm_->poisoned.load(std::memory_order_acquire))
         throw SwitchMLFatal("xgmi switch: the session failed on another worker");
     try {
@@ -525,8 +589,11 @@ void XgmiSwitch::AllReduceSlice(int tid, const void* in, void* out, uint64_t num
         // fail the session for everyone rather than let a barrier pair
         // different phases
         Poison();
-        (void)StreamSync(st, true);
-        (void)StreamSync(planes_[tid].xst, true);
+        // nothing may still touch the planes when the slice is reported
+        // failed — unless a wait already timed out (wedged): then waiting
+        // again would only add timeout_ms per stream
+        if (!Wedged()) (void)StreamSync(st, true);
+        if (!Wedged()) (void)StreamSync(planes_[tid].xst, true);
         throw;
     }
 }

@@ -48,6 +48,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -82,6 +83,27 @@ class XgmiSwitch {
     // (backend.dummy.fail_worker_thread) calls it too.
     void Poison();
 
+    // Wait for the work queued on a worker's stream for at most
+    // backend.xgmi.timeout_ms; never throws.  False: the device did not
+    // finish (or failed) — the switch is then wedged.
+    bool WaitBounded(hipStream_t st) { return StreamSync(st, true); }
+    // A wait on this worker's device work timed out: kernels of this switch
+    // may still be reading or writing its planes (or a peer's, over xGMI),
+    // and they may never finish.  Nothing on the worker threads waits on
+    // that device work again: the failing slices return at once, and
+    // teardown hands the planes, peer mappings and streams to a detached
+    // reaper thread that frees them only once the stuck streams have
+    // drained (hipFree / hipStreamDestroy / hipIpcCloseMemHandle under
+    // running kernels would block, or pull memory from under them).  A new
+    // switch in the same process first waits (bounded) for earlier reapers:
+    // a peer mapping still open from a wedged session could otherwise alias
+    // a peer's new plane.
+    bool Wedged() const { return wedged_.load(std::memory_order_acquire); }
+    // Worker thread `tid`'s stream `st` (the caller's, not the switch's) was
+    // abandoned with work still queued: the reaper waits for it too.  The
+    // caller keeps the stream alive (never destroys it).
+    void NoteStuckStream(int tid, hipStream_t st);
+
   private:
     struct ThreadPlanes {
         int8_t* exps = nullptr;        // own planes (IPC-exported)
@@ -95,6 +117,7 @@ class XgmiSwitch {
         std::vector<const int32_t*> peer_payload;  // [W]
         std::vector<const float*> peer_out;        // [W]
         hipStream_t xst = nullptr;     // the exchange stream (K6, gather) beside the caller's
+        hipStream_t stuck = nullptr;   // the caller's stream, abandoned with work queued (NoteStuckStream)
     };
 
     void OpenSegment();
@@ -113,6 +136,7 @@ class XgmiSwitch {
     void PushShard(ThreadPlanes& tp, uint64_t n, uint64_t B, uint64_t S, hipStream_t st);
 
     int rank_, W_, T_;
+    int device_ = -1;
     uint32_t P_;
     uint64_t cap_;          // elements per chunk (multiple of 1024)
     uint64_t timeout_ms_;
@@ -124,6 +148,7 @@ class XgmiSwitch {
     bool attached_ = false;   // counted in shm_->attached
     std::vector<ThreadPlanes> planes_;
     std::vector<void*> opened_;  // peer mappings to close
+    std::atomic<bool> wedged_{false};
 };
 
 }  // namespace switchml

@@ -396,6 +396,15 @@ __global__ __launch_bounds__(kBlockThreads) void k_rdma_imm(const int8_t* exps, 
     }
 }
 
+// Fault injection (sml_debug_stall): one wave that occupies its stream for
+// `ticks` of the constant-rate wall clock, then exits — a kernel that does
+// not finish within a caller's timeout, yet always ends on its own.
+constexpr uint32_t kMaxStallMicros = 60u * 1000u * 1000u;
+__global__ __launch_bounds__(64) void k_stall(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 __global__ void k_scale_lut(float* lut, uint32_t W) {
     lut[threadIdx.x] = scale_for(W, (int)(int8_t)(uint8_t)threadIdx.x);
 }
@@ -796,10 +805,31 @@ sml_status_t sml_roundtrip_loopback_batch(const sml_slice* slices, uint32_t num_
 
 sml_status_t sml_rdma_imm(const int8_t* d_exps, uint64_t B, uint32_t batch_max, uint32_t* d_imm, void* stream) {
     if (B == 0) return SML_OK;
-    if (!d_imm || (d_exps && batch_max == 0)) return SML_ERR_INVALID_ARG;
-    // d_exps null: an INT32 slice — B messages (no extra batch), byte 2 untouched (0)
-    const uint64_t total = d_exps ? B + (B < batch_max ? B : batch_max) : B;
+    // a FLOAT32 slice needs its exponent plane: a null one is an error, not
+    // an INT32 slice (sml_rdma_imm_int32 is that)
+    if (!d_imm || !d_exps || batch_max == 0) return SML_ERR_INVALID_ARG;
+    const uint64_t total = B + (B < batch_max ? B : batch_max);
     k_rdma_imm<<<grid_for_vec(total), kBlockThreads, 0, (hipStream_t)stream>>>(d_exps, B, total, d_imm);
+    return launch_check();
+}
+
+sml_status_t sml_rdma_imm_int32(uint64_t B, uint32_t* d_imm, void* stream) {
+    if (B == 0) return SML_OK;
+    if (!d_imm) return SML_ERR_INVALID_ARG;
+    // B messages (no extra batch, ppp.cc:65-67), byte 2 untouched (0)
+    k_rdma_imm<<<grid_for_vec(B), kBlockThreads, 0, (hipStream_t)stream>>>(nullptr, B, B, d_imm);
+    return launch_check();
+}
+
+sml_status_t sml_debug_stall(uint32_t microseconds, void* stream) {
+    if (microseconds == 0) return SML_OK;
+    if (microseconds > kMaxStallMicros) return SML_ERR_INVALID_ARG;
+    int dev = 0, khz = 0;
+    sml_status_t s = hip_check(hipGetDevice(&dev));
+    if (s == SML_OK) s = hip_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    if (s != SML_OK) return s;
+    if (khz <= 0) return SML_ERR_HIP;
+    k_stall<<<1, 64, 0, (hipStream_t)stream>>>((uint64_t)microseconds * (uint64_t)khz / 1000u);
     return launch_check();
 }
 

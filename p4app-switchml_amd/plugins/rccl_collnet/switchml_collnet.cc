@@ -102,6 +102,7 @@ struct Request {
     int32_t* dwidened;                    // temp int32 buffer (uint8 case, device buffers)
     sml_collnet::CallKey key;
     bool failed;
+    hipStream_t aux = nullptr;            // aux_stream of dwidened's device (uint8 case, device buffers)
 };
 
 // One submission order for every worker of the in-node switch (job_order.h);
@@ -310,15 +311,42 @@ void pump() {
     }
 }
 
-// The plugin's own stream for the uint8 widen / narrow kernels (created on
-// the calling thread's device at first use; RCCL's proxy thread has it set).
-hipStream_t aux_stream() {
-    static hipStream_t st = nullptr;
-    if (!st && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+// The plugin's own stream for the uint8 widen / narrow kernels and their
+// scratch, one per device: the stream of the device that holds
+// the call's buffers, created on that device at its first use, so a process
+// that drives several GPUs never runs a kernel or an allocation on another
+// device's stream.  Null when the device cannot be determined or the stream
+// cannot be created.
+hipStream_t aux_stream(int dev) {
+    static std::mutex mu;
+    static std::map<int, hipStream_t> streams;
+    if (dev < 0) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = streams.find(dev);
+    if (it != streams.end()) return it->second;
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || (cur != dev && hipSetDevice(dev) != hipSuccess)) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
         (void)hipGetLastError();
         st = nullptr;
     }
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (st) streams[dev] = st;
     return st;
+}
+
+// The device a device buffer lives on (-1: not a device pointer).
+int device_of(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return a.device;
 }
 
 // The device scratch is stream-ordered (hipMallocAsync / hipFreeAsync on the
@@ -328,7 +356,7 @@ hipStream_t aux_stream() {
 void release_widened(Request* r) {
     delete[] r->widened;
     r->widened = nullptr;
-    if (r->dwidened) (void)hipFreeAsync(r->dwidened, aux_stream());
+    if (r->dwidened) (void)hipFreeAsync(r->dwidened, r->aux);
     r->dwidened = nullptr;
 }
 
@@ -354,7 +382,10 @@ ncclResult_t sml_iallreduce(void* coll_comm, void* send, void* recv, int count, 
             if (ds) {
                 // device buffers: widen on the GPU into a device int32 scratch;
                 // the job reads it only after this stream has finished
-                hipStream_t st = aux_stream();
+                hipStream_t st = aux_stream(device_of(send));
+                if (device_of(recv) != device_of(send))   // widened scratch and both buffers on one device
+                    throw std::runtime_error("uint8 send and recv buffers are on different devices");
+                r->aux = st;
                 if (!st || hipMallocAsync(reinterpret_cast<void**>(&r->dwidened), 4ull * (count > 0 ? count : 1), st) !=
                                hipSuccess) {
                     (void)hipGetLastError();
@@ -429,7 +460,7 @@ ncclResult_t sml_test(void* request, int* done, int* size) {
     }
     if (r->dtype == ncclUint8) {   // switchml_plugin.cc:370-378
         if (r->dwidened) {
-            hipStream_t st = aux_stream();
+            hipStream_t st = r->aux;   // the stream of the buffers' device (set at widening)
             const bool ok = sml_narrow_i32_u8(r->dwidened, static_cast<uint8_t*>(r->user_recv), (uint64_t)r->count,
                                               st) == SML_OK &&
                             hipStreamSynchronize(st) == hipSuccess;

@@ -123,6 +123,10 @@ def lib():
     L.sml_stream_copy.argtypes = [vp, vp, u64, vp]
     L.sml_rdma_imm.restype = i32
     L.sml_rdma_imm.argtypes = [vp, u64, u32, vp, vp]
+    L.sml_rdma_imm_int32.restype = i32
+    L.sml_rdma_imm_int32.argtypes = [u64, vp, vp]
+    L.sml_debug_stall.restype = i32
+    L.sml_debug_stall.argtypes = [u32, vp]
     L.sml_frame_bytes.restype = u64
     L.sml_frame_bytes.argtypes = [u32]
     L.sml_rx_state_words.restype = u64
@@ -693,6 +697,12 @@ def unpack_frames_int32(frames, num_frames: int, rx: RxSliceInt32, job_id: int =
     return rx.out
 
 
+def debug_stall(microseconds: int, stream=None):
+    """Fault injection for tests: keep `stream` busy for `microseconds` of
+    device wall-clock time (<= 60 s), then end (sml_debug_stall)."""
+    _check("sml_debug_stall", lib().sml_debug_stall(int(microseconds), _stream(stream)))
+
+
 def rdma_imm(exps, batch_max: int = 64, stream=None, num_blocks_int32: int | None = None, device=None):
     """RDMA immediates of one slice's B + b messages (uint32 in host order, as
     int32 tensor): (msg_id & 0xFFFF) | exponent << 16.  exps=None with
@@ -701,8 +711,8 @@ def rdma_imm(exps, batch_max: int = 64, stream=None, num_blocks_int32: int | Non
     if exps is None:
         B = int(num_blocks_int32)
         out = torch.empty(B, dtype=torch.int32, device=device or "cuda")
-        _check("sml_rdma_imm", lib().sml_rdma_imm(None, B, batch_max, _dev(out, torch.int32, "imm"),
-                                                 _stream(stream, out)))
+        _check("sml_rdma_imm_int32", lib().sml_rdma_imm_int32(B, _dev(out, torch.int32, "imm"),
+                                                             _stream(stream, out)))
         return out
     B = exps.numel()
     out = torch.empty(B + min(B, batch_max), dtype=torch.int32, device=exps.device)

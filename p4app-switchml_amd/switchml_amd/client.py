@@ -63,7 +63,8 @@ def make_config(**kw) -> str:
     general = {k: v for k, v in kw.items() if k in (
         "rank", "num_workers", "num_worker_threads", "max_outstanding_packets", "packet_numel",
         "backend", "scheduler", "prepostprocessor", "instant_job_completion")}
-    dummy = {k: v for k, v in kw.items() if k in ("bandwidth", "process_packets", "fail_worker_thread")}
+    dummy = {k: v for k, v in kw.items() if k in ("bandwidth", "process_packets", "fail_worker_thread",
+                                                  "stall_worker_thread", "stall_ms")}
     hip = {k: v for k, v in kw.items() if k in ("device", "mode", "packet_ring", "burst_server", "batch_jobs",
                                                      "coalesce_us", "vcl")}
     xgmi = {k: v for k, v in kw.items() if k in ("session", "max_slice_numel", "timeout_ms", "push")}

@@ -43,11 +43,22 @@ def main(tag="r02", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
             if "sml::" in r["Name"] or "copyBuffer" in r["Name"]:
                 w.writerow(r)
 
-    # full-workload launches: the largest grid seen for the quantize kernel
+    # the headline's launches: the grid of the 256 MiB bucket (the most
+    # launches: 2000 timed + warmup); other grids (the strong_1GiB reading's
+    # 1 GiB job, 200 timed launches) are summarised apart in per_grid
     q = [r for r in trace if "k_quantize_pack" in r["Kernel_Name"]]
     gsz = lambda r: int(r.get("Grid_Size") or r["Grid_Size_X"])
-    grid = max(gsz(r) for r in q)
-    full = [r for r in q if gsz(r) == grid]
+    by_grid = {}
+    for r in q:
+        by_grid.setdefault(gsz(r), []).append(r)
+    grid = max(by_grid, key=lambda g: len(by_grid[g]))
+    per_grid = []
+    for g, rs in sorted(by_grid.items()):
+        rs = sorted(rs, key=lambda r: int(r["Start_Timestamp"]))
+        d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rs]
+        per_grid.append({"grid_threads": g, "launches": len(d), "avg_duration_ns": statistics.mean(d),
+                         "last_200_avg_duration_ns": statistics.mean(d[-200:])})
+    full = by_grid[grid]
     full.sort(key=lambda r: int(r["Start_Timestamp"]))
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in full]
     timed = durs[-timed_steps:]   # the bench's timed window (the last K full-grid launches)
@@ -93,6 +104,7 @@ def main(tag="r02", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
         "hbm_bytes_per_launch": fetch_b + write_b,
         "traffic_over_algorithmic": (fetch_b + write_b) / (alg_read + alg_write),
         "default_steps": "4 distinct buckets cycled (cold HBM)" if cycling else "one resident bucket",
+        "per_grid": per_grid,
     }
     key = "resident" if cycling else "cold"
     summary[f"{key}_hbm_bytes_per_launch"] = other_b
@@ -121,7 +133,7 @@ def main(tag="r02", numel=64 * 1024 * 1024, packet_numel=256, timed_steps=2000):
 def slice_traffic(src, packet_numel):
     """K1's HBM bytes per launch at configs[3]'s per-GPU FIFO slice sizes
     (run_profiles.sh: slice_<numel>_{fetch,write}, 4 buckets cycled), for the
-    N > 1 lines' roofline.traffic."""
+    strong_1GiB reading's roofline.traffic at N = 1, 2 and 8."""
     out = []
     for d in sorted(os.listdir(src)) if os.path.isdir(src) else []:
         if not (d.startswith("slice_") and d.endswith("_fetch")):

@@ -8,9 +8,11 @@ job holds exactly that slice of the job) and, after the timed region, hashes
 every bucket's exponent plane and big-endian payload plane and compares them
 with these digests, made here by the C oracle:
 
-  bucket_T1   N = 1: 4 buckets (seeds 4242..4245) of 67,108,864 elements
-              (256 MiB), one slice, P = 256, W = 1
-  job_T{G}    N = G > 1: configs[3]'s 1 GiB job (268,435,456 elements) of each
+  bucket_T1   the headline (weak_256MiB) at every N: 4 buckets (seeds
+              4242..4245) of 67,108,864 elements (256 MiB), one slice,
+              P = 256, W = 1 — every GPU holds its own copy of the same 4
+  job_T{G}    the strong_1GiB reading at N = G (G = 1 included: the whole job
+              on one GPU): configs[3]'s 1 GiB job (268,435,456 elements) of each
               seed split by the FIFO rule into G slices (fifo_scheduler.cc:
               93-109); slice g = rank g's bucket
 
@@ -31,7 +33,7 @@ BUCKETS = 4
 P = 256
 BUCKET_NUMEL = 67_108_864
 JOB_NUMEL = 268_435_456
-JOB_SLICES = (2, 4, 8)
+JOB_SLICES = (1, 2, 4, 8)
 
 
 def planes_digest(x, P):

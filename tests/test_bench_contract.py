@@ -48,8 +48,8 @@ def test_bench_digests_shape_and_bucket0():
         d = json.load(f)
     assert d["packet_numel"] == 256 and d["buckets"] == 4 and d["seed0"] == bench.BENCH_SEED0
     assert len(d["bucket_T1"]) == 4
-    assert sorted(d["job"]) == ["T2", "T4", "T8"]
-    for G in (2, 4, 8):
+    assert sorted(d["job"]) == ["T1", "T2", "T4", "T8"]
+    for G in (1, 2, 4, 8):
         assert [len(r) for r in d["job"][f"T{G}"]] == [G] * 4
     # T = 4 slice 0 of the job IS the N = 1 bucket (same seed, elements [0, 2^26))
     assert d["job"]["T4"][0][0] == d["bucket_T1"][0]
@@ -60,6 +60,11 @@ def test_bench_digests_shape_and_bucket0():
     assert bench.expected_digests(0, 1, 0, d["bucket_numel"], 256, 4) == d["bucket_T1"]
     assert bench.expected_digests(d["job_numel"], 8, 5, 0, 256, 4) == [d["job"]["T8"][b][5] for b in range(4)]
     assert bench.expected_digests(0, 1, 0, d["bucket_numel"], 64, 4) is None
+    # the headline at N > 1: every GPU holds the same 4 buckets -> bucket_T1 on every rank
+    assert bench.expected_digests(0, 8, 7, d["bucket_numel"], 256, 4) == d["bucket_T1"]
+    # the strong reading at N = 1: the whole 1 GiB job on one GPU
+    assert bench.expected_digests(d["job_numel"], 1, 0, d["job_numel"], 256, 4) == [d["job"]["T1"][b][0]
+                                                                                   for b in range(4)]
 
 
 @pytest.mark.gpu
@@ -109,20 +114,61 @@ def test_switch_verdicts_wrong_bits_fatal_for_every_path():
     assert fatal == [] and diag == []
 
 
-def test_n_gt1_line_names_both_readings():
-    """at N > 1 the line carries the strong-scaling `value`
-    and the weak-scaling 256 MiB-per-GPU figure as a named top-level field
-    with its own roofline, and config.readings says which is which."""
-    wk = {"numel_per_gpu": 67_108_864, "buckets": 4, "ms_per_step": 0.0835, "value_GBps": 51_000.0,
-          "per_gpu_GBps": 6375.0, "kernel_ms": 0.0820, "kernel_GBps_per_gpu": 6550.0, "frac_per_gpu": 0.8188}
-    r = bench.weak_readings(wk, 8)
-    assert r["weak_256MiB_value"] == 51_000.0
-    w = r["weak_256MiB"]
-    assert w["scaling"] == "weak" and w["unit"] == "GB/s" and w["n_gpus"] == 8 and w["buckets_cycled"] == 4
-    assert w["roofline"]["frac"] == 0.8188 and w["roofline"]["peak"] == bench.HBM_PEAK_GBPS
-    assert set(r["readings"]) == {"value", "weak_256MiB_value"}
-    assert "strong" in r["readings"]["value"] and "weak" in r["readings"]["weak_256MiB_value"]
-    assert bench.weak_readings(wk, 1) == {} and bench.weak_readings({"error": "x"}, 8) == {}
+def _reading(name, job_numel, world, n, elapsed_s, kernel_ms, steps=20, ok=True):
+    """A synthetic k1_reading result (bench.py) of rank 0's slice `n`."""
+    B = -(-n // 256)
+    slices = ([n] * world if job_numel == 0 else
+              [-(-job_numel // world) if g < job_numel % world else job_numel // world for g in range(world)])
+    return {"name": name, "job_numel": job_numel or world * n, "numel_per_gpu": n, "num_blocks_per_gpu": B,
+            "alg_bytes_per_gpu": 8 * n + B, "total_alg": sum(8 * m + -(-m // 256) for m in slices),
+            "steps": steps, "warmup": 10, "elapsed_s": elapsed_s, "kernel_ms": kernel_ms, "ok": ok,
+            "checked": 4, "check_note": "x"}
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_every_line_names_the_same_two_readings(world):
+    """every line at every N carries weak_256MiB_value (=
+    value) and strong_1GiB_value, each with its own roofline, and
+    config.readings says which is which; `scaling` is "weak" at every N (the
+    headline is the same reading at every N)."""
+    n = 67_108_864
+    hl = _reading("weak_256MiB", 0, world, n, 20 * 0.0825e-3, 0.0818)
+    sn = 268_435_456 // world
+    st = _reading("strong_1GiB", 268_435_456, world, sn, 200 * 0.0825e-3 * sn / n, 0.0818 * sn / n, steps=200)
+    r = bench.readings(hl, st, world, 4, 256)
+    assert set(r) == {"weak_256MiB_value", "weak_256MiB", "strong_1GiB_value", "strong_1GiB", "readings"}
+    assert set(r["readings"]) == {"value", "weak_256MiB_value", "strong_1GiB_value"}
+    w, s = r["weak_256MiB"], r["strong_1GiB"]
+    assert w["scaling"] == "weak" and s["scaling"] == "strong" and w["n_gpus"] == s["n_gpus"] == world
+    assert r["weak_256MiB_value"] == w["value"] and r["strong_1GiB_value"] == s["value"]
+    # weak: world x (8n + B) per step; strong: the whole 1 GiB job per step
+    assert abs(w["value"] - world * (8 * n + n // 256) / 0.0825e-3 / 1e9) < 0.01
+    assert abs(s["value"] - (8 * 268_435_456 + 268_435_456 // 256) / (0.0825e-3 * sn / n) / 1e9) < 0.5
+    for blk in (w, s):
+        rf = blk["roofline"]
+        assert rf["bound"] == "hbm" and rf["peak"] == bench.HBM_PEAK_GBPS and rf["unit"] == "GB/s"
+        assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3 and 0.7 < rf["frac"] < 1.0
+    assert s["job_numel"] == 268_435_456 and s["numel_per_gpu"] == sn and s["steps"] == 200
+    # the strong reading skipped (--job-numel 0): the key is still there, null
+    r0 = bench.readings(hl, None, world, 4, 256)
+    assert r0["strong_1GiB_value"] is None and "strong_1GiB" not in r0
+
+
+def test_rehearsal_fields_are_labelled_not_measured():
+    """when the ranks share one GPU no fraction of the xGMI
+    bound is reported (null, with a note), and phases say they timed the TCP
+    net; on a node (rehearsal None) the fields are untouched."""
+    def res():
+        return {"switchsim": {"frac_of_xgmi_bound": 2.10, "busbw_GBps": 300.0, "phases_ms": {"payload_sum": 208.0}},
+                "xgmi_switch": {"frac_of_xgmi_bound": 1.91},
+                "rccl_fp32_allreduce": {"frac_of_xgmi_bound": 0.4},
+                "p2p_switch": {"error": "boom"}}
+    r = bench.label_rehearsal(res(), "ranks share one GPU: RCCL")
+    for k in ("switchsim", "xgmi_switch", "rccl_fp32_allreduce"):
+        assert r[k]["frac_of_xgmi_bound"] is None and "rehearsal" in r[k]["rehearsal_note"]
+    assert "TCP net" in r["switchsim"]["phases_note"] and "phases_note" not in r["xgmi_switch"]
+    assert r["p2p_switch"] == {"error": "boom"}
+    assert bench.label_rehearsal(res(), None) == res()
 
 
 def test_roofline_traffic_covers_the_n_gt1_slices():
@@ -130,29 +176,32 @@ def test_roofline_traffic_covers_the_n_gt1_slices():
     K1's PMC bytes per launch at the headline bucket and at configs[3]'s
     per-GPU FIFO slices for N = 2 / 8 (N = 4's slice is the headline
     bucket), each within 0.1 % of the algorithmic bytes."""
-    for G in (1, 2, 4, 8):
-        n = 67_108_864 if G == 1 else 268_435_456 // G
+    for n in (67_108_864, 268_435_456, 134_217_728, 33_554_432):   # headline; strong slices at N = 1, 2, 8
         t = bench.load_traffic(n, 256, "quantize_pack_cold")
-        assert t is not None, G
+        assert t is not None, n
         alg = 8 * n + n // 256
-        assert abs(t / alg - 1) < 1e-3, (G, t / alg)
+        assert abs(t / alg - 1) < 1e-3, (n, t / alg)
     assert bench.load_traffic(12345, 256, "quantize_pack_cold") is None
+
+
+def _scale_report():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("scale_report", os.path.join(ROOT, "tools", "scale_report.py"))
+    sr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sr)
+    return sr
 
 
 def test_scale_report_tabulates_bench_lines(tmp_path):
     """tools/scale_report.py finds bench lines in JSON files and text logs and
     tabulates them (used on the driver's scaling run)."""
-    import importlib.util
-    import json
-    import os
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    spec = importlib.util.spec_from_file_location("scale_report", os.path.join(root, "tools", "scale_report.py"))
-    sr = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(sr)
+    sr = _scale_report()
     one = {"metric": "m", "n_gpus": 1, "value": 6500.0, "roofline": {"frac": 0.82}, "ms_per_step": 0.082,
-           "self_check": True}
+           "self_check": True, "scaling": "weak", "weak_256MiB_value": 6500.0, "strong_1GiB_value": 6700.0,
+           "strong_1GiB": {"roofline": {"frac": 0.84}, "self_check": True}}
     two = {"metric": "m", "n_gpus": 2, "value": 12000.0, "roofline": {"frac": 0.8}, "ms_per_step": 0.09,
-           "self_check": True, "weak_256MiB_value": 13000.0, "weak_256MiB": {"roofline": {"frac": 0.81}},
+           "self_check": True, "scaling": "weak", "weak_256MiB_value": 12000.0, "strong_1GiB_value": 13000.0,
+           "strong_1GiB": {"roofline": {"frac": 0.81}, "self_check": True},
            "switchsim": {"ms_per_allreduce": 5.0, "busbw_GBps": 200.0, "frac_of_xgmi_bound": 0.4, "verified": True,
                          "phases_ms": {"k2": 0.1, "payload_sum": 4.0}}}
     (tmp_path / "scale.json").write_text(json.dumps({"runs": [two, one]}))
@@ -161,4 +210,21 @@ def test_scale_report_tabulates_bench_lines(tmp_path):
     assert [b["n_gpus"] for b in got] == [2, 1, 2]
     rep = sr.report(got[:2])
     assert "| 2 | switchsim | 5.000 |" in rep and "payload_sum 4.00" in rep
-    assert "| 2 | 0.923 |" in rep                     # 12000 / (2 x 6500)
+    assert "| 2 | 0.923 | 0.923 | 0.970 |" in rep      # 12000 / (2 x 6500) twice; 13000 / (2 x 6700)
+
+
+def test_scale_report_efficiency_is_per_reading():
+    """each reading's efficiency is against the SAME reading at
+    N = 1 — a strong 1 GiB rate is never divided by the weak 256 MiB rate."""
+    sr = _scale_report()
+    mk = lambda n, w, s: {"metric": "m", "n_gpus": n, "value": w, "weak_256MiB_value": w,  # noqa: E731
+                          "strong_1GiB_value": s}
+    lines = [mk(1, 6500.0, 6700.0), mk(2, 13000.0, 13400.0), mk(4, 25350.0, 24120.0), mk(8, 51350.0, 42880.0)]
+    eff = sr.efficiency(lines)
+    assert eff["value"] == eff["weak_256MiB_value"]
+    assert [round(eff["weak_256MiB_value"][n], 4) for n in (1, 2, 4, 8)] == [1.0, 1.0, 0.975, 0.9875]
+    assert [round(eff["strong_1GiB_value"][n], 4) for n in (1, 2, 4, 8)] == [1.0, 1.0, 0.9, 0.8]
+    # an N = 1 line without the strong reading: no strong efficiency at all (not a mixed one)
+    lines[0]["strong_1GiB_value"] = None
+    assert sr.efficiency(lines)["strong_1GiB_value"] == {}
+    assert sr.efficiency(lines[1:]) == {"value": {}, "weak_256MiB_value": {}, "strong_1GiB_value": {}}

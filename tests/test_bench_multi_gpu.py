@@ -52,11 +52,51 @@ def run_child(cmd, env, out_dir, timeout, what):
     return p.returncode, out, err, wall
 
 
-def _free_port():
+def rendezvous_port():
+    """A --master-port for the driver-form launch, chosen BELOW the kernel's
+    ephemeral range (/proc/sys/net/ipv4/ip_local_port_range): no outgoing
+    connection (RCCL's, the TCP net's, the store clients') is ever given such
+    a port, so between this pick and torchrun's bind only another explicit
+    listener could take it — not the bind-0-close-reuse race.
+    Checked free (bindable) at pick time; random within [lo - 12000, lo)."""
+    import random
     import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo = int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        lo = 32768
+    top = max(lo, 2048)
+    cands = list(range(max(1025, top - 12000), top))
+    random.SystemRandom().shuffle(cands)
+    for port in cands[:200]:
+        with socket.socket() as s:
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+        return port
+    raise RuntimeError("no free port below the ephemeral range")
+
+
+def assert_two_readings(line, n, nb=4):
+    """the same keys at every N — value = weak_256MiB_value
+    (256 MiB per GPU), strong_1GiB_value (configs[3]'s 1 GiB job over the N
+    GPUs), each with its own roofline and self-check — and `scaling` "weak"
+    at every N."""
+    assert line["scaling"] == "weak"
+    assert line["value"] == line["weak_256MiB_value"] > 0
+    assert set(line["config"]["readings"]) == {"value", "weak_256MiB_value", "strong_1GiB_value"}
+    for key, blk in (("weak_256MiB_value", "weak_256MiB"), ("strong_1GiB_value", "strong_1GiB")):
+        b = line[blk]
+        assert line[key] == b["value"] > 0 and b["n_gpus"] == n
+        assert b["self_check"] is True and b["buckets_checked_min_over_ranks"] == nb, (blk, b)
+        assert b["roofline"]["bound"] == "hbm" and 0 < b["roofline"]["frac"] < 1.0
+    assert line["weak_256MiB"]["numel_per_gpu"] == 67_108_864
+    assert line["strong_1GiB"]["job_numel"] == 268_435_456
+    assert line["strong_1GiB"]["numel_per_gpu"] == 268_435_456 // n
+    assert line["strong_1GiB"]["scaling"] == "strong" and line["weak_256MiB"]["scaling"] == "weak"
 
 
 @pytest.mark.gpu
@@ -76,7 +116,7 @@ def test_bench_n2_rehearsal_line(cuda, tmp_path, launcher, n):
         cmd = [sys.executable, "-u", *args]
     else:
         cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *args]
+               "--master-addr", "127.0.0.1", "--master-port", str(rendezvous_port()), *args]
     rc, out, err, wall = run_child(cmd, env, str(tmp_path), 800, f"bench.py --gpus {n} (rehearsal, {launcher})")
     lines = [l for l in out.splitlines() if l.startswith("{")]
     assert lines, f"no JSON line (rc {rc}); stderr tail:\n{err}"
@@ -91,10 +131,13 @@ def test_bench_n2_rehearsal_line(cuda, tmp_path, launcher, n):
         assert line[k]["workers"] == n
     assert line["p2p_switch"]["bit_equal_to_switchsim"] and line["xgmi_switch"]["bit_equal_to_switchsim"]
     assert line["ms_per_step"] * line["steps"] / 1e3 < wall
-    assert line["value"] > 0 and line["roofline"]["frac"] > 0
-    assert line["weak_256MiB_value"] > 0 and line["weak_256MiB"]["roofline"]["frac"] > 0
-    assert set(line["config"]["readings"]) == {"value", "weak_256MiB_value"}
-    assert line["scaling"] == "strong"
+    assert_two_readings(line, n)
+    # rehearsal-only fields are labelled, never reported as measured against xGMI
+    assert line["rehearsal_note"]
+    for k in (*bench.SWITCH_PATHS, "rccl_fp32_allreduce"):
+        f = line.get(k, {})
+        assert f.get("frac_of_xgmi_bound") is None and f.get("rehearsal_note"), (k, f)
+    assert line["switchsim"]["phases_note"] and line["configs4_plugin"]["rehearsal_note"]
 
 
 @pytest.mark.gpu
@@ -131,6 +174,8 @@ def test_bench_n1_line(cuda, tmp_path):
         assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3 and 0.3 < r["frac"] < 1.0
         n, P = line["config"]["numel_per_gpu"], line["config"]["packet_numel"]
         assert abs(r["traffic"] / (8 * n + -(-n // P)) - 1) < 1e-3
+        assert_two_readings(line, 1, nb)
+        assert "rehearsal_note" not in line
         if not extra:
             cb = line["cpu_baseline"]
             assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["unit"].startswith("GB/s")

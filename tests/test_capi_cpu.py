@@ -162,6 +162,13 @@ def test_frames_and_rdma_validation_without_gpu(sw):
     assert L.sml_quantize_pack_frames(None, 0, 256, 1, None, 64, ctypes.byref(fp), None, 1076, None) == sw.SML_OK
     assert L.sml_rdma_imm(None, 0, 64, None, None) == sw.SML_OK
     assert L.sml_rdma_imm(None, 10, 64, None, None) == sw.SML_ERR_INVALID_ARG
+    # a null exponent plane is an error for FLOAT32 even with d_imm given
+    # (the INT32 immediates have their own entry point)
+    assert L.sml_rdma_imm(None, 10, 64, ctypes.c_void_p(16), None) == sw.SML_ERR_INVALID_ARG
+    assert L.sml_rdma_imm_int32(0, None, None) == sw.SML_OK
+    assert L.sml_rdma_imm_int32(10, None, None) == sw.SML_ERR_INVALID_ARG
+    assert L.sml_debug_stall(0, None) == sw.SML_OK
+    assert L.sml_debug_stall(60_000_001, None) == sw.SML_ERR_INVALID_ARG
 
 
 def test_frame_params_layout_matches_header(sw):

@@ -308,12 +308,19 @@ def lead_stream(x, fp, P, K, pairs_iters, other_job):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("P", [256, 1024])
-def test_int32_rx_later_copy_claiming_first_is_fixed_up(cuda, P):
-    """Cover of the fix-up by real races: later copies that claim their
-    pkt_ids BEFORE the earlier copies (their wave runs ahead), with different
-    payloads.  The output must be the first copies' words and the counts
-    exact; the slice's conflict total (printed) shows how many later copies
-    did claim first."""
+def test_int32_rx_racing_copies_smoke(cuda, P):
+    """A SMOKE TEST of real scheduling, not the pin of the fix-up (VERDICT r5
+    #5): a stream laid out so that later copies of pkt_ids (different
+    payloads) tend to reach the claim atomic before the earlier copies (their
+    wave runs ahead).  Asserted: the output is the first copies' words and the
+    counts are exact, whatever the scheduling did.  NOT asserted: that any
+    later copy actually claimed first — the hardware decides the interleaving
+    of waves, so the number that did (printed) can be 0 on a given run
+    (r05z: 0 of 256; other runs: all of them).  No launch order makes it
+    deterministic: a frame's tag is its position in the call, and one wave
+    walks its tiles in that order, so only a cross-wave race can put a later
+    copy first.  The fix-up itself is pinned, deterministically, by
+    test_int32_rx_fixup_rewrites_displaced_claims (pre-seeded later claims)."""
     import torch
     import switchml_amd as sw
     K, pairs_iters = 3000, 64
@@ -342,10 +349,8 @@ def test_int32_rx_later_copy_claiming_first_is_fixed_up(cuda, P):
     bad = np.flatnonzero(got != ref)
     assert bad.size == 0, (bad.size, bad[:8].tolist())
     assert rx.counts.cpu().tolist() == [acc, dis]
-    # 256 of 256 (P = 256) and 64 of 64 (P = 1024) on MI355X in every run so
-    # far; a scheduling fact, not a correctness one, so reported rather than
-    # asserted (the fix-up itself is pinned by the white-box test below)
-    print(f"P={P}: {rx.conflicts} of {pairs_iters * F} later copies claimed first")
+    # a scheduling fact, not a correctness one: reported, never asserted
+    print(f"P={P}: {rx.conflicts} of {pairs_iters * F} later copies claimed first (smoke: any number passes)")
 
 
 def claim_tag(call, f):

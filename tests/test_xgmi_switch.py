@@ -246,3 +246,61 @@ def test_xgmi_replaces_stale_segment(cuda):
         assert res is not None, (rank, err)
         assert all(res), (rank, res)
     assert not os.path.exists(path)
+
+
+def _stalled_worker(rank, W, init, session, stall_rank, stall_ms, timeout_ms):
+    """Worker `stall_rank` queues a kernel that keeps its worker stream busy
+    for stall_ms (backend.dummy.stall_worker_thread / stall_ms:
+    sml_debug_stall, which ends on its own) before its slice — a device that
+    does not finish within backend.xgmi.timeout_ms.  ADVICE r5: the slice must
+    be reported FAILED within about timeout_ms, not block the worker thread in
+    an unbounded stream synchronize; later jobs fail at once (wedged worker
+    or poisoned session); and once the stalled kernel has ended on its own,
+    a new session on the same device works again (the wedged switch's reaper
+    has freed its planes and closed its peer mappings by then; the new
+    switch waits for it)."""
+    import time
+    from switchml_amd import client as C
+    kw = dict(stall_worker_thread=0, stall_ms=stall_ms) if rank == stall_rank else {}
+    C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=1, packet_numel=256,
+                          max_outstanding_packets=64, mode="bulk", bandwidth=0, device=0, session=session,
+                          timeout_ms=timeout_ms, **kw))
+    t_start = time.time()
+    sts, secs = [], []
+    for j in range(2):
+        x = torch.from_numpy(worker_bucket(rank, 100_000, j)).cuda()
+        t0 = time.time()
+        job = C.allreduce_async(x)
+        C.wait_for_all_jobs()
+        secs.append(time.time() - t0)
+        sts.append(job.status())
+    C.stop()
+    # the stalled kernel ends stall_ms after it started: then the device is usable again
+    time.sleep(max(0.0, stall_ms / 1e3 - (time.time() - t_start)) + 0.5)
+    torch.cuda.synchronize()
+    C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=1, packet_numel=256,
+                          max_outstanding_packets=64, mode="bulk", bandwidth=0, device=0,
+                          session=session + "-after", timeout_ms=30000))
+    xs = [worker_bucket(r, 50_000, 9) for r in range(W)]
+    t = torch.from_numpy(xs[rank].copy()).cuda()
+    C.allreduce(t)
+    after_ok = bool(np.array_equal(t.cpu().numpy().view(np.uint32), oracle_switch_allreduce(xs, 256, 1).view(np.uint32)))
+    C.stop()
+    return {"statuses": sts, "seconds": secs, "after_ok": after_ok}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [1, 2])
+def test_xgmi_stalled_device_fails_slice_within_timeout(cuda, W):
+    from switchml_amd import client as C
+    session = "stall-" + uuid.uuid4().hex
+    stall_ms, timeout_ms = 4000, 300
+    out = _run(_stalled_worker, W, (session, 0, stall_ms, timeout_ms), timeout=120)
+    for rank, res, err in out:
+        assert res is not None, (rank, err)
+    allres = {rank: res for rank, res, _ in out}
+    for rank, res in allres.items():
+        assert res["statuses"] == [C.JOB_FAILED] * 2, allres
+        # reported within ~timeout_ms (a few bounded waits at most), long before the stall ends
+        assert res["seconds"][0] < 2.0 and res["seconds"][1] < 1.0, allres
+        assert res["after_ok"], allres

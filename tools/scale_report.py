@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Tabulate the N > 1 bench lines of a scaling run (the driver's SCALE_rNN.json,
-or any files holding bench.py JSON lines) as markdown: per N the headline
-(strong: configs[3]'s 1 GiB job over N GPUs) and the weak 256 MiB-per-GPU
-reading with their per-GPU roofline fractions, then each switch path's time
+or any files holding bench.py JSON lines) as markdown: per N the two readings
+every line carries (value = weak_256MiB_value: 256 MiB buckets on every GPU;
+strong_1GiB_value: configs[3]'s 1 GiB job over the N GPUs) with their per-GPU
+roofline fractions, the scaling efficiency of EACH reading against the same
+reading at N = 1, then each switch path's time
 per all-reduce, its fraction of the xGMI bound and its phases — the numbers
 DESIGN.md §10 says to act on once a real node has run.  Reads any JSON: every
 object carrying "n_gpus" and "metric" counts as a bench line (also lines
@@ -49,21 +51,51 @@ def fmt(v, nd=3):
     return f"{v:.{nd}f}" if isinstance(v, float) else str(v)
 
 
+READINGS = (("value", "value (= weak_256MiB_value)"), ("weak_256MiB_value", "weak 256 MiB per GPU"),
+            ("strong_1GiB_value", "strong 1 GiB job"))
+
+
+def reading_frac(b, key):
+    """The per-GPU roofline fraction of one reading of a line."""
+    sub = {"value": b, "weak_256MiB_value": b.get("weak_256MiB") or {},
+           "strong_1GiB_value": b.get("strong_1GiB") or {}}[key]
+    return (sub.get("roofline") or {}).get("frac")
+
+
+def efficiency(lines):
+    """{reading: {N: rate(N) / (N x rate(1))}} — each reading against the SAME
+    reading at N = 1 (never one workload's rate over another's).
+    A reading missing at N = 1 or at N gets no entry for that N.  Weak and
+    strong readings both ideally scale as N x rate(1) (strong: the job's time
+    shrinks N-fold)."""
+    base = next((b for b in lines if b["n_gpus"] == 1), None)
+    out = {}
+    for key, _ in READINGS:
+        r1 = base.get(key) if base else None
+        out[key] = {b["n_gpus"]: b[key] / (b["n_gpus"] * r1) for b in lines
+                    if r1 and isinstance(b.get(key), (int, float))}
+    return out
+
+
 def report(lines):
     lines = sorted(lines, key=lambda b: b["n_gpus"])
-    out = ["| N | value (GB/s) | frac / GPU | ms/step | weak 256 MiB (GB/s) | weak frac / GPU | self_check |",
-           "|---|---|---|---|---|---|---|"]
+    out = ["| N | weak 256 MiB = value (GB/s) | weak frac / GPU | ms/step | strong 1 GiB (GB/s) | "
+           "strong frac / GPU | scaling | self_check |",
+           "|---|---|---|---|---|---|---|---|"]
     for b in lines:
-        wk = b.get("weak_256MiB") or {}
-        out.append(f"| {b['n_gpus']} | {fmt(b.get('value'), 1)} | {fmt((b.get('roofline') or {}).get('frac'))} | "
-                   f"{fmt(b.get('ms_per_step'), 5)} | {fmt(b.get('weak_256MiB_value'), 1)} | "
-                   f"{fmt((wk.get('roofline') or {}).get('frac'))} | {b.get('self_check')} |")
-    base = next((b for b in lines if b["n_gpus"] == 1), None)
-    if base:
-        out += ["", "Scaling of `value` against N = 1 (strong; the driver computes its own):", ""]
-        out += ["| N | value / (N x value(1)) |", "|---|---|"]
+        st = b.get("strong_1GiB") or {}
+        out.append(f"| {b['n_gpus']} | {fmt(b.get('value'), 1)} | {fmt(reading_frac(b, 'value'))} | "
+                   f"{fmt(b.get('ms_per_step'), 5)} | {fmt(b.get('strong_1GiB_value'), 1)} | "
+                   f"{fmt(reading_frac(b, 'strong_1GiB_value'))} | {b.get('scaling')} | "
+                   f"{b.get('self_check')}{'' if st.get('self_check', True) else ' (strong: FAILED)'} |")
+    eff = efficiency(lines)
+    if any(eff.values()):
+        out += ["", "Scaling efficiency per reading, rate(N) / (N x rate(1)) of the SAME reading "
+                "(the driver computes its own from `value`):", ""]
+        out += ["| N | " + " | ".join(name for _, name in READINGS) + " |", "|---" * (len(READINGS) + 1) + "|"]
         for b in lines:
-            out.append(f"| {b['n_gpus']} | {fmt(b['value'] / (b['n_gpus'] * base['value']))} |")
+            n = b["n_gpus"]
+            out.append(f"| {n} | " + " | ".join(fmt(eff[k].get(n)) for k, _ in READINGS) + " |")
     out += ["", "| N | path | ms / all-reduce | busbw GB/s | frac of xGMI bound | verified | phases (ms) |",
             "|---|---|---|---|---|---|---|"]
     for b in lines:
@@ -74,6 +106,8 @@ def report(lines):
             ph = ", ".join(f"{p} {fmt(t, 2)}" for p, t in (f.get("phases_ms") or {}).items())
             out.append(f"| {b['n_gpus']} | {k} | {fmt(f.get('ms_per_allreduce'))} | {fmt(f.get('busbw_GBps'), 2)} | "
                        f"{fmt(f.get('frac_of_xgmi_bound'), 4)} | {f.get('verified', '–')} | {ph or f.get('error', '–')} |")
+    if any(b.get("rehearsal_note") for b in lines):
+        out += ["", "Rehearsal lines (ranks sharing one GPU) are present: their rates are not N-GPU measurements."]
     fails = [(b["n_gpus"], b.get("failures"), b.get("diagnostic_failures")) for b in lines
              if b.get("failures") or b.get("diagnostic_failures")]
     if fails:
