@@ -325,6 +325,9 @@ def main():
         world = 1
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
+    on_term = {"emit": None}
+    if world > 1:
+        term_guard(on_term)
 
     import torch
     import torch.distributed as dist
@@ -392,10 +395,21 @@ def main():
     diag_failures = []          # diagnostic fields: reported, not fatal (module docstring)
     side, fields, extra = {}, {}, {}
 
+    emit_lock, emitted = threading.Lock(), [False]
+
     def emit():
-        """Rank 0's one JSON line, from whatever has been measured so far."""
+        """Rank 0's one JSON line, from whatever has been measured so far —
+        exactly once, whichever of the normal end, the watchdog or the
+        launcher's SIGTERM (term_guard) comes first."""
         if rank != 0:
             return
+        with emit_lock:
+            if emitted[0]:
+                return
+            emitted[0] = True
+            emit_line()
+
+    def emit_line():
         ms_per_step = elapsed * 1e3 / args.steps
         value = hl["total_alg"] / (elapsed / args.steps) / 1e9
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
@@ -473,6 +487,12 @@ def main():
         print(json.dumps(line), flush=True)
 
     side_cpu = {}
+
+    def on_sigterm():
+        diag_failures.append("terminated: SIGTERM from the launcher (another rank failed or the run was stopped) "
+                             "during the multi-GPU diagnostic phase; the fields above are what was measured")
+        emit()
+    on_term["emit"] = on_sigterm
 
     def guarded(key, fn):
         """A side measurement: its failure is reported, never the headline's."""
@@ -556,6 +576,32 @@ def main():
     emit()
     if failures:
         sys.exit(1)
+
+
+def term_guard(on_term):
+    """N > 1: keep rank 0's line when the launcher stops the ranks.
+
+    torch.distributed.run stops every rank with SIGTERM (SIGKILL 30 s later)
+    as soon as ONE rank fails — a rank that faults on its first peer-memory
+    access on a real node (first contact) would otherwise take the
+    measured and checked headline down with it, unprinted.  SIGTERM is
+    blocked in this thread before torch, RCCL or HIP start theirs (so all of
+    them inherit the mask) and taken by one daemon thread in sigwait, which
+    runs on_term["emit"] (rank 0's line with a "terminated" diagnostic, once
+    the headline exists) and exits 1.  Every blocking wait of the main thread
+    (collectives, device syncs, ctypes calls) releases the GIL, so the thread
+    runs while the main thread is stuck in one."""
+    import signal
+    signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGTERM})
+
+    def waiter():
+        signal.sigwait({signal.SIGTERM})
+        try:
+            if on_term["emit"] is not None:
+                on_term["emit"]()
+        finally:
+            os._exit(1)
+    threading.Thread(target=waiter, name="sigterm-guard", daemon=True).start()
 
 
 REHEARSAL_NOTE = ("rehearsal: the ranks share ONE GPU (SML_BENCH_REHEARSE), so these rates are one device's "
@@ -930,103 +976,145 @@ def exchange_measure(sw, torch, dist, n, P, world, rank, dev, reps=5, rehearsal=
         dist.all_reduce(d, op=dist.ReduceOp.MAX)
         return {k: round(float(v) * 1e3, 3) for k, v in zip(keys[1:], d.tolist())}
 
+    def agreed(fn):
+        """Run fn on this rank, then learn (one all_reduce MIN) whether it
+        succeeded on EVERY rank: a path that fails on one rank — its first
+        contact with a peer's HBM over xGMI on a real node — is then skipped
+        by all of them together, instead of leaving the others blocked in a
+        collective that rank will never join (first contact).
+        Returns (ok on all ranks, fn's value, this rank's exception)."""
+        val, err = None, None
+        try:
+            val = fn()
+        except Exception as e:  # noqa: BLE001 - reported in the path's field
+            err = e
+        t = torch.tensor([0 if err is not None else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item()), val, err
+
+    def failed(pipe, what, err):
+        return {"error": (repr(err)[:400] if err is not None else f"{what} failed on another rank"),
+                "failed_phase": what, "pipeline": pipe}
+
+    def run_path(name, pipe, setup, call, teardown, local_teardown, with_phases):
+        """One switch path through agreed phases: setup, a first call checked
+        against the fp32 all-reduce, `reps` timed calls (each keeping its
+        result), optional phase marks, teardown; every timed call must equal
+        the first (planes are reused call after call)."""
+        ok, ar, err = agreed(setup)
+        if not ok:
+            if ar is not None:
+                # set up here but not on another rank: undo it locally (a
+                # collective teardown would wait for the rank that failed)
+                try:
+                    local_teardown(ar)
+                except Exception:  # noqa: BLE001 - the path already failed
+                    pass
+            res[name] = failed(pipe, "setup", err)
+            return
+        out = torch.empty_like(x)
+
+        def first():
+            call(ar, out)
+            torch.cuda.synchronize()
+            e = (out - ref).abs()
+            return bool((e <= tol).all().item()), float(e.max().item())
+        ok, v, err = agreed(first)
+        if not ok:
+            try:
+                teardown(ar)
+            except Exception:  # noqa: BLE001
+                pass
+            res[name] = failed(pipe, "first call", err)
+            return
+        within, max_err = v
+        touts = [torch.empty_like(x) for _ in range(reps)]   # every timed call keeps its result
+        dist.barrier()
+        t0, terr = time.perf_counter(), None
+        try:
+            for i in range(reps):
+                call(ar, touts[i])
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 - agreed just below, with the time
+            terr = e
+        tt = torch.tensor([(time.perf_counter() - t0) / reps, 1.0 if terr is not None else 0.0],
+                          dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        phases = None
+        if with_phases and not float(tt[1]):
+            try:
+                phases = phase_ms(ar, lambda: call(ar, out))
+            except Exception as e:  # noqa: BLE001 - diagnostic only
+                phases = {"error": repr(e)[:200]}
+        try:
+            teardown(ar)
+        except Exception as e:  # noqa: BLE001
+            terr = terr or e
+        if float(tt[1]):
+            res[name] = failed(pipe, "timed calls", terr)
+            return
+        t = float(tt[0])
+        same = all(bool(torch.equal(o, out)) for o in touts)
+        del touts
+        ok_t = torch.tensor([int(within), int(same)], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        outs[name] = out
+        res[name] = {"workers": W, "numel_per_worker": n, "packet_numel": P,
+                     "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * n / t / 1e9, 2),
+                     "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
+                     "xgmi_bound_ms": round(bound_s * 1e3, 3),
+                     "frac_of_xgmi_bound": round(bound_s / t, 4),
+                     "within_quantization_bound": bool(ok_t[0].item()),
+                     "timed_calls_equal_first": bool(ok_t[1].item()),
+                     "max_abs_err_vs_fp32_allreduce": max_err, "pipeline": pipe}
+        if with_phases:
+            res[name]["phases_ms"] = phases
+
+    def torch_teardown(ar):
+        if hasattr(ar, "close"):
+            ar.close()
+
     for name, cls, pipe in (
             ("switchsim", SwitchSimAllReduce,
              "K2 exps -> all_reduce(int8, MAX) -> K3 LE payload -> all_reduce(int32, SUM) -> K4"),
             ("p2p_switch", PeerSwitchAllReduce,
              "K2 exps -> all_reduce(int8, MAX) -> K3 BE payload -> K6 over the peers' planes (hipIpc, xGMI) "
              "on this rank's block shard -> all_gather(fp32)")):
-        try:
-            ar = cls(n, P, dev)
-            out = torch.empty_like(x)
-            ar(x, out)
-            torch.cuda.synchronize()
-            err = (out - ref).abs()
-            within = bool((err <= tol).all().item())
-            touts = [torch.empty_like(x) for _ in range(reps)]   # every timed call keeps its result
-            dist.barrier()
-            t0 = time.perf_counter()
-            for i in range(reps):
-                ar(x, touts[i])
-            torch.cuda.synchronize()
-            tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            t = float(tt[0])
-            try:
-                phases = phase_ms(ar, lambda: ar(x, out))
-            except Exception as e:  # noqa: BLE001 - diagnostic only
-                phases = {"error": repr(e)[:200]}
-            if hasattr(ar, "close"):
-                ar.close()
-            del ar
-            # planes are reused call after call: every timed call must give the first call's bits
-            same = all(bool(torch.equal(o, out)) for o in touts)
-            del touts
-            ok_t = torch.tensor([int(within), int(same)], dtype=torch.int32, device=dev)
-            dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
-            same = bool(ok_t[1].item())
-            outs[name] = out
-            res[name] = {"workers": W, "numel_per_worker": n, "packet_numel": P,
-                         "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * n / t / 1e9, 2),
-                         "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
-                         "xgmi_bound_ms": round(bound_s * 1e3, 3),
-                         "frac_of_xgmi_bound": round(bound_s / t, 4),
-                         "within_quantization_bound": bool(ok_t[0].item()),
-                         "timed_calls_equal_first": same,
-                         "max_abs_err_vs_fp32_allreduce": float(err.max().item()),
-                         "pipeline": pipe, "phases_ms": phases}
-            del err
-        except Exception as e:  # noqa: BLE001
-            res[name] = {"error": repr(e)[:400], "pipeline": pipe}
+        run_path(name, pipe, lambda cls=cls: cls(n, P, dev), lambda ar, o: ar(x, o), torch_teardown,
+                 lambda ar: getattr(ar, "_unmap", lambda: None)(), True)
     # the native in-node switch: the client's Context with backend = xgmi
-    # (C++ runtime, no torch.distributed in the data path), in its pull form
+    # (C++ runtime, no torch.distributed in the data path: a failure there is
+    # a barrier timeout or a poisoned session, never a hang), in its pull form
     # (K6 reads the peers' planes over xGMI) and its push form (K3 writes
     # each shard into its owner's inbox over xGMI; backend.xgmi.push)
+    from switchml_amd import client as C
     for name, push in (("xgmi_switch", False), ("xgmi_switch_push", True)):
         pipe = ("Context::AllReduce, backend xgmi: K2 -> int8 max over the peers' exponent planes -> " +
                 ("K3 writing each shard into its owner's inbox (hipIpc, xGMI) -> K6 on this worker's shard over "
                  "the local inbox" if push else
                  "K3 BE -> K6 on this worker's shard over the peers' planes (hipIpc, xGMI)") +
                 " -> gather of the W shards")
-        try:
-            from switchml_amd import client as C
-            session = [f"bench-xgmi-{os.getpid()}-{int(time.time() * 1e3)}-{int(push)}" if rank == 0 else None]
-            dist.broadcast_object_list(session, src=0)
+        session = [f"bench-xgmi-{os.getpid()}-{int(time.time() * 1e3)}-{int(push)}" if rank == 0 else None]
+        dist.broadcast_object_list(session, src=0)
+
+        # SML_BENCH_INJECT=<path>:<rank> (tests only): that rank's worker fails
+        # right after joining the session (backend.xgmi.fail_setup) — what a
+        # failed first mapping of a peer's plane looks like to the run
+        inject = os.environ.get("SML_BENCH_INJECT", "") == f"{name}:{rank}"
+
+        def xgmi_setup(push=push, sess=session[0], inject=inject):
             if C.state() == C.RUNNING:
                 C.stop()
             C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=1, packet_numel=P,
                                   max_outstanding_packets=256, mode="bulk", bandwidth=0, device=dev.index,
-                                  session=session[0], max_slice_numel=64 << 20, push=push))
-            out = torch.empty_like(x)
-            C.allreduce(x, out)
-            torch.cuda.synchronize()
-            err = (out - ref).abs()
-            within = bool((err <= tol).all().item())
-            touts = [torch.empty_like(x) for _ in range(reps)]
-            dist.barrier()
-            t0 = time.perf_counter()
-            for i in range(reps):
-                C.allreduce(x, touts[i])
-            torch.cuda.synchronize()
-            tt = torch.tensor([(time.perf_counter() - t0) / reps], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            t = float(tt[0])
-            C.stop()
-            same = all(bool(torch.equal(o, out)) for o in touts)
-            del touts
-            ok_t = torch.tensor([int(within), int(same)], dtype=torch.int32, device=dev)
-            dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
-            same = bool(ok_t[1].item())
-            outs[name] = out
-            res[name] = {"workers": W, "numel_per_worker": n, "packet_numel": P,
-                         "ms_per_allreduce": round(t * 1e3, 3), "algbw_GBps": round(4 * n / t / 1e9, 2),
-                         "busbw_GBps": round(2 * (W - 1) / W * 4 * n / t / 1e9, 2),
-                         "xgmi_bound_ms": round(bound_s * 1e3, 3), "frac_of_xgmi_bound": round(bound_s / t, 4),
-                         "within_quantization_bound": bool(ok_t[0].item()), "timed_calls_equal_first": same,
-                         "max_abs_err_vs_fp32_allreduce": float(err.max().item()), "pipeline": pipe}
-            del err
-        except Exception as e:  # noqa: BLE001
-            res[name] = {"error": repr(e)[:400], "pipeline": pipe}
+                                  session=sess, max_slice_numel=64 << 20, push=push, timeout_ms=60000,
+                                  fail_setup=inject))
+            return C
+
+        def xgmi_teardown(_c):
+            if C.state() == C.RUNNING:
+                C.stop()
+        run_path(name, pipe, xgmi_setup, lambda c, o: c.allreduce(x, o), xgmi_teardown, xgmi_teardown, False)
     # the three paths compute the same switch: bit-equal outputs
     paths = ("switchsim", "p2p_switch", "xgmi_switch", "xgmi_switch_push")
     names = [k for k in paths if k in outs]
@@ -1262,10 +1350,20 @@ def plugin_measure_ranks(torch, dist, dev, world):
            "max_outstanding_packets = 256\n[backend.dummy]\nbandwidth = 0\n[backend.hip]\nmode = bulk\ndevice = %d\n"
            "[backend.xgmi]\nsession = %s\n" % (rank, world, dev.index, session[0]))
     dist.barrier()
-    r = plugin_buckets(torch, dev, ini=ini, nranks=world, rank=rank)
-    t = torch.tensor([r["device"]["ms_per_iteration"], r["pinned_host"]["ms_per_iteration"],
-                      0.0 if r["placements_agree"] else 1.0], dtype=torch.float64, device=dev)
+    # a failure on one rank (its first xGMI contact) is agreed on by all of
+    # them in the one collective that follows, instead of leaving the others
+    # waiting in it (the plugin's own exchange fails by its barrier timeout)
+    r, err = None, None
+    try:
+        r = plugin_buckets(torch, dev, ini=ini, nranks=world, rank=rank)
+    except Exception as e:  # noqa: BLE001 - agreed below, reported by the caller
+        err = e
+    t = torch.tensor([r["device"]["ms_per_iteration"] if r else 0.0, r["pinned_host"]["ms_per_iteration"] if r else 0.0,
+                      0.0 if (r and r["placements_agree"]) else 1.0, 1.0 if r is None else 0.0],
+                     dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if float(t[3]):
+        raise RuntimeError(repr(err)[:300] if err is not None else "configs4_plugin failed on another rank")
     out = {k: r[k] for k in ("buckets", "params", "num_workers", "num_worker_threads", "packet_numel", "backend")}
     out["ranks"] = world
     for i, name in enumerate(("device", "pinned_host")):

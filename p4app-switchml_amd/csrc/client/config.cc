@@ -79,6 +79,7 @@ bool Config::LoadFromString(const std::string& ini) {
         else if (full == "backend.xgmi.max_slice_numel") backend_.xgmi.max_slice_numel = parse_uint<uint64_t>(full, val, ~0ull);
         else if (full == "backend.xgmi.timeout_ms") backend_.xgmi.timeout_ms = parse_uint<uint64_t>(full, val, ~0ull);
         else if (full == "backend.xgmi.push") backend_.xgmi.push = parse_bool(val);
+        else if (full == "backend.xgmi.fail_setup") backend_.xgmi.fail_setup = parse_bool(val);
         else if (full == "backend.hip.mode") backend_.hip.mode = val;
         else if (full == "backend.hip.packet_ring") backend_.hip.packet_ring = val;
         else if (full == "backend.hip.burst_server") backend_.hip.burst_server = parse_bool(val);
@@ -170,6 +171,7 @@ std::string Config::ToString() const {
       << "\n\n[backend.xgmi]\nsession = " << backend_.xgmi.session
       << "\nmax_slice_numel = " << backend_.xgmi.max_slice_numel << "\ntimeout_ms = " << backend_.xgmi.timeout_ms
       << "\npush = " << (backend_.xgmi.push ? "true" : "false")
+      << "\nfail_setup = " << (backend_.xgmi.fail_setup ? "true" : "false")
       << "\n";
     return o.str();
 }

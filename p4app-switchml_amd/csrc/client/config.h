@@ -92,6 +92,10 @@ struct XgmiBackendConfig {
     // xGMI and K6 reads only local HBM (push).  Same bytes; all workers of a
     // session must agree.  The multicast (gather) pulls in both.
     bool push = false;
+    // Fault injection for tests: this worker fails right after joining the
+    // session (handles published, the workers' barrier passed), as one that
+    // cannot map a peer's plane on its first contact with another GPU does.
+    bool fail_setup = false;
 };
 
 struct BackendConfig {

@@ -164,6 +164,7 @@ XgmiSwitch::XgmiSwitch(const Config& config, int device) {
     timeout_ms_ = config.backend_.xgmi.timeout_ms;
     round_flags_ = config.backend_.hip.vcl ? SML_FLAG_ROUND_RNE : 0u;
     push_ = config.backend_.xgmi.push;
+    fail_setup_ = config.backend_.xgmi.fail_setup;
     if (W_ < 1 || W_ > kMaxW) throw SwitchMLFatal("xgmi switch: num_workers must be 1..16");
     if (T_ < 1 || T_ > kMaxT) throw SwitchMLFatal("xgmi switch: num_worker_threads must be 1..16");
     if (rank_ < 0 || rank_ >= W_) throw SwitchMLFatal("xgmi switch: general.rank must be < num_workers");
@@ -171,6 +172,11 @@ XgmiSwitch::XgmiSwitch(const Config& config, int device) {
     try {
         Setup(device);
     } catch (...) {
+        // a worker that joined the session and then failed (e.g. it cannot
+        // map a peer's plane: the first contact with another GPU) poisons
+        // it, so the peers' first exchange fails at once instead of waiting
+        // out backend.xgmi.timeout_ms at a barrier this worker never reaches
+        if (attached_) Poison();
         Release();   // no planes, mappings or segment left behind by a failed construction
         throw;
     }
@@ -218,6 +224,7 @@ void XgmiSwitch::Setup(int device) {
         shm_->push != (push_ ? 1u : 0u))
         throw SwitchMLFatal("xgmi switch: workers disagree on num_workers / num_worker_threads / packet_numel / "
                             "max_slice_numel / push");
+    if (fail_setup_) throw SwitchMLFatal("xgmi switch: injected setup failure (backend.xgmi.fail_setup)");
     for (int t = 0; t < T_; t++) {
         ThreadPlanes& tp = planes_[t];
         tp.peer_exps.resize(W_);

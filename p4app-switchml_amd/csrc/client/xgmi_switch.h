@@ -142,6 +142,7 @@ class XgmiSwitch {
     uint64_t timeout_ms_;
     uint32_t round_flags_ = 0;   // SML_FLAG_ROUND_RNE under backend.hip.vcl
     bool push_ = false;     // backend.xgmi.push: K3 writes into the owners' inboxes
+    bool fail_setup_ = false;   // backend.xgmi.fail_setup (fault injection)
     std::string name_;
     XgmiShm* shm_ = nullptr;
     bool created_ = false;    // this worker (rank 0) created the segment

@@ -421,10 +421,13 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
 // there is no exponent to take from another frame (NeedsExtraBatch false,
 // ppp.cc:65-67; PostprocessSingle's INT32 branch, ppp.cc:262-298) — so one
 // pass in stream order decides and writes each frame: no claim pass over the
-// headers, no second walk in block order.  State: uint64[B + 3] per slice:
+// headers, no second walk in block order.  State: uint64[2B + 4] per slice:
 // [0, B) the rx bitmap, [B] the call sequence c of this slice, [B + 1] the
 // conflict count of the running call, [B + 2] the conflicts resolved in the
-// slice so far (a statistic: copies that arrived ahead of an earlier one).  A frame's tag is
+// slice so far (a statistic: copies that arrived ahead of an earlier one),
+// [B + 3] the length of the running call's dirty list, [B + 4, 2B + 4) that
+// list: the pkt_ids marked dirty in this call (appended by the claim that
+// sets a pkt_id's dirty bit), so the fix-up visits only them.  A frame's tag is
 //   (0xFFFFFFFF - c) << 32 | (0x7FFFFFFF - f) << 1      (bit 0: dirty),
 // larger for an earlier call and, within a call, for an earlier frame f, so
 // a 64-bit atomicMax on state[pkt_id] keeps the first copy of the stream,
@@ -440,7 +443,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
 //                      discard).
 // Which of two racing writes lands last is not ordered, so the fix-up
 // (k_rx_int32_fixup, same stream) rewrites every dirty pkt_id from its final
-// winner — the highest tag, the first copy — and then advances c.  Copies
+// winner — the highest tag, the first copy — and then advances c.  It walks
+// the dirty list (not all B state words for one conflict); a
+// list that overflowed its B entries (one pkt_id can be appended again when a
+// later claim's atomicMax clears its dirty bit for an instant) falls back to
+// the scan of every state word.  Copies
 // of one pkt_id are normally identical (retransmissions), but the rule holds
 // for any payloads.
 constexpr uint32_t kRxI32MaxFrames = 0x7FFFFFFFu;
@@ -521,8 +528,11 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_int32(RxArgs a) {
                     keep = true;
                 } else if ((old & ~1ull) < tag) {
                     write = true;
-                    atomicOr(a.state + pid, 1ull);
                     atomicAdd(conflicts, 1ull);
+                    if (!(atomicOr(a.state + pid, 1ull) & 1ull)) {   // this claim made it dirty: list it
+                        const unsigned long long i = atomicAdd(a.state + a.nblocks + 3, 1ull);
+                        if (i < a.nblocks) a.state[a.nblocks + 4 + i] = pid;
+                    }
                 }
             }
             if (!keep) disc++;
@@ -571,13 +581,39 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_int32(RxArgs a) {
 // first copy) and cleaned; then the conflict count is cleared and the call
 // sequence advanced (the slice's conflict total accumulates).  Without
 // conflicts (no copies claimed out of order) it only advances the sequence.
+// Rewrite dirty pkt_id k from the frame its tag names (the first copy), the
+// whole wave lane-strided over the block's words.
+__device__ __forceinline__ void rx_int32_rewrite(const RxArgs& a, uint32_t P, uint64_t k, unsigned long long s,
+                                                 int lane) {
+    const uint64_t f = kRxI32MaxFrames - ((uint32_t)s >> 1);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + f * a.stride + 52);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(a.out) + k * P;
+    const uint64_t valid = a.numel - k * P < P ? a.numel - k * P : P;
+    for (uint64_t i = lane; i < valid; i += kWave) dst[i] = bswap(src[i]);
+}
+
 __global__ __launch_bounds__(kBlockThreads) void k_rx_int32_fixup(RxArgs a, uint32_t P) {
     const unsigned long long n = a.state[a.nblocks + 1];
     const unsigned long long call = a.state[a.nblocks];
-    if (n) {
-        // each wave scans 64 state words at a time; the dirty ones (a ballot)
-        // are rewritten one after another by the whole wave, lane-strided
-        const int lane = threadIdx.x & (kWave - 1);
+    const unsigned long long listed = a.state[a.nblocks + 3];
+    const int lane = threadIdx.x & (kWave - 1);
+    if (n && listed <= a.nblocks) {
+        // the dirty list: one pkt_id per wave at a time (an id listed twice
+        // is rewritten twice with the same words; its bit cleared either way)
+        for (uint64_t i = wave_index(); i < listed; i += kWavesPerBlock) {
+            const uint64_t k = a.state[a.nblocks + 4 + i];
+            const unsigned long long s = a.state[k];
+            if (s & 1ull) rx_int32_rewrite(a, P, k, s, lane);
+        }
+        __syncthreads();   // every rewrite has read its state word before any is cleaned
+        for (uint64_t i = wave_index(); i < listed; i += kWavesPerBlock) {
+            const uint64_t k = a.state[a.nblocks + 4 + i];
+            if (lane == 0) a.state[k] &= ~1ull;
+        }
+    } else if (n) {
+        // the list overflowed: each wave scans 64 state words at a time; the
+        // dirty ones (a ballot) are rewritten one after another by the whole
+        // wave, lane-strided
         for (uint64_t k0 = (uint64_t)wave_index() * kWave; k0 < a.nblocks; k0 += kBlockThreads) {
             const uint64_t k = k0 + lane;
             const unsigned long long s = k < a.nblocks ? a.state[k] : 0ull;
@@ -585,13 +621,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_int32_fixup(RxArgs a, uint
             while (dirty) {
                 const int j = __builtin_ctzll(dirty);
                 dirty &= dirty - 1;
-                const uint64_t kd = k0 + j;
                 const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)s, j);
-                const uint64_t f = kRxI32MaxFrames - (lo >> 1);
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(a.frames + f * a.stride + 52);
-                uint32_t* dst = reinterpret_cast<uint32_t*>(a.out) + kd * P;
-                const uint64_t valid = a.numel - kd * P < P ? a.numel - kd * P : P;
-                for (uint64_t i = lane; i < valid; i += kWave) dst[i] = bswap(src[i]);
+                rx_int32_rewrite(a, P, k0 + j, lo, lane);
             }
             if (s & 1ull) a.state[k] = s & ~1ull;
         }
@@ -601,6 +632,7 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_int32_fixup(RxArgs a, uint
         if (n) {
             a.state[a.nblocks + 2] += n;
             a.state[a.nblocks + 1] = 0ull;
+            a.state[a.nblocks + 3] = 0ull;
         }
         a.state[a.nblocks] = call + 1;
     }
@@ -663,7 +695,7 @@ uint64_t sml_frame_bytes(uint32_t packet_numel) { return 52ull + 4ull * packet_n
 uint64_t sml_rx_state_words(uint64_t numel, uint32_t packet_numel, uint32_t batch_max, int int32) {
     if (!valid_packet(packet_numel)) return 0;
     const uint64_t B = sml_num_blocks(numel, packet_numel);
-    if (int32) return B + 3;
+    if (int32) return 2 * B + 4;   // bitmap, sequence, conflict counts, dirty list (k_rx_int32)
     const uint64_t w = B + (B < batch_max ? B : batch_max);
     return w ? w : 1;
 }

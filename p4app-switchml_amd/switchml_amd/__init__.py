@@ -660,12 +660,14 @@ def pack_frames_int32(x, params: FrameParams, packet_numel: int = 256, frames=No
 class RxSliceInt32:
     """Receive-side state of one INT32 job slice for unpack_frames_int32: the
     rx bitmap over its B pkt_ids plus the slice's call sequence, the running
-    call's conflict count and the slice's conflict total (uint64[B + 3]),
-    {accepted, discarded} counters, the output."""
+    call's conflict count, the slice's conflict total and the fix-up's dirty
+    list (uint64[2B + 4], sml_rx_state_words), {accepted, discarded}
+    counters, the output."""
 
     def __init__(self, numel: int, packet_numel: int = 256, device="cuda", out=None):
         torch = _torch()
         self.numel, self.packet_numel = numel, packet_numel
+        self.nblocks = num_blocks(numel, packet_numel)
         self.state = torch.zeros(int(lib().sml_rx_state_words(numel, packet_numel, 1, 1)), dtype=torch.int64,
                                  device=device)
         self.counts = torch.zeros(2, dtype=torch.int64, device=device)
@@ -675,7 +677,7 @@ class RxSliceInt32:
     def conflicts(self) -> int:
         """Copies of a pkt_id that claimed it ahead of an earlier copy and were
         resolved by the fix-up, over the slice so far (reads the device)."""
-        return int(self.state[-1].item())
+        return int(self.state[self.nblocks + 2].item())
 
     def reset(self, stream=None):
         """rte_bitmap_reset for a new job slice (sml_rx_reset)."""

@@ -67,7 +67,7 @@ def make_config(**kw) -> str:
                                                   "stall_worker_thread", "stall_ms")}
     hip = {k: v for k, v in kw.items() if k in ("device", "mode", "packet_ring", "burst_server", "batch_jobs",
                                                      "coalesce_us", "vcl")}
-    xgmi = {k: v for k, v in kw.items() if k in ("session", "max_slice_numel", "timeout_ms", "push")}
+    xgmi = {k: v for k, v in kw.items() if k in ("session", "max_slice_numel", "timeout_ms", "push", "fail_setup")}
     unknown = set(kw) - set(general) - set(dummy) - set(hip) - set(xgmi)
     if unknown:
         raise KeyError(f"unknown config keys {sorted(unknown)}")

@@ -228,3 +228,28 @@ def test_scale_report_efficiency_is_per_reading():
     lines[0]["strong_1GiB_value"] = None
     assert sr.efficiency(lines)["strong_1GiB_value"] == {}
     assert sr.efficiency(lines[1:]) == {"value": {}, "weak_256MiB_value": {}, "strong_1GiB_value": {}}
+
+
+def test_term_guard_prints_the_line_when_the_launcher_stops_the_ranks(tmp_path):
+    """N > 1 (first contact): torch.distributed.run SIGTERMs every
+    rank once one rank fails; bench.term_guard takes the signal on its own
+    thread while the main thread is blocked (here in a sleep, on a node in a
+    collective or a device sync), prints rank 0's line once and exits 1.
+    Before the line exists (on_term["emit"] unset) it just exits 1."""
+    import subprocess
+    prog = tmp_path / "p.py"
+    prog.write_text(
+        "import os, sys, threading, time, signal\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import bench\n"
+        "on = {'emit': None}\n"
+        "bench.term_guard(on)\n"
+        "if sys.argv[1] == 'line':\n"
+        "    on['emit'] = lambda: print('{\"metric\": \"m\", \"terminated\": true}', flush=True)\n"
+        "threading.Timer(0.5, lambda: os.kill(os.getpid(), signal.SIGTERM)).start()\n"
+        "time.sleep(30)\n"
+        "print('not reached', flush=True)\n")
+    for mode, want in (("line", '{"metric": "m", "terminated": true}'), ("early", "")):
+        p = subprocess.run([sys.executable, str(prog), mode], capture_output=True, text=True, timeout=60)
+        assert p.returncode == 1, (p.returncode, p.stderr[-500:])
+        assert p.stdout.strip() == want, p.stdout

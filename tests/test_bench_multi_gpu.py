@@ -181,3 +181,34 @@ def test_bench_n1_line(cuda, tmp_path):
             assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["value"] > 0 and cb["unit"].startswith("GB/s")
         elif "--graph-steps" in extra:
             assert "hipGraph" in line["config"]["launch"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_rehearsal_survives_a_failed_first_contact(cuda, tmp_path):
+    """DESIGN §6, first contact: one rank's in-node switch fails right after
+    joining its session (SML_BENCH_INJECT=xgmi_switch:1 ->
+    backend.xgmi.fail_setup), as a worker that cannot map a peer's plane on
+    the driver's first 8-GPU run would.  The ranks agree on the failure
+    collectively and move on: the line is printed, exit 0 (a path that could
+    not run is diagnostic), xgmi_switch reports its error and failed phase,
+    the other three switch paths are verified, and nothing waited out a
+    barrier timeout (the session was poisoned)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+           and not k.startswith("TORCHELASTIC_")}
+    env["SML_BENCH_REHEARSE"] = "1"
+    env["SML_BENCH_INJECT"] = "xgmi_switch:1"
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
+           "--switch-numel", "4194304", "--job-numel", "0", "--no-plugin", "--no-rccl-collnet"]
+    rc, out, err, wall = run_child(cmd, env, str(tmp_path), 500, "bench.py --gpus 2 (injected xgmi setup failure)")
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert lines, f"no JSON line (rc {rc}); stderr tail:\n{err}"
+    line = json.loads(lines[-1])
+    assert rc == 0, (rc, line.get("failures"), line.get("diagnostic_failures"), err[-1500:])
+    x = line["xgmi_switch"]
+    assert x["failed_phase"] == "setup" and ("injected setup failure" in x["error"] or "another rank" in x["error"]), x
+    for k in ("switchsim", "p2p_switch", "xgmi_switch_push"):
+        assert line[k].get("verified") is True, (k, line[k])
+    assert any(d.startswith("xgmi_switch:") for d in line["diagnostic_failures"]), line["diagnostic_failures"]
+    assert wall < 300, wall

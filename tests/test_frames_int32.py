@@ -117,10 +117,10 @@ def test_rx_state_words():
     L = sw.lib()
     for n, P, bm in [(0, 256, 64), (1, 64, 64), (20_011, 256, 64), (3 * 1024, 1024, 2), (10 ** 9 + 7, 128, 512)]:
         B = O.num_blocks(n, P)
-        assert L.sml_rx_state_words(n, P, bm, 1) == B + 3
+        assert L.sml_rx_state_words(n, P, bm, 1) == 2 * B + 4        # + the fix-up's dirty list
         assert L.sml_rx_state_words(n, P, bm, 0) == max(1, B + min(B, bm))
     assert L.sml_rx_state_words(1000, 100, 64, 0) == 0          # unsupported packet size
-    assert sw.RxSliceInt32(20_011, 256, device="cpu").state.numel() == O.num_blocks(20_011, 256) + 3
+    assert sw.RxSliceInt32(20_011, 256, device="cpu").state.numel() == 2 * O.num_blocks(20_011, 256) + 4
 
 
 # ---------------------------------------------------------------- GPU --
@@ -360,14 +360,18 @@ def claim_tag(call, f):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("overflow", [False, True])
 @pytest.mark.parametrize("P", [64, 256, 1024])
-def test_int32_rx_fixup_rewrites_displaced_claims(cuda, P):
+def test_int32_rx_fixup_rewrites_displaced_claims(cuda, P, overflow):
     """The fix-up path, white box: before the call, some pkt_ids hold the
     claim tag of a LATER frame of this call (as when a later copy wins the
     race to the atomic) and their output words hold that copy's garbage.  The
     real (earlier) frames must displace those claims, mark them dirty, and
     the fix-up must leave the earlier frames' words, clean state words, the
-    conflict count in the slice total, and the call sequence advanced."""
+    conflict count in the slice total, and the call sequence advanced.  The
+    fix-up visits the call's dirty list (state[B + 4 ...], ADVICE r5);
+    overflow=True plants a full list first, so every append is dropped and
+    the fix-up takes its fallback, the scan of all B state words."""
     import torch
     import switchml_amd as sw
     n = 40_000 + 7
@@ -383,6 +387,8 @@ def test_int32_rx_fixup_rewrites_displaced_claims(cuda, P):
     st = rx.state.cpu().numpy()
     for k in stolen:                                    # frame k's later twin (index B + k) claimed k first
         st[k] = claim_tag(0, B + int(k))
+    if overflow:
+        st[B + 3] = B                                   # the list is full: the fix-up must scan
     rx.state.copy_(torch.from_numpy(st))
     rx.out.fill_(-1)
     sw.unpack_frames_int32(torch.from_numpy(frames).to(cuda), B, rx, job_id=4)
@@ -390,7 +396,9 @@ def test_int32_rx_fixup_rewrites_displaced_claims(cuda, P):
     assert np.array_equal(rx.out.cpu().numpy(), x)
     st = rx.state.cpu().numpy()
     assert not (st[:B] & 1).any()
-    assert [int(v) for v in st[B:]] == [1, 0, len(stolen)]
+    assert [int(v) for v in st[B:B + 4]] == [1, 0, len(stolen), 0]   # sequence, conflicts, total, list length
+    if not overflow:                                    # each displaced pkt_id listed once, in some order
+        assert sorted(int(v) for v in st[B + 4:B + 4 + len(stolen)]) == [int(k) for k in stolen]
     assert rx.conflicts == len(stolen)
     # displaced claims count as the discards (their twins were counted accepted)
     assert rx.counts.cpu().tolist() == [B - len(stolen), len(stolen)]
@@ -527,7 +535,7 @@ def test_int32_rx_random_streams(cuda):
             torch.cuda.synchronize()
             assert np.array_equal(rx.out.cpu().numpy(), ref), (n, P, lo, hi)
             assert rx.counts.cpu().tolist() == [acc, dis], (n, P, lo, hi)
-        assert int(rx.state[-3].item()) == len(bounds) - 1          # call sequence
+        assert int(rx.state[O.num_blocks(n, P)].item()) == len(bounds) - 1          # call sequence
     check()
 
 

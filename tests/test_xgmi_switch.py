@@ -304,3 +304,42 @@ def test_xgmi_stalled_device_fails_slice_within_timeout(cuda, W):
         # reported within ~timeout_ms (a few bounded waits at most), long before the stall ends
         assert res["seconds"][0] < 2.0 and res["seconds"][1] < 1.0, allres
         assert res["after_ok"], allres
+
+
+def _setup_failing_worker(rank, W, init, session, fail_rank):
+    """Worker `fail_rank` fails right after joining the session
+    (backend.xgmi.fail_setup: what a worker that cannot map a peer's plane
+    on its first contact with another GPU does).  It must poison the session
+    (first contact): the other workers' Context starts, but their
+    first job fails at once — not after backend.xgmi.timeout_ms at a barrier
+    the failed worker never reaches — and their Stop does not wait either."""
+    import time
+    from switchml_amd import client as C
+    t0 = time.time()
+    try:
+        C.start(C.make_config(backend="xgmi", rank=rank, num_workers=W, num_worker_threads=1, packet_numel=256,
+                              max_outstanding_packets=64, mode="bulk", bandwidth=0, device=0, session=session,
+                              timeout_ms=30000, fail_setup=rank == fail_rank))
+    except C.ContextError as e:
+        return {"started": False, "error": str(e), "seconds": time.time() - t0}
+    x = torch.from_numpy(worker_bucket(rank, 100_000, 1)).cuda()
+    job = C.allreduce_async(x)
+    try:
+        C.wait_for_all_jobs()
+    except C.ContextError:
+        pass
+    st = job.status()
+    C.stop()
+    return {"started": True, "status": st, "seconds": time.time() - t0}
+
+
+@pytest.mark.gpu
+def test_xgmi_setup_failure_poisons_session(cuda):
+    from switchml_amd import client as C
+    session = "setupfail-" + uuid.uuid4().hex
+    out = {rank: res for rank, res, err in _run(_setup_failing_worker, 2, (session, 1), timeout=120)}
+    assert set(out) == {0, 1} and all(v is not None for v in out.values()), out
+    assert out[1]["started"] is False and "injected setup failure" in out[1]["error"], out
+    assert out[0]["started"] is True and out[0]["status"] == C.JOB_FAILED, out
+    assert max(v["seconds"] for v in out.values()) < 20, out      # no 30 s barrier timeout waited out
+    assert not os.path.exists(f"/dev/shm/switchml-{session}")
