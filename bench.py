@@ -511,6 +511,15 @@ def main():
         def on_timeout():
             diag_failures.append(f"timeout: the multi-GPU diagnostic phase exceeded {args.exchange_timeout:g} s")
             try:
+                # where every thread of this rank is stuck (to stderr; the
+                # driver's record keeps it): the call a hang sits in
+                import faulthandler
+                sys.stderr.write(f"[bench rank {rank}] watchdog: stacks at the timeout\n")
+                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                sys.stderr.flush()
+            except Exception:  # noqa: BLE001 - diagnostics only
+                pass
+            try:
                 emit()
             finally:
                 os._exit(1 if failures else 0)

@@ -335,7 +335,7 @@ uint64_t sml_frame_bytes(uint32_t packet_numel);
 
 /* Words of the per-slice rx state (d_state) a receive call needs: FLOAT32
  * (sml_dequantize_frames) max(1, B + b) with b = min(batch_max, B); INT32
- * (sml_unpack_frames_int32, int32 != 0) 2B + 4.  B = ceil(numel / P). */
+ * (sml_unpack_frames_int32, int32 != 0) 2B + 6.  B = ceil(numel / P). */
 uint64_t sml_rx_state_words(uint64_t numel, uint32_t packet_numel, uint32_t batch_max, int int32);
 
 /* Fused K1 -> frames: quantize + pack one job slice straight into B + b
@@ -394,21 +394,22 @@ sml_status_t sml_pack_frames_int32(const int32_t* d_in, uint64_t numel, uint32_t
  * sml_dequantize_frames (this job, a pkt_id < B not received before, the
  * first copy wins), and PostprocessSingle's INT32 branch (ppp.cc:262-298):
  * ntohl of the accepted frame's words into d_out[pkt_id*P ..
- * pkt_id*P + min(P, numel - pkt_id*P)).  d_state: uint64[2B + 4] (the rx
- * bitmap, the slice's call sequence, the running call's conflict count, the
- * slice's count of copies that claimed ahead of an earlier copy, and the
- * running call's list of those pkt_ids: its length, then up to B entries),
+ * pkt_id*P + min(P, numel - pkt_id*P)).  d_state: uint64[2B + 6] (the rx
+ * bitmap, the slice's call sequence, the slice's count of copies that
+ * claimed ahead of an earlier copy, two alternating slots of a call's
+ * conflict count and dirty-list length, then up to B listed pkt_ids),
  * zeroed per slice (sml_rx_reset), persists across calls; d_counts as for
  * sml_dequantize_frames.  One pass in stream order over the frames (an INT32
- * frame needs no other frame) plus a one-workgroup fix-up that rewrites the
- * listed pkt_ids only (all B state words if the list overflowed), on `stream`;
+ * frame needs no other frame) plus a fix-up over a grid of workgroups that
+ * rewrites the listed pkt_ids only (all B state words if the list
+ * overflowed), on `stream`;
  * num_frames < 2^31 per call, fewer than 2^32 - 1 calls per slice. */
 sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, uint64_t frame_stride,
                                      uint64_t numel, uint32_t packet_numel, uint64_t job_id,
                                      uint64_t* d_state, int32_t* d_out, uint64_t* d_counts, void* stream);
 
 /* rte_bitmap_reset for one slice (dpdk_worker_thread.cc, per job slice):
- * zero d_state (uint64[B + b]; for INT32 slices uint64[2B + 4]) before the
+ * zero d_state (uint64[B + b]; for INT32 slices uint64[2B + 6]) before the
  * slice's first sml_dequantize_frames / sml_unpack_frames_int32
  * call.  One async memset on `stream`. */
 sml_status_t sml_rx_reset(uint64_t* d_state, uint64_t num_words, void* stream);

@@ -220,11 +220,29 @@ void XgmiSwitch::Setup(int device) {
         sp.published.store(1, std::memory_order_release);
     }
     Barrier(kMaxT);   // every worker's handles are published
+    // The outcome of this worker's setup is held back until every worker has
+    // imported (or failed to import) every peer's planes: a worker that
+    // failed must not free its exported planes while a peer is still inside
+    // hipIpcOpenMemHandle on them — the importer then hangs in the runtime
+    // (measured on MI355X, the N = 8 first-contact rehearsal: > 90 s).
+    std::string err;
     if (shm_->W != (uint32_t)W_ || shm_->T != (uint32_t)T_ || shm_->P != P_ || shm_->cap != cap_ ||
         shm_->push != (push_ ? 1u : 0u))
-        throw SwitchMLFatal("xgmi switch: workers disagree on num_workers / num_worker_threads / packet_numel / "
-                            "max_slice_numel / push");
-    if (fail_setup_) throw SwitchMLFatal("xgmi switch: injected setup failure (backend.xgmi.fail_setup)");
+        err = "workers disagree on num_workers / num_worker_threads / packet_numel / max_slice_numel / push";
+    else if (fail_setup_)
+        err = "injected setup failure (backend.xgmi.fail_setup)";
+    else
+        try {
+            OpenPeers();
+        } catch (const std::exception& e) {
+            err = e.what();
+        }
+    Barrier(kMaxT);   // every worker is done importing
+    if (!err.empty()) throw SwitchMLFatal(err.rfind("xgmi switch: ", 0) == 0 ? err : "xgmi switch: " + err);
+}
+
+// Map every peer's planes of every worker thread (hipIpc; over xGMI on a node).
+void XgmiSwitch::OpenPeers() {
     for (int t = 0; t < T_; t++) {
         ThreadPlanes& tp = planes_[t];
         tp.peer_exps.resize(W_);

@@ -122,6 +122,7 @@ class XgmiSwitch {
 
     void OpenSegment();
     void Setup(int device);
+    void OpenPeers();
     void Release();
     void Barrier(int index);
     // Wait for the work queued on `st`, polling against backend.xgmi.timeout_ms

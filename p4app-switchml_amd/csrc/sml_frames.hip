@@ -421,13 +421,17 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
 // there is no exponent to take from another frame (NeedsExtraBatch false,
 // ppp.cc:65-67; PostprocessSingle's INT32 branch, ppp.cc:262-298) — so one
 // pass in stream order decides and writes each frame: no claim pass over the
-// headers, no second walk in block order.  State: uint64[2B + 4] per slice:
+// headers, no second walk in block order.  State: uint64[2B + 6] per slice:
 // [0, B) the rx bitmap, [B] the call sequence c of this slice, [B + 1] the
-// conflict count of the running call, [B + 2] the conflicts resolved in the
-// slice so far (a statistic: copies that arrived ahead of an earlier one),
-// [B + 3] the length of the running call's dirty list, [B + 4, 2B + 4) that
-// list: the pkt_ids marked dirty in this call (appended by the claim that
-// sets a pkt_id's dirty bit), so the fix-up visits only them.  A frame's tag is
+// conflicts resolved in the slice so far (a statistic: copies that arrived
+// ahead of an earlier one), [B + 2 + (c & 1)] the conflict count of call c,
+// [B + 4 + (c & 1)] the length of call c's dirty list, [B + 6, 2B + 6) that
+// list: the pkt_ids marked dirty in call c (appended by the claim that sets
+// a pkt_id's dirty bit), so the fix-up visits only them.  The per-call
+// counters alternate between two slots so that the fix-up's workgroups can
+// all read call c's without a grid-wide barrier: the fix-up of call c clears
+// the OTHER slot (call c - 1's, whose fix-up has ended), ready for c + 1.
+// A frame's tag is
 //   (0xFFFFFFFF - c) << 32 | (0x7FFFFFFF - f) << 1      (bit 0: dirty),
 // larger for an earlier call and, within a call, for an earlier frame f, so
 // a 64-bit atomicMax on state[pkt_id] keeps the first copy of the stream,
@@ -444,13 +448,15 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_apply(RxArgs a) {
 // Which of two racing writes lands last is not ordered, so the fix-up
 // (k_rx_int32_fixup, same stream) rewrites every dirty pkt_id from its final
 // winner — the highest tag, the first copy — and then advances c.  It walks
-// the dirty list (not all B state words for one conflict); a
-// list that overflowed its B entries (one pkt_id can be appended again when a
-// later claim's atomicMax clears its dirty bit for an instant) falls back to
-// the scan of every state word.  Copies
+// the dirty list over a grid of workgroups (not one workgroup
+// scanning all B state words for one conflict); a list that overflowed its
+// B entries (one pkt_id can be appended again when a later claim's
+// atomicMax clears its dirty bit for an instant) falls back to the scan of
+// every state word, over the same grid.  Copies
 // of one pkt_id are normally identical (retransmissions), but the rule holds
 // for any payloads.
 constexpr uint32_t kRxI32MaxFrames = 0x7FFFFFFFu;
+constexpr uint32_t kRxFixupBlocks = 128;   // k_rx_int32_fixup's grid
 
 __host__ __device__ constexpr int rx_int32_slices(int P) { return P / 256 > 4 ? P / 256 : 4; }
 
@@ -504,7 +510,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_int32(RxArgs a) {
     const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint64_t ntiles = (a.nframes + kF - 1) / kF;
     const uint32_t call = (uint32_t)a.state[a.nblocks];
-    unsigned long long* const conflicts = a.state + a.nblocks + 1;
+    unsigned long long* const conflicts = a.state + a.nblocks + 2 + (call & 1u);
+    unsigned long long* const listed = a.state + a.nblocks + 4 + (call & 1u);
     uint32_t disc = 0;
     uint64_t t = xcd_block(a.xcd) * kWavesPerBlock + wave_index();
     RxI32Tile<P> cur, nxt;
@@ -530,8 +537,8 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_int32(RxArgs a) {
                     write = true;
                     atomicAdd(conflicts, 1ull);
                     if (!(atomicOr(a.state + pid, 1ull) & 1ull)) {   // this claim made it dirty: list it
-                        const unsigned long long i = atomicAdd(a.state + a.nblocks + 3, 1ull);
-                        if (i < a.nblocks) a.state[a.nblocks + 4 + i] = pid;
+                        const unsigned long long i = atomicAdd(listed, 1ull);
+                        if (i < a.nblocks) a.state[a.nblocks + 6 + i] = pid;
                     }
                 }
             }
@@ -576,11 +583,6 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_int32(RxArgs a) {
     }
 }
 
-// One workgroup, after k_rx_int32 on the same stream: with conflicts in this
-// call, every dirty pkt_id is rewritten from the frame its tag names (the
-// first copy) and cleaned; then the conflict count is cleared and the call
-// sequence advanced (the slice's conflict total accumulates).  Without
-// conflicts (no copies claimed out of order) it only advances the sequence.
 // Rewrite dirty pkt_id k from the frame its tag names (the first copy), the
 // whole wave lane-strided over the block's words.
 __device__ __forceinline__ void rx_int32_rewrite(const RxArgs& a, uint32_t P, uint64_t k, unsigned long long s,
@@ -592,29 +594,36 @@ __device__ __forceinline__ void rx_int32_rewrite(const RxArgs& a, uint32_t P, ui
     for (uint64_t i = lane; i < valid; i += kWave) dst[i] = bswap(src[i]);
 }
 
+// kRxFixupBlocks workgroups, after k_rx_int32 on the same stream: with
+// conflicts in this call, every dirty pkt_id is rewritten from the frame its
+// tag names (the first copy) and cleaned; the slice's conflict total
+// accumulates, the other counter slot is cleared and the call sequence
+// advanced.  Without conflicts (no copies claimed out of order) it only does
+// the last three.
 __global__ __launch_bounds__(kBlockThreads) void k_rx_int32_fixup(RxArgs a, uint32_t P) {
-    const unsigned long long n = a.state[a.nblocks + 1];
     const unsigned long long call = a.state[a.nblocks];
-    const unsigned long long listed = a.state[a.nblocks + 3];
+    const uint32_t slot = (uint32_t)call & 1u;
+    const unsigned long long n = a.state[a.nblocks + 2 + slot];
+    const unsigned long long listed = a.state[a.nblocks + 4 + slot];
     const int lane = threadIdx.x & (kWave - 1);
+    const uint64_t wave = (uint64_t)blockIdx.x * kWavesPerBlock + wave_index();
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerBlock;
     if (n && listed <= a.nblocks) {
-        // the dirty list: one pkt_id per wave at a time (an id listed twice
-        // is rewritten twice with the same words; its bit cleared either way)
-        for (uint64_t i = wave_index(); i < listed; i += kWavesPerBlock) {
-            const uint64_t k = a.state[a.nblocks + 4 + i];
+        // the dirty list, one pkt_id per wave at a time; the wave that finds
+        // the bit set rewrites the block, then cleans the bit (an id listed
+        // twice is rewritten twice with the same words, or found clean)
+        for (uint64_t i = wave; i < listed; i += nwaves) {
+            const uint64_t k = a.state[a.nblocks + 6 + i];
             const unsigned long long s = a.state[k];
-            if (s & 1ull) rx_int32_rewrite(a, P, k, s, lane);
-        }
-        __syncthreads();   // every rewrite has read its state word before any is cleaned
-        for (uint64_t i = wave_index(); i < listed; i += kWavesPerBlock) {
-            const uint64_t k = a.state[a.nblocks + 4 + i];
-            if (lane == 0) a.state[k] &= ~1ull;
+            if (s & 1ull) {
+                rx_int32_rewrite(a, P, k, s, lane);
+                if (lane == 0) a.state[k] = s & ~1ull;
+            }
         }
     } else if (n) {
-        // the list overflowed: each wave scans 64 state words at a time; the
-        // dirty ones (a ballot) are rewritten one after another by the whole
-        // wave, lane-strided
-        for (uint64_t k0 = (uint64_t)wave_index() * kWave; k0 < a.nblocks; k0 += kBlockThreads) {
+        // the list overflowed: every state word, 64 per wave at a time; the
+        // dirty ones (a ballot) rewritten one after another by the whole wave
+        for (uint64_t k0 = wave * kWave; k0 < a.nblocks; k0 += nwaves * kWave) {
             const uint64_t k = k0 + lane;
             const unsigned long long s = k < a.nblocks ? a.state[k] : 0ull;
             unsigned long long dirty = __ballot((s & 1ull) != 0);
@@ -627,13 +636,14 @@ __global__ __launch_bounds__(kBlockThreads) void k_rx_int32_fixup(RxArgs a, uint
             if (s & 1ull) a.state[k] = s & ~1ull;
         }
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (n) {
-            a.state[a.nblocks + 2] += n;
-            a.state[a.nblocks + 1] = 0ull;
-            a.state[a.nblocks + 3] = 0ull;
-        }
+    // one thread of the grid: the slice's total, the other slot cleared (call
+    // c - 1's: its fix-up has ended) for call c + 1, the sequence advanced.
+    // No workgroup of this launch reads those words after its start, and the
+    // next rx call runs after the whole launch (stream order).
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (n) a.state[a.nblocks + 1] += n;
+        a.state[a.nblocks + 2 + (slot ^ 1u)] = 0ull;
+        a.state[a.nblocks + 4 + (slot ^ 1u)] = 0ull;
         a.state[a.nblocks] = call + 1;
     }
 }
@@ -695,7 +705,7 @@ uint64_t sml_frame_bytes(uint32_t packet_numel) { return 52ull + 4ull * packet_n
 uint64_t sml_rx_state_words(uint64_t numel, uint32_t packet_numel, uint32_t batch_max, int int32) {
     if (!valid_packet(packet_numel)) return 0;
     const uint64_t B = sml_num_blocks(numel, packet_numel);
-    if (int32) return 2 * B + 4;   // bitmap, sequence, conflict counts, dirty list (k_rx_int32)
+    if (int32) return 2 * B + 6;   // bitmap, sequence, conflict counts, dirty list (k_rx_int32)
     const uint64_t w = B + (B < batch_max ? B : batch_max);
     return w ? w : 1;
 }
@@ -868,7 +878,9 @@ sml_status_t sml_unpack_frames_int32(const void* frames, uint64_t num_frames, ui
     const dim3 grid(grid_for_tiles((num_frames + frames_per_tile - 1) / frames_per_tile));
     if (4 * numel >= g_nt_threshold.load(std::memory_order_relaxed)) launch_rx_int32_nt<true>(P, grid, st, a);
     else launch_rx_int32_nt<false>(P, grid, st, a);
-    k_rx_int32_fixup<<<1, kBlockThreads, 0, st>>>(a, P);
+    // a grid that spreads a call's dirty pkt_ids over the chip; with no
+    // conflict its workgroups read two words and end
+    k_rx_int32_fixup<<<kRxFixupBlocks, kBlockThreads, 0, st>>>(a, P);
     return launch_check();
 }
 

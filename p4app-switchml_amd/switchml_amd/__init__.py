@@ -661,7 +661,7 @@ class RxSliceInt32:
     """Receive-side state of one INT32 job slice for unpack_frames_int32: the
     rx bitmap over its B pkt_ids plus the slice's call sequence, the running
     call's conflict count, the slice's conflict total and the fix-up's dirty
-    list (uint64[2B + 4], sml_rx_state_words), {accepted, discarded}
+    list (uint64[2B + 6], sml_rx_state_words), {accepted, discarded}
     counters, the output."""
 
     def __init__(self, numel: int, packet_numel: int = 256, device="cuda", out=None):
@@ -677,7 +677,7 @@ class RxSliceInt32:
     def conflicts(self) -> int:
         """Copies of a pkt_id that claimed it ahead of an earlier copy and were
         resolved by the fix-up, over the slice so far (reads the device)."""
-        return int(self.state[self.nblocks + 2].item())
+        return int(self.state[self.nblocks + 1].item())
 
     def reset(self, stream=None):
         """rte_bitmap_reset for a new job slice (sml_rx_reset)."""

@@ -117,10 +117,10 @@ def test_rx_state_words():
     L = sw.lib()
     for n, P, bm in [(0, 256, 64), (1, 64, 64), (20_011, 256, 64), (3 * 1024, 1024, 2), (10 ** 9 + 7, 128, 512)]:
         B = O.num_blocks(n, P)
-        assert L.sml_rx_state_words(n, P, bm, 1) == 2 * B + 4        # + the fix-up's dirty list
+        assert L.sml_rx_state_words(n, P, bm, 1) == 2 * B + 6        # + the fix-up's dirty list
         assert L.sml_rx_state_words(n, P, bm, 0) == max(1, B + min(B, bm))
     assert L.sml_rx_state_words(1000, 100, 64, 0) == 0          # unsupported packet size
-    assert sw.RxSliceInt32(20_011, 256, device="cpu").state.numel() == 2 * O.num_blocks(20_011, 256) + 4
+    assert sw.RxSliceInt32(20_011, 256, device="cpu").state.numel() == 2 * O.num_blocks(20_011, 256) + 6
 
 
 # ---------------------------------------------------------------- GPU --
@@ -270,7 +270,7 @@ def test_int32_rx_first_copy_wins_over_racing_copies(cuda, P, n, pairs):
     assert bad.size == 0, (bad.size, bad[:8].tolist())
     assert rx.counts.cpu().tolist() == [acc, dis] and acc == B and dis == pairs
     st = rx.state.cpu().numpy()
-    assert st[B] == 1 and st[B + 1] == 0                      # call sequence advanced, conflicts cleared
+    assert st[B] == 1 and st[B + 3] == 0 and st[B + 5] == 0   # call sequence advanced, call 1's slot clear
     assert not (st[:B] & 1).any()                              # no dirty pkt_id left
     print(f"P={P}: {rx.conflicts} of {pairs} copies claimed ahead of an earlier copy")
 
@@ -388,7 +388,7 @@ def test_int32_rx_fixup_rewrites_displaced_claims(cuda, P, overflow):
     for k in stolen:                                    # frame k's later twin (index B + k) claimed k first
         st[k] = claim_tag(0, B + int(k))
     if overflow:
-        st[B + 3] = B                                   # the list is full: the fix-up must scan
+        st[B + 4] = B                                   # call 0's list is full: the fix-up must scan
     rx.state.copy_(torch.from_numpy(st))
     rx.out.fill_(-1)
     sw.unpack_frames_int32(torch.from_numpy(frames).to(cuda), B, rx, job_id=4)
@@ -396,9 +396,12 @@ def test_int32_rx_fixup_rewrites_displaced_claims(cuda, P, overflow):
     assert np.array_equal(rx.out.cpu().numpy(), x)
     st = rx.state.cpu().numpy()
     assert not (st[:B] & 1).any()
-    assert [int(v) for v in st[B:B + 4]] == [1, 0, len(stolen), 0]   # sequence, conflicts, total, list length
+    # sequence, slice total, call 0's conflict count and list length (left:
+    # the next fix-up clears them), call 1's (cleared)
+    assert [int(v) for v in st[B:B + 6]] == [1, len(stolen), len(stolen), 0,
+                                             B + len(stolen) if overflow else len(stolen), 0]
     if not overflow:                                    # each displaced pkt_id listed once, in some order
-        assert sorted(int(v) for v in st[B + 4:B + 4 + len(stolen)]) == [int(k) for k in stolen]
+        assert sorted(int(v) for v in st[B + 6:B + 6 + len(stolen)]) == [int(k) for k in stolen]
     assert rx.conflicts == len(stolen)
     # displaced claims count as the discards (their twins were counted accepted)
     assert rx.counts.cpu().tolist() == [B - len(stolen), len(stolen)]
