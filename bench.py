@@ -396,18 +396,40 @@ def main():
     side, fields, extra = {}, {}, {}
 
     emit_lock, emitted = threading.Lock(), [False]
+    # N > 1: the launcher's store (torch.distributed.run hosts it in its
+    # agent, so it outlives any rank) holds a one-shot token; whichever rank
+    # takes it prints the line
+    store = dist.distributed_c10d._get_default_store() if world > 1 else None
 
-    def emit():
-        """Rank 0's one JSON line, from whatever has been measured so far —
+    def take_token():
+        """Every printing path takes it (rank 0's normal end and watchdog
+        too), so a rank SIGTERMed after rank 0 printed stays silent."""
+        if store is None:
+            return True
+        try:
+            import datetime
+            store.set_timeout(datetime.timedelta(seconds=20))   # the end of the run: never wait long
+            return int(store.add("sml_bench_line_token", 1)) == 1
+        except Exception:  # noqa: BLE001 - no store: rank 0 alone prints
+            return rank == 0
+
+    def emit(any_rank=False):
+        """The run's one JSON line, from whatever has been measured so far —
         exactly once, whichever of the normal end, the watchdog or the
-        launcher's SIGTERM (term_guard) comes first."""
-        if rank != 0:
+        launcher's SIGTERM (term_guard) comes first.  Rank 0 prints it; on
+        SIGTERM (another rank died) any surviving rank may, the store's token
+        deciding which — so a fault that kills rank 0 itself on its first
+        peer access does not lose the line (every rank holds the same
+        all-reduced readings and switch fields; only `side.topology` is
+        rank 0's)."""
+        if rank != 0 and not any_rank:
             return
         with emit_lock:
             if emitted[0]:
                 return
             emitted[0] = True
-            emit_line()
+            if take_token():
+                emit_line()
 
     def emit_line():
         ms_per_step = elapsed * 1e3 / args.steps
@@ -490,8 +512,9 @@ def main():
 
     def on_sigterm():
         diag_failures.append("terminated: SIGTERM from the launcher (another rank failed or the run was stopped) "
-                             "during the multi-GPU diagnostic phase; the fields above are what was measured")
-        emit()
+                             "during the multi-GPU diagnostic phase; the fields above are what was measured"
+                             + ("" if rank == 0 else f" (line printed by rank {rank})"))
+        emit(any_rank=True)
     on_term["emit"] = on_sigterm
 
     def guarded(key, fn):
@@ -539,6 +562,13 @@ def main():
                 "devices": ndev, "name": torch.cuda.get_device_name(dev),
                 "peer_access": [[i == j or torch.cuda.can_device_access_peer(i, j) for j in range(ndev)]
                                 for i in range(ndev)]})
+    if world > 1 and os.environ.get("SML_BENCH_INJECT", "") == f"die:{rank}":
+        # tests only: this rank dies at the start of the diagnostic phase, as
+        # one that faults on its first peer access would (the launcher then
+        # SIGTERMs the others: term_guard)
+        sys.stderr.write(f"[bench rank {rank}] SML_BENCH_INJECT: dying\n")
+        sys.stderr.flush()
+        os._exit(7)
     if world > 1 and args.switch_numel:
         try:
             fields.update(exchange_measure(sw, torch, dist, args.switch_numel, P, world, rank, dev,

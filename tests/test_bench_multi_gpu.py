@@ -214,3 +214,36 @@ def test_bench_rehearsal_survives_a_failed_first_contact(cuda, tmp_path):
         assert line[k].get("verified") is True, (k, line[k])
     assert any(d.startswith("xgmi_switch:") for d in line["diagnostic_failures"]), line["diagnostic_failures"]
     assert wall < 150, wall
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dying", [0, 1])
+def test_bench_line_survives_a_dead_rank(cuda, tmp_path, dying):
+    """DESIGN §6, first contact: a rank that DIES in the diagnostic phase (a
+    fault on its first peer access; here SML_BENCH_INJECT=die:<rank>,
+    os._exit(7) at the phase's start).  The driver's launcher,
+    torch.distributed.run, then SIGTERMs the surviving ranks; bench.term_guard
+    takes the signal on its own thread and the rank holding the store's token
+    prints the line — rank 0, or rank 1 when rank 0 is the one that died —
+    with the measured, self-checked headline and a "terminated" diagnostic.
+    The run's exit status is the failure's (non-zero), but the line is there."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+           and not k.startswith("TORCHELASTIC_")}
+    env["SML_BENCH_REHEARSE"] = "1"
+    env["SML_BENCH_INJECT"] = f"die:{dying}"
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2", "--job-numel", "0",
+            "--switch-numel", "4194304", "--no-rccl-collnet", "--exchange-timeout", "200"]
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(rendezvous_port()), *args]
+    rc, out, err, wall = run_child(cmd, env, str(tmp_path), 500, f"bench.py --gpus 2 (rank {dying} dies)")
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, (rc, lines, err[-2000:])
+    line = json.loads(lines[0])
+    assert rc != 0
+    assert line["self_check"] is True and line["value"] > 0 and line["n_gpus"] == 2
+    term = [d for d in line.get("diagnostic_failures", []) if d.startswith("terminated")]
+    assert term, (line.get("diagnostic_failures"), err[-2000:])
+    assert ("printed by rank 1" in term[0]) == (dying == 0), term
+    assert wall < 150, wall      # SIGTERM answered at once, not after the watchdog or the SIGKILL grace
