@@ -247,3 +247,18 @@ def test_bench_line_survives_a_dead_rank(cuda, tmp_path, dying):
     assert term, (line.get("diagnostic_failures"), err[-2000:])
     assert ("printed by rank 1" in term[0]) == (dying == 0), term
     assert wall < 150, wall      # SIGTERM answered at once, not after the watchdog or the SIGKILL grace
+
+
+def test_rendezvous_port_is_below_the_ephemeral_range():
+    """the driver-form rehearsal's --master-port is never an
+    ephemeral port (no outgoing connection can be handed it between the pick
+    and torchrun's bind) and is free when picked."""
+    import socket
+    with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+        lo = int(f.read().split()[0])
+    for _ in range(5):
+        p = rendezvous_port()
+        assert 1024 < p < max(lo, 2048), (p, lo)
+        with socket.socket() as s:
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            s.bind(("127.0.0.1", p))
