@@ -98,6 +98,18 @@ def test_config_validation(ctx):
     C.start(C.make_config(prepostprocessor="bypass", vcl=True, bandwidth=0))
     assert "vcl = true" in C.config_text()
     C.stop()
+    # the fault-injection keys (round 6): a stalled worker stream, a failed xgmi setup — off by default
+    C.start(C.make_config(prepostprocessor="bypass", bandwidth=0))
+    t = C.config_text()
+    assert "stall_worker_thread = -1" in t and "stall_ms = 0" in t and "fail_setup = false" in t
+    C.stop()
+    C.start(C.make_config(prepostprocessor="bypass", bandwidth=0, stall_worker_thread=1, stall_ms=250,
+                          fail_setup=True))
+    t = C.config_text()
+    assert "stall_worker_thread = 1" in t and "stall_ms = 250" in t and "fail_setup = true" in t
+    C.stop()
+    with pytest.raises(C.ContextError):                    # at most 60 s of injected stall
+        C.start(C.make_config(prepostprocessor="bypass", bandwidth=0, stall_ms=60001))
     for bad in (dict(prepostprocessor="nope"), dict(backend="dpdk"), dict(mode="turbo"),
                 dict(num_worker_threads=8, max_outstanding_packets=4)):
         kw = dict(prepostprocessor="bypass", bandwidth=0)
